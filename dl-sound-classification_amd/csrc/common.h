@@ -1,0 +1,127 @@
+// Shared device/host helpers for libmiaudio (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <math.h>
+
+#include "../../include/miaudio.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define MIA_LDS __attribute__((address_space(3)))
+
+// ---------------------------------------------------------------- error handling
+namespace mia {
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+}  // namespace mia
+
+#define MIA_CHECK_ARG(cond, ...)                       \
+  do {                                                 \
+    if (!(cond)) return mia::fail(-22, __VA_ARGS__);   \
+  } while (0)
+
+#define MIA_LAUNCH_CHECK(what)                                                   \
+  do {                                                                           \
+    hipError_t e__ = hipGetLastError();                                          \
+    if (e__ != hipSuccess)                                                       \
+      return mia::fail(-(int)e__, "%s: launch failed: %s", what, hipGetErrorString(e__)); \
+  } while (0)
+
+static inline hipStream_t as_stream(mia_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+template <typename T> __device__ __forceinline__ float to_f(T x);
+template <> __device__ __forceinline__ float to_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ float to_f<bf16>(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// dtype-dispatched scalar load/store on raw pointers
+__device__ __forceinline__ float ld_elem(const void* p, int dtype, int64_t i) {
+  return dtype == MIA_F32 ? ((const float*)p)[i] : (float)((const bf16*)p)[i];
+}
+__device__ __forceinline__ void st_elem(void* p, int dtype, int64_t i, float v) {
+  if (dtype == MIA_F32) ((float*)p)[i] = v;
+  else ((bf16*)p)[i] = (bf16)v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// splitmix64 counter hash -> uniform [0,1) (dropout masks; same recipe as oracle/synth.py)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float hash_u01(uint64_t seed, uint64_t idx) {
+  uint64_t z = splitmix64(idx ^ (seed * 0xD1B54A32D192ED03ull));
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// 8 consecutive elements (16 B bf16 / 32 B f32, aligned) <-> 8 floats
+__device__ __forceinline__ void load8(const void* p, int dtype, int64_t off, float (&f)[8]) {
+  if (dtype == MIA_BF16) {
+    uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + off);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+    const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + off);
+    float4 a = q[0], b = q[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+}
+__device__ __forceinline__ void store8(void* p, int dtype, int64_t off, const float (&f)[8]) {
+  if (dtype == MIA_BF16) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+      w[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + off) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + off);
+    q[0] = make_float4(f[0], f[1], f[2], f[3]);
+    q[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+

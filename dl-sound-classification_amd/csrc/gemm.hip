@@ -1,0 +1,657 @@
+// Implicit-GEMM on MFMA for gfx950 — the dense contractions of the hot path.
+//
+// One kernel template serves: every EnvNet-v2 conv (fwd = im2col(x) . W^T, dgrad = conv of the
+// padded dY with the flipped kernel, wgrad = dY^T . im2col(x)), the FC layers, the AST linears and
+// the AST patch-embed conv.  Operands are gathered straight from NHWC activations (no im2col
+// buffer), converted to the compute type while staging into LDS, optionally transformed by the
+// previous layer's BatchNorm affine + ReLU (so BN-apply never takes its own HBM pass).
+//
+//  * compute bf16: v_mfma_f32_32x32x16_bf16, lane holds 8 consecutive k of its row.
+//  * compute f32 : v_mfma_f32_32x32x2_f32 x 8 per 16-k step over the SAME 8-consecutive-k lane
+//                  fragments (the k order inside a step is permuted identically for A and B,
+//                  so the sum is unchanged) — exact-f32 path used for parity.
+//  * LDS tile layouts: KC = [row][k] (+16 B row pad: conflict-free ds_read_b128),
+//                      RC = [k][row] read with ds_read_b64_tr_b16 (bf16) / ds_read_b32 (f32),
+//                      row stride padded to 16 dwords mod 64 (conflict-free transposed reads).
+//  * 256 threads = 4 waves, each owning (BM/WM) x (BN/WN) of 32x32 accumulator tiles;
+//    register-staged double-buffered K loop (BK = 32), one barrier per K tile.
+//  * split-K writes f32 partial slabs; a reduce kernel applies the epilogue.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int NT = 256;
+
+struct OpDev {
+  const char* ptr;
+  int kind, dtype, pre;
+  int64_t rows, cols, ld;
+  int n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw;
+  int npix, ohw, kwc, jtot;
+  const float* ps;
+  const float* pt;
+};
+
+struct EpiDev {
+  char* ptr;
+  int dtype, act, accumulate, aux_dtype;
+  int64_t ldc, rm_inner, rm_outer, rm_istride, rm_offset;
+  const float* bias;
+  const char* aux;
+  int64_t ldaux;
+  float alpha, act_scale;
+};
+
+struct GemmArgs {
+  OpDev a, b;
+  EpiDev e;
+  int64_t M, N, K, kper;
+  int split;
+  float* ws;
+};
+
+template <typename T> struct TT;
+template <> struct TT<bf16> { static constexpr int dt = MIA_BF16; static constexpr int CW = 4; };
+template <> struct TT<float> { static constexpr int dt = MIA_F32; static constexpr int CW = 8; };
+
+__device__ __forceinline__ float apply_pre(const OpDev& o, float v, int ch) {
+  if (o.pre == MIA_PRE_AFFINE || o.pre == MIA_PRE_AFFINE_RELU) {
+    v = fmaf(v, o.ps[ch], o.pt[ch]);
+    if (o.pre == MIA_PRE_AFFINE_RELU) v = fmaxf(v, 0.f);
+  } else if (o.pre == MIA_PRE_GELU) {
+    v = gelu_erf(v);
+  }
+  return v;
+}
+
+// Load 8 consecutive source elements starting at element offset `off` (off < 0: zeros),
+// apply the pre-op, and pack them as the compute type T into v[].
+template <typename T>
+__device__ __forceinline__ void load_chunk(const OpDev& o, int64_t off, int nvalid, int ch,
+                                           uint32_t (&v)[TT<T>::CW]) {
+  constexpr int CW = TT<T>::CW;
+  if (off < 0) {
+#pragma unroll
+    for (int i = 0; i < CW; ++i) v[i] = 0u;
+    return;
+  }
+  float f[8];
+  if (o.dtype == MIA_BF16) {
+    const bf16* p = reinterpret_cast<const bf16*>(o.ptr) + off;
+    if (nvalid == 8 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+      uint4 u = *reinterpret_cast<const uint4*>(p);
+      if constexpr (TT<T>::dt == MIA_BF16) {
+        if (o.pre == MIA_PRE_NONE) {
+          v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+          return;
+        }
+      }
+      uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(w4[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = i < nvalid ? (float)p[i] : 0.f;
+    }
+  } else {
+    const float* p = reinterpret_cast<const float*>(o.ptr) + off;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if (nvalid == 8 && (a & 15) == 0) {
+      float4 x0 = reinterpret_cast<const float4*>(p)[0];
+      float4 x1 = reinterpret_cast<const float4*>(p)[1];
+      f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w;
+      f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
+    } else if (nvalid == 8 && (a & 7) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float2 x = reinterpret_cast<const float2*>(p)[i];
+        f[2 * i] = x.x; f[2 * i + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = i < nvalid ? p[i] : 0.f;
+    }
+  }
+  if (o.pre != MIA_PRE_NONE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = i < nvalid ? apply_pre(o, f[i], ch + i) : 0.f;
+  }
+  if constexpr (TT<T>::dt == MIA_BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+      v[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
+             ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __float_as_uint(f[i]);
+  }
+}
+
+// -------------------------------------------------------------------------- loaders
+// KC: tile rows R, each row = BK k-elements; a thread owns chunk column kq = t%4 and rows t/4+64s.
+template <typename T, int R>
+struct LoaderKC {
+  static constexpr int CHUNKS = R * BK / 8;
+  static constexpr int CH = (CHUNKS + NT - 1) / NT;
+  static constexpr int CW = TT<T>::CW;
+  static constexpr int RS = BK * (int)sizeof(T) + 16;  // LDS row stride (bytes)
+  static constexpr int BYTES = R * RS;
+  int kq;
+  bool active[CH];
+  int64_t rowoff[CH];        // DENSE
+  int bh[CH], bih[CH], biw[CH];  // CONV: b*h, y*sh-ph, x*sw-pw
+  bool rvalid[CH];
+  int ky, kx, ci;            // CONV tap state for j
+  int64_t j;
+  uint32_t v[CH][CW];
+
+  __device__ __forceinline__ void init(const OpDev& o, int64_t r0, int64_t kbeg, int t) {
+    kq = t & 3;
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int chunk = t + NT * s;
+      active[s] = chunk < CHUNKS;
+      const int64_t row = r0 + (chunk >> 2);
+      if (o.kind == MIA_OP_DENSE) {
+        rvalid[s] = row < o.rows;
+        rowoff[s] = row * o.ld;
+      } else {
+        rvalid[s] = row < o.npix;
+        const int ri = rvalid[s] ? (int)row : 0;
+        const int b = ri / o.ohw;
+        const int rr = ri - b * o.ohw;
+        const int y = rr / o.ow;
+        const int x = rr - y * o.ow;
+        bh[s] = b * o.h;
+        bih[s] = y * o.sh - o.ph;
+        biw[s] = x * o.sw - o.pw;
+      }
+    }
+    j = kbeg + kq * 8;
+    if (o.kind == MIA_OP_CONV) {
+      ci = (int)(j % o.c);
+      const int tt = (int)(j / o.c);
+      kx = tt % o.kw;
+      ky = tt / o.kw;
+    } else if (o.kind == MIA_OP_CONVROW) {
+      ky = (int)(j / o.kwc);
+      ci = (int)(j - (int64_t)ky * o.kwc);
+      kx = 0;
+    }
+  }
+  __device__ __forceinline__ void advance(const OpDev& o) {
+    j += BK;
+    if (o.kind == MIA_OP_CONV) {
+      ci += BK;
+      while (ci >= o.c) {
+        ci -= o.c;
+        if (++kx == o.kw) { kx = 0; ++ky; }
+      }
+    } else if (o.kind == MIA_OP_CONVROW) {
+      ci += BK;
+      while (ci >= o.kwc) { ci -= o.kwc; ++ky; }
+    }
+  }
+  __device__ __forceinline__ void load(const OpDev& o, int64_t kend) {
+    const bool jok = j < kend;
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (!active[s]) continue;
+      int64_t off = -1;
+      int nvalid = 8;
+      int ch = 0;
+      if (jok && rvalid[s]) {
+        if (o.kind == MIA_OP_DENSE) {
+          if (j < o.cols) {
+            off = rowoff[s] + j;
+            const int64_t rem = o.cols - j;
+            nvalid = rem < 8 ? (int)rem : 8;
+            ch = (int)j;
+          }
+        } else if (j < o.jtot) {
+          const int ih = bih[s] + ky;
+          const int iw = biw[s] + kx;
+          if (ih >= 0 && ih < o.h && iw >= 0 && iw < o.w) {
+            off = ((int64_t)(bh[s] + ih) * o.w + iw) * o.c + ci;
+            ch = ci;
+          }
+        }
+      }
+      load_chunk<T>(o, off, nvalid, ch, v[s]);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int t) const {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (!active[s]) continue;
+      const int row = (t + NT * s) >> 2;
+      char* p = lds + row * RS + kq * 8 * (int)sizeof(T);
+      if constexpr (CW == 4) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(v[s][0], v[s][1], v[s][2], v[s][3]);
+      } else {
+        reinterpret_cast<uint4*>(p)[0] = make_uint4(v[s][0], v[s][1], v[s][2], v[s][3]);
+        reinterpret_cast<uint4*>(p)[1] = make_uint4(v[s][4], v[s][5], v[s][6], v[s][7]);
+      }
+    }
+  }
+};
+
+// RC: tile = BK k-rows x R contiguous elements; thread owns row-chunk rq = t%RQ, k-rows t/RQ + step*s.
+template <typename T, int R>
+struct LoaderRC {
+  static constexpr int RQ = R / 8;
+  static constexpr int STEP = NT / RQ;
+  static constexpr int CHUNKS = BK * RQ;
+  static constexpr int CH = (CHUNKS + NT - 1) / NT;
+  static constexpr int CW = TT<T>::CW;
+  static constexpr int PADDW = sizeof(T) == 2 ? ((16 - R / 2) % 64 + 64) % 64 : 4;
+  static constexpr int RS = R * (int)sizeof(T) + PADDW * 4;
+  static constexpr int BYTES = BK * RS;
+  int rq, kr0;
+  bool active[CH];
+  bool jvalid;
+  int64_t j;
+  int ky, kx, ci;
+  uint32_t v[CH][CW];
+  int64_t k0;
+
+  __device__ __forceinline__ void init(const OpDev& o, int64_t r0, int64_t kbeg, int t) {
+    rq = t % RQ;
+    kr0 = t / RQ;
+#pragma unroll
+    for (int s = 0; s < CH; ++s) active[s] = (t + NT * s) < CHUNKS;
+    j = r0 + rq * 8;
+    if (o.kind == MIA_OP_DENSE) {
+      jvalid = j < o.cols;
+    } else {
+      jvalid = j < o.jtot;
+      if (o.kind == MIA_OP_CONV) {
+        ci = (int)(j % o.c);
+        const int tt = (int)(j / o.c);
+        kx = tt % o.kw;
+        ky = tt / o.kw;
+      } else {
+        ky = (int)(j / o.kwc);
+        ci = (int)(j - (int64_t)ky * o.kwc);
+        kx = 0;
+      }
+    }
+    k0 = kbeg;
+  }
+  __device__ __forceinline__ void advance(const OpDev&) { k0 += BK; }
+  __device__ __forceinline__ void load(const OpDev& o, int64_t kend) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (!active[s]) continue;
+      const int64_t k = k0 + kr0 + STEP * s;
+      int64_t off = -1;
+      int nvalid = 8;
+      int ch = 0;
+      if (jvalid && k < kend) {
+        if (o.kind == MIA_OP_DENSE) {
+          if (k < o.rows) {
+            off = k * o.ld + j;
+            const int64_t rem = o.cols - j;
+            nvalid = rem < 8 ? (int)rem : 8;
+            ch = (int)j;
+          }
+        } else if (k < o.npix) {
+          const int ki = (int)k;
+          const int b = ki / o.ohw;
+          const int rr = ki - b * o.ohw;
+          const int y = rr / o.ow;
+          const int x = rr - y * o.ow;
+          const int ih = y * o.sh - o.ph + ky;
+          const int iw = x * o.sw - o.pw + kx;
+          if (ih >= 0 && ih < o.h && iw >= 0 && iw < o.w) {
+            off = ((int64_t)(b * o.h + ih) * o.w + iw) * o.c + ci;
+            ch = ci;
+          }
+        }
+      }
+      load_chunk<T>(o, off, nvalid, ch, v[s]);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int t) const {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (!active[s]) continue;
+      const int kr = kr0 + STEP * s;
+      char* p = lds + kr * RS + rq * 8 * (int)sizeof(T);
+      if constexpr (CW == 4) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(v[s][0], v[s][1], v[s][2], v[s][3]);
+      } else {
+        reinterpret_cast<uint4*>(p)[0] = make_uint4(v[s][0], v[s][1], v[s][2], v[s][3]);
+        reinterpret_cast<uint4*>(p)[1] = make_uint4(v[s][4], v[s][5], v[s][6], v[s][7]);
+      }
+    }
+  }
+};
+
+template <typename T, int L, int R> struct LoaderSel;
+template <typename T, int R> struct LoaderSel<T, MIA_LAYOUT_KC, R> { using type = LoaderKC<T, R>; };
+template <typename T, int R> struct LoaderSel<T, MIA_LAYOUT_RC, R> { using type = LoaderRC<T, R>; };
+
+// -------------------------------------------------------------------------- fragments
+// Fragment of 8 consecutive k (k = ks*16 + 8*(lane>>5) ..+7) for tile row `row`.
+template <typename T> struct Frag;
+template <> struct Frag<bf16> { bf16x8 x; };
+template <> struct Frag<float> { float x[8]; };
+
+template <typename T, int L, int R>
+__device__ __forceinline__ Frag<T> read_frag(const char* lds, int row, int ks, int lane) {
+  Frag<T> f;
+  if constexpr (L == MIA_LAYOUT_KC) {
+    constexpr int RS = LoaderKC<T, R>::RS;
+    const int kbyte = (ks * 16 + 8 * (lane >> 5)) * (int)sizeof(T);
+    const char* p = lds + row * RS + kbyte;
+    if constexpr (sizeof(T) == 2) {
+      f.x = *reinterpret_cast<const bf16x8*>(p);
+    } else {
+      float4 a = reinterpret_cast<const float4*>(p)[0];
+      float4 b = reinterpret_cast<const float4*>(p)[1];
+      f.x[0] = a.x; f.x[1] = a.y; f.x[2] = a.z; f.x[3] = a.w;
+      f.x[4] = b.x; f.x[5] = b.y; f.x[6] = b.z; f.x[7] = b.w;
+    }
+  } else {
+    constexpr int RS = LoaderRC<T, R>::RS;
+    if constexpr (sizeof(T) == 2) {
+      // row = base + (lane & 31); transposed read: group g = lane>>4 reads rows
+      // k0..k0+3 (k0 = ks*16 + 8*(g>>1)) x columns col0..col0+15 (col0 = base + 16*(g&1)).
+      const int i16 = lane & 15;
+      const int g = lane >> 4;
+      const int base = row - (lane & 31);
+      const int col = base + 16 * (g & 1) + 4 * (i16 & 3);
+      const int kr = ks * 16 + 8 * (g >> 1) + (i16 >> 2);
+      const char* p0 = lds + kr * RS + col * 2;
+      const char* p1 = p0 + 4 * RS;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      f.x = __builtin_bit_cast(bf16x8, c);
+    } else {
+      const int kr = ks * 16 + 8 * (lane >> 5);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        f.x[t] = *reinterpret_cast<const float*>(lds + (kr + t) * RS + row * 4);
+    }
+  }
+  return f;
+}
+
+__device__ __forceinline__ void mma(f32x16& acc, const Frag<bf16>& a, const Frag<bf16>& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.x, b.x, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x[t], b.x[t], acc, 0, 0, 0);
+}
+
+// -------------------------------------------------------------------------- epilogue
+__device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n, float acc) {
+  float v = acc * e.alpha;
+  if (e.bias) v += e.bias[n];
+  switch (e.act) {
+    case MIA_ACT_RELU: v = fmaxf(v, 0.f); break;
+    case MIA_ACT_GELU: v = gelu_erf(v); break;
+    case MIA_DACT_NZ: {
+      const float a = ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n);
+      v = a != 0.f ? v * e.act_scale : 0.f;
+      break;
+    }
+    case MIA_DACT_GELU: v *= gelu_erf_grad(ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n)); break;
+    default: break;
+  }
+  int64_t prow = m;
+  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+  const int64_t idx = prow * e.ldc + n;
+  if (e.accumulate) v += ld_elem(e.ptr, e.dtype, idx);
+  st_elem(e.ptr, e.dtype, idx, v);
+}
+
+template <typename T, int BM, int BN, int WM, int LA, int LB>
+__global__ __launch_bounds__(NT) void igemm_kernel(GemmArgs g) {
+  constexpr int WN = 4 / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  using LA_t = typename LoaderSel<T, LA, BM>::type;
+  using LB_t = typename LoaderSel<T, LB, BN>::type;
+  constexpr int ABYTES = LA_t::BYTES, BBYTES = LB_t::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (ABYTES + BBYTES)];
+  static_assert(2 * (ABYTES + BBYTES) >= 4 * 32 * 33 * 4, "epilogue staging needs 16.5 KB of LDS");
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int z = blockIdx.z;
+  const int64_t kbeg = (int64_t)z * g.kper;
+  int64_t kend = kbeg + g.kper;
+  if (kend > g.K) kend = g.K;
+  const int nk = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+
+  LA_t la;
+  LB_t lb;
+  la.init(g.a, m0, kbeg, t);
+  lb.init(g.b, n0, kbeg, t);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int jn = 0; jn < TN; ++jn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][jn][r] = 0.f;
+
+  if (nk > 0) {
+    la.load(g.a, kend);
+    lb.load(g.b, kend);
+    la.store(smem, t);
+    lb.store(smem + ABYTES, t);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const char* As = smem + cur * (ABYTES + BBYTES);
+    const char* Bs = As + ABYTES;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.advance(g.a);
+      lb.advance(g.b);
+      la.load(g.a, kend);
+      lb.load(g.b, kend);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      Frag<T> fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = read_frag<T, LA, BM>(As, wm * WTM + i * 32 + (lane & 31), ks, lane);
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn) fb[jn] = read_frag<T, LB, BN>(Bs, wn * WTN + jn * 32 + (lane & 31), ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < TN; ++jn) mma(acc[i][jn], fa[i], fb[jn]);
+    }
+    if (more) {
+      char* An = smem + (cur ^ 1) * (ABYTES + BBYTES);
+      la.store(An, t);
+      lb.store(An + ABYTES, t);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue, staged through LDS per 32x32 accumulator tile so each lane then owns 16
+  // contiguous output columns of one row (coalesced stores, static accumulator indexing).
+  // C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int jn = 0; jn < TN; ++jn) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = acc[i][jn][r];
+      __syncthreads();
+      const int row = lane >> 1;
+      const int c0 = (lane & 1) * 16;
+      const int64_t m = m0 + wm * WTM + i * 32 + row;
+      const int64_t nb = n0 + wn * WTN + jn * 32 + c0;
+      if (m < g.M) {
+        if (g.split > 1) {
+          float* dst = g.ws + ((int64_t)z * g.M + m) * g.N;
+          for (int c = 0; c < 16; ++c)
+            if (nb + c < g.N) dst[nb + c] = stage[row * 33 + c0 + c];
+        } else {
+          for (int c = 0; c < 16; ++c)
+            if (nb + c < g.N) epi_store(g.e, m, nb + c, stage[row * 33 + c0 + c]);
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__global__ void splitk_reduce_kernel(const float* ws, int split, int64_t M, int64_t N, EpiDev e) {
+  const int64_t total = M * N;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < split; ++z) s += ws[z * total + idx];
+    epi_store(e, idx / N, idx % N, s);
+  }
+}
+
+OpDev to_dev(const MiaOperand& o) {
+  OpDev d;
+  memset(&d, 0, sizeof(d));
+  d.ptr = reinterpret_cast<const char*>(o.ptr);
+  d.kind = o.kind; d.dtype = o.dtype; d.pre = o.pre;
+  d.rows = o.rows; d.cols = o.cols; d.ld = o.ld;
+  d.n = o.n; d.h = o.h; d.w = o.w; d.c = o.c; d.oh = o.oh; d.ow = o.ow;
+  d.kh = o.kh; d.kw = o.kw; d.sh = o.sh; d.sw = o.sw; d.ph = o.ph; d.pw = o.pw;
+  d.npix = o.n * o.oh * o.ow;
+  d.ohw = o.oh * o.ow;
+  d.kwc = o.kw * o.c;
+  d.jtot = o.kh * o.kw * o.c;
+  d.ps = o.pre_scale; d.pt = o.pre_shift;
+  return d;
+}
+
+EpiDev to_dev(const MiaEpilogue& e) {
+  EpiDev d;
+  d.ptr = reinterpret_cast<char*>(e.ptr);
+  d.dtype = e.dtype; d.act = e.act; d.accumulate = e.accumulate; d.aux_dtype = e.aux_dtype;
+  d.ldc = e.ldc; d.rm_inner = e.rm_inner; d.rm_outer = e.rm_outer; d.rm_istride = e.rm_istride;
+  d.rm_offset = e.rm_offset; d.bias = e.bias; d.aux = reinterpret_cast<const char*>(e.aux);
+  d.ldaux = e.ldaux; d.alpha = e.alpha; d.act_scale = e.act_scale;
+  return d;
+}
+
+int check_operand(const MiaOperand& o, const char* name) {
+  MIA_CHECK_ARG(o.ptr != nullptr, "gemm: operand %s is null", name);
+  MIA_CHECK_ARG(o.dtype == MIA_F32 || o.dtype == MIA_BF16, "gemm: operand %s dtype %d", name, o.dtype);
+  MIA_CHECK_ARG(o.layout == MIA_LAYOUT_KC || o.layout == MIA_LAYOUT_RC, "gemm: operand %s layout", name);
+  if (o.pre == MIA_PRE_AFFINE || o.pre == MIA_PRE_AFFINE_RELU)
+    MIA_CHECK_ARG(o.pre_scale && o.pre_shift && o.kind != MIA_OP_CONVROW,
+                  "gemm: operand %s affine pre-op needs scale/shift and a DENSE/CONV source", name);
+  if (o.kind == MIA_OP_DENSE) {
+    MIA_CHECK_ARG(o.rows >= 0 && o.cols >= 0 && o.ld >= o.cols, "gemm: operand %s dense extents", name);
+  } else {
+    MIA_CHECK_ARG(o.n > 0 && o.h > 0 && o.w > 0 && o.c > 0 && o.oh > 0 && o.ow > 0 && o.kh > 0 &&
+                      o.kw > 0 && o.sh > 0 && o.sw > 0,
+                  "gemm: operand %s conv geometry", name);
+    MIA_CHECK_ARG((int64_t)o.n * o.oh * o.ow < (1ll << 31), "gemm: operand %s too many pixels", name);
+    if (o.kind == MIA_OP_CONV) {
+      MIA_CHECK_ARG(o.c % 8 == 0, "gemm: operand %s CONV needs c %% 8 == 0 (c=%d)", name, o.c);
+    } else {
+      MIA_CHECK_ARG((o.kw * o.c) % 8 == 0 && o.pw == 0, "gemm: operand %s CONVROW needs kw*c %% 8 == 0, pw == 0", name);
+      MIA_CHECK_ARG((int64_t)(o.ow - 1) * o.sw + o.kw <= o.w, "gemm: operand %s CONVROW row overruns input", name);
+    }
+  }
+  return 0;
+}
+
+template <typename T, int BM, int BN, int WM>
+hipError_t launch_cfg(const GemmArgs& g, int LA, int LB, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.N, BN), (unsigned)g.split);
+  if (LA == MIA_LAYOUT_KC && LB == MIA_LAYOUT_KC)
+    igemm_kernel<T, BM, BN, WM, MIA_LAYOUT_KC, MIA_LAYOUT_KC><<<grid, NT, 0, s>>>(g);
+  else if (LA == MIA_LAYOUT_KC && LB == MIA_LAYOUT_RC)
+    igemm_kernel<T, BM, BN, WM, MIA_LAYOUT_KC, MIA_LAYOUT_RC><<<grid, NT, 0, s>>>(g);
+  else if (LA == MIA_LAYOUT_RC && LB == MIA_LAYOUT_KC)
+    igemm_kernel<T, BM, BN, WM, MIA_LAYOUT_RC, MIA_LAYOUT_KC><<<grid, NT, 0, s>>>(g);
+  else
+    igemm_kernel<T, BM, BN, WM, MIA_LAYOUT_RC, MIA_LAYOUT_RC><<<grid, NT, 0, s>>>(g);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_t(const GemmArgs& g, int LA, int LB, hipStream_t s) {
+  if (g.N <= 32) return launch_cfg<T, 256, 32, 4>(g, LA, LB, s);
+  if (g.N <= 64) return launch_cfg<T, 128, 64, 2>(g, LA, LB, s);
+  if (g.M <= 32) return launch_cfg<T, 32, 128, 1>(g, LA, LB, s);
+  if (g.M <= 64) return launch_cfg<T, 64, 128, 1>(g, LA, LB, s);
+  return launch_cfg<T, 128, 128, 2>(g, LA, LB, s);
+}
+
+}  // namespace
+
+extern "C" int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k) {
+  return split_k > 1 ? (int64_t)split_k * M * N * 4 : 0;
+}
+
+extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
+                        int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
+                        mia_stream_t stream) {
+  MIA_CHECK_ARG(A && B && E, "gemm: null descriptor");
+  MIA_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative extent");
+  MIA_CHECK_ARG(M < (1ll << 31) * 128 && N < 65535ll * 128, "gemm: extent too large");
+  if (int r = check_operand(*A, "A")) return r;
+  if (int r = check_operand(*B, "B")) return r;
+  MIA_CHECK_ARG(E->ptr != nullptr, "gemm: output is null");
+  MIA_CHECK_ARG(compute_dtype == MIA_F32 || compute_dtype == MIA_BF16, "gemm: compute dtype");
+  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU) MIA_CHECK_ARG(E->aux != nullptr, "gemm: dact needs aux");
+  if (split_k < 1) split_k = 1;
+  if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");
+  if (M == 0 || N == 0) return 0;
+  GemmArgs g;
+  g.a = to_dev(*A);
+  g.b = to_dev(*B);
+  g.e = to_dev(*E);
+  g.M = M; g.N = N; g.K = K;
+  g.split = split_k;
+  g.kper = cdiv(cdiv(K, split_k), BK) * BK;
+  g.ws = reinterpret_cast<float*>(workspace);
+  hipStream_t s = as_stream(stream);
+  hipError_t err = compute_dtype == MIA_BF16 ? launch_t<bf16>(g, A->layout, B->layout, s)
+                                             : launch_t<float>(g, A->layout, B->layout, s);
+  if (err != hipSuccess) return mia::fail(-(int)err, "gemm launch: %s", hipGetErrorString(err));
+  if (split_k > 1) {
+    const int64_t total = M * N;
+    int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g.ws, split_k, M, N, g.e);
+    MIA_LAUNCH_CHECK("splitk_reduce");
+  }
+  return 0;
+}
+
+extern "C" int mia_splitk_reduce(const float* ws, int32_t split_k, int64_t M, int64_t N,
+                                 const MiaEpilogue* E, mia_stream_t stream) {
+  MIA_CHECK_ARG(ws && E && E->ptr, "splitk_reduce: null pointer");
+  EpiDev e = to_dev(*E);
+  const int64_t total = M * N;
+  if (total == 0) return 0;
+  int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+  splitk_reduce_kernel<<<blocks, 256, 0, as_stream(stream)>>>(ws, split_k, M, N, e);
+  MIA_LAUNCH_CHECK("splitk_reduce");
+  return 0;
+}

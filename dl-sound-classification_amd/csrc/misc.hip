@@ -1,0 +1,444 @@
+// Small kernels of the training step: weight repacking, soft-label loss, grad-norm clip + Adam,
+// dropout, AST token assembly, on-GPU BC mixing / SpecAugment+Mixup, casts (gfx950).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// ------------------------------------------------------------------ weight repacking
+__global__ void pack_weight_kernel(const float* __restrict__ src, void* dst, int dtype, int cout, int cin, int kh,
+                                   int kw, int mode) {
+  const int64_t total = (int64_t)cout * cin * kh * kw;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (mode == 0) {  // dst (co, ky, kx, ci) <- src (co, ci, ky, kx)
+      const int ci = (int)(i % cin); int64_t q = i / cin;
+      const int kx = (int)(q % kw); q /= kw;
+      const int ky = (int)(q % kh); const int co = (int)(q / kh);
+      st_elem(dst, dtype, i, src[(((int64_t)co * cin + ci) * kh + ky) * kw + kx]);
+    } else if (mode == 1) {  // dst (ci, ky, kx, co) <- src (co, ci, kh-1-ky, kw-1-kx)
+      const int co = (int)(i % cout); int64_t q = i / cout;
+      const int kx = (int)(q % kw); q /= kw;
+      const int ky = (int)(q % kh); const int ci = (int)(q / kh);
+      st_elem(dst, dtype, i, src[(((int64_t)co * cin + ci) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)]);
+    } else if (mode == 2) {  // dst (p, ci, j, co) <- src (co, ci, 0, 2*(kw/2-1-j)+p), kh == 1
+      const int half = kw / 2;
+      const int co = (int)(i % cout); int64_t q = i / cout;
+      const int j = (int)(q % half); q /= half;
+      const int ci = (int)(q % cin); const int p = (int)(q / cin);
+      st_elem(dst, dtype, i, src[((int64_t)co * cin + ci) * kw + 2 * (half - 1 - j) + p]);
+    } else if (mode == 3) {  // dst (ky, j, co) <- src (co, 0, ky, kw-1-j), cin == 1
+      const int co = (int)(i % cout); int64_t q = i / cout;
+      const int j = (int)(q % kw); const int ky = (int)(q / kw);
+      st_elem(dst, dtype, i, src[((int64_t)co * kh + ky) * kw + (kw - 1 - j)]);
+    } else {  // mode 4: dst (co, ci, ky, kx) <- src (co, ky, kx, ci), f32
+      const int kx = (int)(i % kw); int64_t q = i / kw;
+      const int ky = (int)(q % kh); q /= kh;
+      const int ci = (int)(q % cin); const int co = (int)(q / cin);
+      st_elem(dst, dtype, i, src[(((int64_t)co * kh + ky) * kw + kx) * cin + ci]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ soft-label CE
+// One block; wave w handles rows w, w+4, ...
+__global__ __launch_bounds__(NT) void soft_ce_kernel(const float* __restrict__ logits, const float* __restrict__ y,
+                                                     int B, int C, int input_sigmoid, float* loss_out,
+                                                     float* __restrict__ dlogits, int* correct_out) {
+  __shared__ double wl[4];
+  __shared__ int wc[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double lsum = 0.0;
+  int hits = 0;
+  const float invB = 1.f / (float)B;
+  for (int b = wave; b < B; b += 4) {
+    const float* zr = logits + (int64_t)b * C;
+    const float* yr = y + (int64_t)b * C;
+    // pass 1: max of z (z = sigmoid(logit) if requested), argmax of logits and of y
+    float mx = -INFINITY, bestz = -INFINITY, besty = -INFINITY;
+    int az = 1 << 30, ay = 1 << 30;
+    for (int c = lane; c < C; c += 64) {
+      const float l = zr[c];
+      const float z = input_sigmoid ? 1.f / (1.f + __expf(-l)) : l;
+      mx = fmaxf(mx, z);
+      if (l > bestz) { bestz = l; az = c; }
+      if (yr[c] > besty) { besty = yr[c]; ay = c; }
+    }
+    mx = wave_max(mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float bz = __shfl_xor(bestz, o, 64); const int iz = __shfl_xor(az, o, 64);
+      if (bz > bestz || (bz == bestz && iz < az)) { bestz = bz; az = iz; }
+      const float by = __shfl_xor(besty, o, 64); const int iy = __shfl_xor(ay, o, 64);
+      if (by > besty || (by == besty && iy < ay)) { besty = by; ay = iy; }
+    }
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float l = zr[c];
+      const float z = input_sigmoid ? 1.f / (1.f + __expf(-l)) : l;
+      se += expf(z - mx);
+    }
+    se = wave_sum(se);
+    // pass 2: loss and R = sum_c y_c p_c / (p_c + eps)
+    float lrow = 0.f, R = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float l = zr[c];
+      const float z = input_sigmoid ? 1.f / (1.f + __expf(-l)) : l;
+      const float p = expf(z - mx) / se;
+      lrow += yr[c] * logf(p + 1e-8f);
+      R += yr[c] * p / (p + 1e-8f);
+    }
+    lrow = wave_sum(lrow);
+    R = wave_sum(R);
+    for (int c = lane; c < C; c += 64) {
+      const float l = zr[c];
+      const float s = input_sigmoid ? 1.f / (1.f + __expf(-l)) : l;
+      const float p = expf(s - mx) / se;
+      float g = (p * R - yr[c] * p / (p + 1e-8f)) * invB;
+      if (input_sigmoid) g *= s * (1.f - s);
+      dlogits[(int64_t)b * C + c] = g;
+    }
+    if (lane == 0) { lsum += -(double)lrow; hits += (az == ay); }
+  }
+  if (lane == 0) { wl[wave] = lsum; wc[wave] = hits; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss_out[0] = (float)((wl[0] + wl[1] + wl[2] + wl[3]) / (double)B);
+    if (correct_out) correct_out[0] = wc[0] + wc[1] + wc[2] + wc[3];
+  }
+}
+
+// ------------------------------------------------------------------ clip + Adam
+constexpr int ADAM_PARTS = 512;
+
+__global__ __launch_bounds__(NT) void sqnorm_kernel(void* const* __restrict__ grads, const int64_t* __restrict__ sizes,
+                                                    float* __restrict__ ws) {
+  const int tsr = blockIdx.y;
+  const float* g = reinterpret_cast<const float*>(grads[tsr]);
+  const int64_t n = sizes[tsr];
+  double s = 0.0;
+  float fs = 0.f;
+  int cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float v = g[i];
+    fs = fmaf(v, v, fs);
+    if (++cnt == 256) { s += fs; fs = 0.f; cnt = 0; }
+  }
+  s += fs;
+  s = wave_sum_d(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    reinterpret_cast<double*>(ws)[(int64_t)tsr * ADAM_PARTS + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ws layout (doubles): [ntensors][ADAM_PARTS] partials, then [0] = coef (float in double slot)
+__global__ __launch_bounds__(NT) void norm_final_kernel(double* ws, int ntensors, int nparts, float clip, float* total_out,
+                                                        float* coef_out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < ntensors * nparts; i += NT) {
+    const int tsr = i / nparts, p = i % nparts;
+    s += ws[(int64_t)tsr * ADAM_PARTS + p];
+  }
+  s = wave_sum_d(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double tot = sqrt(red[0] + red[1] + red[2] + red[3]);
+    const float total = (float)tot;
+    float coef = 1.f;
+    if (clip > 0.f) {
+      coef = clip / (total + 1e-6f);
+      if (coef > 1.f) coef = 1.f;
+    }
+    if (total_out) total_out[0] = total;
+    coef_out[0] = coef;
+  }
+}
+
+__global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ params, void* const* __restrict__ grads,
+                                                  void* const* __restrict__ m1, void* const* __restrict__ m2,
+                                                  const int64_t* __restrict__ sizes, const float* __restrict__ coef_p,
+                                                  float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps,
+                                                  float wd) {
+  const int tsr = blockIdx.y;
+  float* p = reinterpret_cast<float*>(params[tsr]);
+  const float* g = reinterpret_cast<const float*>(grads[tsr]);
+  float* m = reinterpret_cast<float*>(m1[tsr]);
+  float* v = reinterpret_cast<float*>(m2[tsr]);
+  const int64_t n = sizes[tsr];
+  const float coef = coef_p[0];
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float pv = p[i];
+    float gv = g[i] * coef;
+    gv = fmaf(wd, pv, gv);
+    float mv = m[i];
+    mv = mv + (1.f - beta1) * (gv - mv);           // exp_avg.lerp_(grad, 1 - beta1)
+    float vv = v[i] * beta2;
+    vv = fmaf((1.f - beta2) * gv, gv, vv);          // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[i] = pv - lr_over_bc1 * (mv / denom);
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+// ------------------------------------------------------------------ dropout / casts
+__global__ void dropout_kernel(void* x, int dtype, int64_t n, float p, uint64_t seed) {
+  const float scale = 1.f / (1.f - p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float u = hash_u01(seed, (uint64_t)i);
+    const float v = u >= p ? ld_elem(x, dtype, i) * scale : 0.f;
+    st_elem(x, dtype, i, v);
+  }
+}
+
+__global__ void cast_kernel(const void* src, int sd, void* dst, int dd, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    st_elem(dst, dd, i, ld_elem(src, sd, i));
+}
+
+__global__ void add_inplace_kernel(float* x, const void* y, int yd, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] += ld_elem(y, yd, i);
+}
+
+// ------------------------------------------------------------------ AST tokens
+__global__ void tokens_fwd_kernel(const float* __restrict__ patches, const float* __restrict__ cls,
+                                  const float* __restrict__ pos, float* __restrict__ out, int B, int Np, int D) {
+  const int64_t total = (int64_t)B * (Np + 1) * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int64_t q = i / D;
+    const int tkn = (int)(q % (Np + 1));
+    const int b = (int)(q / (Np + 1));
+    const float base = tkn == 0 ? cls[d] : patches[((int64_t)b * Np + tkn - 1) * D + d];
+    out[i] = base + pos[(int64_t)tkn * D + d];
+  }
+}
+
+// dpos[t][d] = sum_b dout[b][t][d]; dcls = dpos[0]; dpatches[b][p] = dout[b][1+p]
+__global__ void tokens_bwd_kernel(const float* __restrict__ dout, float* __restrict__ dpatches, float* __restrict__ dcls,
+                                  float* __restrict__ dpos, int B, int Np, int D) {
+  const int64_t total = (int64_t)(Np + 1) * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int tkn = (int)(i / D);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float v = dout[((int64_t)b * (Np + 1) + tkn) * D + d];
+      s += v;
+      if (tkn > 0 && dpatches) dpatches[((int64_t)b * Np + tkn - 1) * D + d] = v;
+    }
+    if (dpos) dpos[i] = s;
+    if (tkn == 0 && dcls) dcls[d] = s;
+  }
+}
+
+// ------------------------------------------------------------------ BC mixing
+__global__ __launch_bounds__(NT) void clip_ms_kernel(const float* __restrict__ x, int64_t T, float* __restrict__ ms) {
+  const float* r = x + (int64_t)blockIdx.x * T;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < T; i += NT) s += (double)r[i] * r[i];
+  s = wave_sum_d(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ms[blockIdx.x] = (float)((red[0] + red[1] + red[2] + red[3]) / (double)T);
+}
+
+__device__ __forceinline__ float spl_db(float ms) {  // BCMixingUtils.a_weighted_spl (preprocessing.py:395-415)
+  const float rms = sqrtf(ms);
+  return rms > 0.f ? 20.f * log10f(rms) + 94.f : -80.f;
+}
+
+// single block: every thread reads the mean squares it needs before any thread overwrites them
+__global__ void bc_coef_kernel(float* ms_then_p, const int* __restrict__ partner, const float* __restrict__ r,
+                               const int64_t* __restrict__ labels, int B, int C, float* __restrict__ yout) {
+  const int b = threadIdx.x;
+  const bool act = b < B;
+  const int q = act ? partner[b] : -1;
+  const float rr = act ? r[b] : 0.f;
+  float p = 1.f;
+  if (act && q >= 0) {
+    // perceptual_mixing_coefficient (preprocessing.py:418-446)
+    const float d = spl_db(ms_then_p[b]) - spl_db(ms_then_p[q]);
+    p = rr;
+    if (fabsf(d) > 10.f) {
+      const float adj = fminf(fabsf(d) / 40.f, 0.3f);
+      p = d > 0.f ? rr * (1.f - adj) : rr * (1.f + adj);
+    }
+    p = fminf(fmaxf(p, 0.f), 1.f);
+  }
+  __syncthreads();
+  if (!act) return;
+  ms_then_p[b] = p;
+  if (yout) {
+    for (int c = 0; c < C; ++c) yout[(int64_t)b * C + c] = 0.f;
+    if (q >= 0) {
+      yout[(int64_t)b * C + labels[b]] = rr;                   // create_soft_labels: uses r, not p
+      yout[(int64_t)b * C + labels[q]] = 1.f - rr;
+    } else {
+      yout[(int64_t)b * C + labels[b]] = 1.f;
+    }
+  }
+}
+
+__global__ void bc_mix_kernel(const float* __restrict__ x, int64_t T, int B, const int* __restrict__ partner,
+                              const float* __restrict__ p_in, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int q = partner[b];
+  const float p = p_in[b];
+  const float norm = sqrtf(p * p + (1.f - p) * (1.f - p));
+  const float* xa = x + (int64_t)b * T;
+  const float* xb = x + (int64_t)(q >= 0 ? q : b) * T;
+  float* o = out + (int64_t)b * T;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = q >= 0 ? (p * xa[i] + (1.f - p) * xb[i]) / norm : xa[i];
+}
+
+// ------------------------------------------------------------------ SpecAugment + Mixup
+__global__ void specaug_mixup_kernel(const float* __restrict__ spec, float* __restrict__ out, int B, int F, int T,
+                                     const int* t0, const int* tl, const int* f0, const int* fl, const int* partner,
+                                     const float* lam) {
+  const int b = blockIdx.y;
+  const int64_t per = (int64_t)F * T;
+  const int q = partner ? partner[b] : -1;
+  const float l = (lam && q >= 0) ? lam[b] : 1.f;
+  const int ts = t0 ? t0[b] : 0, te = ts + (tl ? tl[b] : 0);
+  const int fs = f0 ? f0[b] : 0, fe = fs + (fl ? fl[b] : 0);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T), f = (int)(i / T);
+    float v = spec[(int64_t)b * per + i];
+    if ((t >= ts && t < te) || (f >= fs && f < fe)) v = 0.f;
+    if (q >= 0) v = l * v + (1.f - l) * spec[(int64_t)q * per + i];
+    out[(int64_t)b * per + i] = v;
+  }
+}
+
+int blocks_for(int64_t n, int per = 256, int cap = 16384) {
+  int64_t b = cdiv(n, per);
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int mia_pack_weight(const float* src, void* dst, int32_t dtype, int32_t cout, int32_t cin, int32_t kh,
+                               int32_t kw, int32_t mode, mia_stream_t stream) {
+  MIA_CHECK_ARG(src && dst && cout > 0 && cin > 0 && kh > 0 && kw > 0 && mode >= 0 && mode <= 4, "pack_weight: args");
+  if (mode == 2) MIA_CHECK_ARG(kh == 1 && kw % 2 == 0, "pack_weight: parity mode needs kh == 1 and even kw");
+  if (mode == 3) MIA_CHECK_ARG(cin == 1, "pack_weight: row-split mode needs cin == 1");
+  const int64_t total = (int64_t)cout * cin * kh * kw;
+  pack_weight_kernel<<<blocks_for(total), 256, 0, as_stream(stream)>>>(src, dst, dtype, cout, cin, kh, kw, mode);
+  MIA_LAUNCH_CHECK("pack_weight");
+  return 0;
+}
+
+extern "C" int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32_t input_sigmoid, float* loss,
+                           float* dlogits, int32_t* correct, mia_stream_t stream) {
+  MIA_CHECK_ARG(logits && y && loss && dlogits && B > 0 && C > 0, "soft_ce: args");
+  soft_ce_kernel<<<1, NT, 0, as_stream(stream)>>>(logits, y, B, C, input_sigmoid, loss, dlogits, correct);
+  MIA_LAUNCH_CHECK("soft_ce");
+  return 0;
+}
+
+extern "C" int64_t mia_adam_workspace_bytes(int32_t ntensors) {
+  return ((int64_t)ntensors * ADAM_PARTS + 2) * 8;
+}
+
+extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg, void* const* exp_avg_sq,
+                             const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int32_t step, float clip,
+                             float* total_norm_out, void* sqnorm_ws, mia_stream_t stream) {
+  MIA_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && sizes && sqnorm_ws, "clip_adam: null table");
+  MIA_CHECK_ARG(ntensors > 0 && ntensors < 65536 && step >= 1, "clip_adam: ntensors/step");
+  hipStream_t s = as_stream(stream);
+  double* ws = reinterpret_cast<double*>(sqnorm_ws);
+  float* coef = reinterpret_cast<float*>(ws + (int64_t)ntensors * ADAM_PARTS);
+  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 16)));
+  sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, reinterpret_cast<float*>(ws));
+  MIA_LAUNCH_CHECK("sqnorm");
+  norm_final_kernel<<<1, NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);
+  MIA_LAUNCH_CHECK("norm_final");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const int ablocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, cdiv(max_numel, 256 * 8)));
+  adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, sizes, coef,
+                                                     (float)(lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
+                                                     weight_decay);
+  MIA_LAUNCH_CHECK("adam");
+  return 0;
+}
+
+extern "C" int mia_dropout(void* x, int32_t dtype, int64_t numel, float p, uint64_t seed, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && p >= 0.f && p < 1.f, "dropout: args");
+  if (p == 0.f || numel == 0) return 0;
+  dropout_kernel<<<blocks_for(numel), 256, 0, as_stream(stream)>>>(x, dtype, numel, p, seed);
+  MIA_LAUNCH_CHECK("dropout");
+  return 0;
+}
+
+extern "C" int mia_cast(const void* src, int32_t sdtype, void* dst, int32_t ddtype, int64_t numel, mia_stream_t stream) {
+  MIA_CHECK_ARG(src && dst, "cast: null");
+  if (numel == 0) return 0;
+  cast_kernel<<<blocks_for(numel), 256, 0, as_stream(stream)>>>(src, sdtype, dst, ddtype, numel);
+  MIA_LAUNCH_CHECK("cast");
+  return 0;
+}
+
+extern "C" int mia_add_inplace(float* x, const void* y, int32_t ydtype, int64_t numel, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && y, "add_inplace: null");
+  if (numel == 0) return 0;
+  add_inplace_kernel<<<blocks_for(numel), 256, 0, as_stream(stream)>>>(x, y, ydtype, numel);
+  MIA_LAUNCH_CHECK("add_inplace");
+  return 0;
+}
+
+extern "C" int mia_tokens_fwd(const float* patches, const float* cls, const float* pos, float* out, int32_t B,
+                              int32_t Np, int32_t D, mia_stream_t stream) {
+  MIA_CHECK_ARG(patches && cls && pos && out && B > 0 && Np > 0 && D > 0, "tokens_fwd: args");
+  tokens_fwd_kernel<<<blocks_for((int64_t)B * (Np + 1) * D), 256, 0, as_stream(stream)>>>(patches, cls, pos, out, B, Np, D);
+  MIA_LAUNCH_CHECK("tokens_fwd");
+  return 0;
+}
+
+extern "C" int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, float* dpos, int32_t B, int32_t Np,
+                              int32_t D, mia_stream_t stream) {
+  MIA_CHECK_ARG(dout && B > 0 && Np > 0 && D > 0, "tokens_bwd: args");
+  tokens_bwd_kernel<<<blocks_for((int64_t)(Np + 1) * D), 256, 0, as_stream(stream)>>>(dout, dpatches, dcls, dpos, B, Np, D);
+  MIA_LAUNCH_CHECK("tokens_bwd");
+  return 0;
+}
+
+extern "C" int mia_bc_mix(const float* x, int64_t T, int32_t B, const int32_t* partner, const float* r,
+                          const int64_t* labels, int32_t num_classes, float* out, float* yout, float* p_out,
+                          mia_stream_t stream) {
+  MIA_CHECK_ARG(x && partner && r && labels && out && p_out && B > 0 && T > 0, "bc_mix: args");
+  hipStream_t s = as_stream(stream);
+  // mean squares are parked in p_out first (overwritten by the coefficients)
+  clip_ms_kernel<<<B, NT, 0, s>>>(x, T, p_out);
+  MIA_LAUNCH_CHECK("clip_ms");
+  // coefficient kernel reads ms from p_out and writes p into p_out: run it in a single block,
+  // reading everything before writing (B <= 1024)
+  MIA_CHECK_ARG(B <= 1024, "bc_mix: B must be <= 1024");
+  bc_coef_kernel<<<1, 1024, 0, s>>>(p_out, partner, r, labels, B, num_classes, yout);
+  MIA_LAUNCH_CHECK("bc_coef");
+  bc_mix_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 512), B), 256, 0, s>>>(x, T, B, partner, p_out, out);
+  MIA_LAUNCH_CHECK("bc_mix");
+  return 0;
+}
+
+extern "C" int mia_spec_augment_mixup(const float* spec, float* out, int32_t B, int32_t F, int32_t T, const int32_t* t0,
+                                      const int32_t* tlen, const int32_t* f0, const int32_t* flen,
+                                      const int32_t* partner, const float* lam, mia_stream_t stream) {
+  MIA_CHECK_ARG(spec && out && B > 0 && F > 0 && T > 0, "spec_augment_mixup: args");
+  MIA_CHECK_ARG(spec != out || partner == nullptr, "spec_augment_mixup: in-place mixup is not allowed");
+  specaug_mixup_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv((int64_t)F * T, 256), 512), B), 256, 0,
+                         as_stream(stream)>>>(spec, out, B, F, T, t0, tlen, f0, flen, partner, lam);
+  MIA_LAUNCH_CHECK("spec_augment_mixup");
+  return 0;
+}

@@ -1,0 +1,430 @@
+// BatchNorm2d (train-mode batch statistics) forward/backward and LayerNorm for gfx950.
+//
+// BN runs over channels-last (P, C) activations (P = N*H*W).  Every pass reads 16 B per lane
+// (8 channels of one pixel) and reduces per channel in two deterministic stages:
+// per-block partial sums in LDS -> f32 [nblk][C][2] slab -> one finalize kernel in double.
+// The BN *apply* never takes its own pass in the forward: the consumer GEMM applies
+// scale/shift (+ReLU) while staging its operand (MIA_PRE_AFFINE_RELU), and the pool kernel does
+// the same for the pooled layers.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAXBLK = 1024;
+
+// Reduce per-thread channel partials s1[8], s2[8] (thread owns channel group cg, row slot rs)
+// across row slots through LDS, then write the block's [C][2] partial.
+__device__ __forceinline__ void block_channel_reduce(float (&s1)[8], float (&s2)[8], int C, float* partial) {
+  __shared__ float red[NT * 16];
+  const int t = threadIdx.x;
+  const int G = C / 8;
+  const int rslots = NT / G;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[t * 16 + i] = s1[i]; red[t * 16 + 8 + i] = s2[i]; }
+  __syncthreads();
+  // entry e < 2C sums quantity q=(e/C) of channel c=(e%C) over the row slots
+  for (int e = t; e < 2 * C; e += NT) {
+    const int q = e / C, c = e % C, cg = c / 8, ci = c % 8;
+    float acc = 0.f;
+    for (int r = 0; r < rslots; ++r) acc += red[(r * G + cg) * 16 + q * 8 + ci];
+    partial[((int64_t)blockIdx.x * C + c) * 2 + q] = acc;
+  }
+}
+
+// ---- BN forward statistics: shifted sums about K[c] = x[0][c]
+__global__ __launch_bounds__(NT) void bn_stats_kernel(const void* __restrict__ x, int dtype, int64_t P, int C,
+                                                      float* __restrict__ partial) {
+  const int t = threadIdx.x;
+  const int G = C / 8, cg = t % G, rs = t / G, rslots = NT / G;
+  float K[8];
+  load8(x, dtype, (int64_t)cg * 8, K);
+  float s1[8] = {0}, s2[8] = {0};
+  for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
+    float f[8];
+    load8(x, dtype, r * C + cg * 8, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = f[i] - K[i];
+      s1[i] += d;
+      s2[i] = fmaf(d, d, s2[i]);
+    }
+  }
+  block_channel_reduce(s1, s2, C, partial);
+}
+
+__global__ void bn_finalize_kernel(const void* __restrict__ x, int dtype, const float* __restrict__ partial,
+                                   int nblk, int64_t P, int C, const float* gamma, const float* beta,
+                                   float* running_mean, float* running_var, float momentum, float eps,
+                                   float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += partial[((int64_t)b * C + c) * 2];
+    s2 += partial[((int64_t)b * C + c) * 2 + 1];
+  }
+  const double n = (double)P;
+  const double K = ld_elem(x, dtype, c);
+  const double dm = s1 / n;
+  const double mean = K + dm;
+  double var = s2 / n - dm * dm;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_o[c] = (float)mean;
+  invstd_o[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+  scale_o[c] = g * invstd;
+  shift_o[c] = bb - (float)mean * g * invstd;
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+  if (running_var) {
+    const double unb = P > 1 ? var * n / (n - 1.0) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                               float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+  mean_o[c] = rm[c];
+  invstd_o[c] = invstd;
+  scale_o[c] = g * invstd;
+  shift_o[c] = bb - rm[c] * g * invstd;
+}
+
+// ---- ReLU+BN backward reductions
+__global__ __launch_bounds__(NT) void bn_relu_bwd_reduce_kernel(const void* __restrict__ dact, void* dz,
+                                                                const void* __restrict__ x, int dtype, int64_t P,
+                                                                int C, const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                float* __restrict__ partial) {
+  const int t = threadIdx.x;
+  const int G = C / 8, cg = t % G, rs = t / G, rslots = NT / G;
+  float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[cg * 8 + i]; sh[i] = shift[cg * 8 + i]; mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i];
+  }
+  float s1[8] = {0}, s2[8] = {0};
+  for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
+    float g[8], xv[8];
+    const int64_t off = r * C + cg * 8;
+    load8(dact, dtype, off, g);
+    load8(x, dtype, off, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float z = fmaf(xv[i], sc[i], sh[i]);
+      g[i] = z > 0.f ? g[i] : 0.f;
+      s1[i] += g[i];
+      s2[i] = fmaf(g[i], (xv[i] - mu[i]) * is[i], s2[i]);
+    }
+    store8(dz, dtype, off, g);
+  }
+  block_channel_reduce(s1, s2, C, partial);
+}
+
+// partial [nblk][C][2] -> out0[c] = sum q0, out1[c] = sum q1
+__global__ void channel_partial_sum_kernel(const float* __restrict__ partial, int nblk, int C,
+                                           float* out_q1, float* out_q0) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0, b = 0;
+  for (int k = 0; k < nblk; ++k) {
+    a += partial[((int64_t)k * C + c) * 2];
+    b += partial[((int64_t)k * C + c) * 2 + 1];
+  }
+  if (out_q0) out_q0[c] = (float)a;
+  if (out_q1) out_q1[c] = (float)b;
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const void* __restrict__ dz, const void* __restrict__ x,
+                                                          void* dx, int dtype, int64_t P, int C,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ dgamma,
+                                                          const float* __restrict__ dbeta,
+                                                          float* __restrict__ partial) {
+  const int t = threadIdx.x;
+  const int G = C / 8, cg = t % G, rs = t / G, rslots = NT / G;
+  float a[8], mu[8], is[8], mb[8], mg[8];
+  float s1[8] = {0}, s2[8] = {0};
+  const float invP = 1.f / (float)P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = cg * 8 + i;
+    is[i] = invstd[c];
+    a[i] = (gamma ? gamma[c] : 1.f) * is[i];
+    mu[i] = mean[c];
+    mb[i] = dbeta[c] * invP;
+    mg[i] = dgamma[c] * invP;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
+    float g[8], xv[8];
+    const int64_t off = r * C + cg * 8;
+    load8(dz, dtype, off, g);
+    load8(x, dtype, off, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g[i] = a[i] * (g[i] - mb[i] - (xv[i] - mu[i]) * is[i] * mg[i]);
+      s1[i] += g[i];
+    }
+    store8(dx, dtype, off, g);
+  }
+  if (partial) block_channel_reduce(s1, s2, C, partial);
+}
+
+// ---- generic column sum over a (P, C) matrix with row stride ld (any C, scalar loads)
+__global__ __launch_bounds__(NT) void colsum_kernel(const void* __restrict__ x, int dtype, int64_t P, int C,
+                                                    int64_t ld, float* __restrict__ partial) {
+  const int c = blockIdx.y * NT + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int64_t r = blockIdx.x; r < P; r += gridDim.x) s += ld_elem(x, dtype, r * ld + c);
+  partial[(int64_t)blockIdx.x * C + c] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ partial, int nblk, int C, float* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0;
+  for (int k = 0; k < nblk; ++k) s += partial[(int64_t)k * C + c];
+  out[c] = (float)s;
+}
+
+int nblocks_for(int64_t P, int C) {
+  const int rslots = NT / (C / 8);
+  int64_t nb = cdiv(P, (int64_t)rslots * 8);
+  if (nb > MAXBLK) nb = MAXBLK;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+int check_bn(const void* x, int dtype, int64_t P, int C) {
+  MIA_CHECK_ARG(x != nullptr, "bn: null input");
+  MIA_CHECK_ARG(dtype == MIA_F32 || dtype == MIA_BF16, "bn: dtype");
+  MIA_CHECK_ARG(C % 8 == 0 && C >= 8 && C <= 2048 && (NT % (C / 8)) == 0,
+                "bn: C must be a multiple of 8 dividing 2048 (got %d)", C);
+  MIA_CHECK_ARG(P > 0, "bn: empty input");
+  return 0;
+}
+
+// ---------------------------------------------------------------- LayerNorm (rows x D), one wave per row
+template <int PER>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(const void* __restrict__ x, int xdt, const float* __restrict__ g,
+                                                    const float* __restrict__ b, void* y, int ydt,
+                                                    float* __restrict__ mean_o, float* __restrict__ rstd_o,
+                                                    int64_t rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int d = lane + 64 * i;
+    v[i] = d < D ? ld_elem(x, xdt, row * D + d) : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int d = lane + 64 * i;
+    const float dd = d < D ? v[i] - mean : 0.f;
+    ss = fmaf(dd, dd, ss);
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int d = lane + 64 * i;
+    if (d < D) st_elem(y, ydt, row * D + d, (v[i] - mean) * rstd * g[d] + b[d]);
+  }
+  if (lane == 0) { mean_o[row] = mean; rstd_o[row] = rstd; }
+}
+
+template <int PER>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy, int dydt, const void* __restrict__ x,
+                                                    int xdt, const float* __restrict__ g,
+                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                    void* dx, int dxdt, int accumulate, float* __restrict__ partial,
+                                                    int64_t rows, int D, int rows_per_block) {
+  // partial layout: [gridDim.x][2][D] (dgamma, dbeta) accumulated by each block in LDS
+  __shared__ float pg[2][1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2 * D; i += NT) pg[i / D][i % D] = 0.f;
+  __syncthreads();
+  float ag[PER], ab[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t row = r0 + wave; row < r0 + rows_per_block && row < rows; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[PER], gy[PER];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int d = lane + 64 * i;
+      if (d < D) {
+        const float dv = ld_elem(dy, dydt, row * D + d);
+        xh[i] = (ld_elem(x, xdt, row * D + d) - mu) * rs;
+        gy[i] = dv * g[d];
+        ag[i] = fmaf(dv, xh[i], ag[i]);
+        ab[i] += dv;
+      } else {
+        xh[i] = 0.f; gy[i] = 0.f;
+      }
+      s1 += gy[i];
+      s2 = fmaf(gy[i], xh[i], s2);
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int d = lane + 64 * i;
+      if (d < D) {
+        float v = rs * (gy[i] - s1 - xh[i] * s2);
+        const int64_t idx = row * D + d;
+        if (accumulate) v += ld_elem(dx, dxdt, idx);
+        st_elem(dx, dxdt, idx, v);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int d = lane + 64 * i;
+    if (d < D) { atomicAdd(&pg[0][d], ag[i]); atomicAdd(&pg[1][d], ab[i]); }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += NT) partial[(int64_t)blockIdx.x * 2 * D + i] = pg[i / D][i % D];
+}
+
+__global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, float* dgamma, float* dbeta) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  double a = 0, b = 0;
+  for (int k = 0; k < nblk; ++k) { a += partial[(int64_t)k * 2 * D + d]; b += partial[(int64_t)k * 2 * D + D + d]; }
+  if (dgamma) dgamma[d] = (float)a;
+  if (dbeta) dbeta[d] = (float)b;
+}
+
+constexpr int LN_ROWS_PER_BLOCK = 256;
+
+}  // namespace
+
+extern "C" int64_t mia_bn_partial_bytes(int64_t P, int32_t C) {
+  if (C < 8 || C % 8) return 0;
+  return (int64_t)MAXBLK * C * 2 * 4;
+}
+
+extern "C" int mia_bn_fwd_stats(const void* x, int32_t dtype, int64_t P, int32_t C, const float* gamma,
+                                const float* beta, float* running_mean, float* running_var, float momentum,
+                                float eps, int32_t training, float* mean, float* invstd, float* scale,
+                                float* shift, void* partial, mia_stream_t stream) {
+  MIA_CHECK_ARG(mean && invstd && scale && shift, "bn_fwd_stats: null output");
+  hipStream_t s = as_stream(stream);
+  if (!training) {
+    MIA_CHECK_ARG(running_mean && running_var, "bn_fwd_stats: eval needs running stats");
+    bn_eval_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>(C, gamma, beta, running_mean, running_var, eps, mean, invstd,
+                                                          scale, shift);
+    MIA_LAUNCH_CHECK("bn_eval");
+    return 0;
+  }
+  if (int r = check_bn(x, dtype, P, C)) return r;
+  MIA_CHECK_ARG(partial != nullptr, "bn_fwd_stats: null partial workspace");
+  const int nb = nblocks_for(P, C);
+  bn_stats_kernel<<<nb, NT, 0, s>>>(x, dtype, P, C, (float*)partial);
+  MIA_LAUNCH_CHECK("bn_stats");
+  bn_finalize_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>(x, dtype, (const float*)partial, nb, P, C, gamma, beta,
+                                                            running_mean, running_var, momentum, eps, mean, invstd,
+                                                            scale, shift);
+  MIA_LAUNCH_CHECK("bn_finalize");
+  return 0;
+}
+
+extern "C" int mia_bn_relu_bwd_reduce(const void* dact, void* dz, const void* x, int32_t dtype, int64_t P,
+                                      int32_t C, const float* scale, const float* shift, const float* mean,
+                                      const float* invstd, float* dgamma, float* dbeta, void* partial,
+                                      mia_stream_t stream) {
+  if (int r = check_bn(x, dtype, P, C)) return r;
+  MIA_CHECK_ARG(dact && dz && scale && shift && mean && invstd && dgamma && dbeta && partial,
+                "bn_relu_bwd_reduce: null pointer");
+  hipStream_t s = as_stream(stream);
+  const int nb = nblocks_for(P, C);
+  bn_relu_bwd_reduce_kernel<<<nb, NT, 0, s>>>(dact, dz, x, dtype, P, C, scale, shift, mean, invstd, (float*)partial);
+  MIA_LAUNCH_CHECK("bn_relu_bwd_reduce");
+  channel_partial_sum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, dgamma, dbeta);
+  MIA_LAUNCH_CHECK("channel_partial_sum");
+  return 0;
+}
+
+extern "C" int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t dtype, int64_t P, int32_t C,
+                                const float* gamma, const float* mean, const float* invstd, const float* dgamma,
+                                const float* dbeta, float* dbias, void* partial, mia_stream_t stream) {
+  if (int r = check_bn(x, dtype, P, C)) return r;
+  MIA_CHECK_ARG(dz && dx && mean && invstd && dgamma && dbeta, "bn_bwd_apply: null pointer");
+  MIA_CHECK_ARG(!dbias || partial, "bn_bwd_apply: dbias needs the partial workspace");
+  const int nb = nblocks_for(P, C);
+  hipStream_t s = as_stream(stream);
+  bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(dz, x, dx, dtype, P, C, gamma, mean, invstd, dgamma, dbeta,
+                                        dbias ? (float*)partial : nullptr);
+  MIA_LAUNCH_CHECK("bn_bwd_apply");
+  if (dbias) {
+    channel_partial_sum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, nullptr, dbias);
+    MIA_LAUNCH_CHECK("channel_partial_sum");
+  }
+  return 0;
+}
+
+extern "C" int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, int64_t ld, float* out, void* partial,
+                          mia_stream_t stream) {
+  MIA_CHECK_ARG(x && out && partial && C > 0 && P > 0 && ld >= C, "colsum: bad arguments");
+  int nb = (int)std::min<int64_t>(P, 256);
+  hipStream_t s = as_stream(stream);
+  colsum_kernel<<<dim3(nb, (unsigned)cdiv(C, NT)), NT, 0, s>>>(x, dtype, P, C, ld, (float*)partial);
+  MIA_LAUNCH_CHECK("colsum");
+  colsum_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, out);
+  MIA_LAUNCH_CHECK("colsum_final");
+  return 0;
+}
+
+extern "C" int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gamma, const float* beta, void* y,
+                                 int32_t ydtype, float* mean, float* rstd, int64_t rows, int32_t D, float eps,
+                                 mia_stream_t stream) {
+  MIA_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
+  MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_fwd: D must be <= 1024");
+  const unsigned nb = (unsigned)cdiv(rows, 4);
+  hipStream_t s = as_stream(stream);
+  if (D <= 768) ln_fwd_kernel<12><<<nb, NT, 0, s>>>(x, xdtype, gamma, beta, y, ydtype, mean, rstd, rows, D, eps);
+  else ln_fwd_kernel<16><<<nb, NT, 0, s>>>(x, xdtype, gamma, beta, y, ydtype, mean, rstd, rows, D, eps);
+  MIA_LAUNCH_CHECK("layernorm_fwd");
+  return 0;
+}
+
+extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
+  return cdiv(rows, LN_ROWS_PER_BLOCK) * 2 * D * 4;
+}
+
+extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
+                                 const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
+                                 float* dgamma, float* dbeta, void* partial, int64_t rows, int32_t D,
+                                 mia_stream_t stream) {
+  MIA_CHECK_ARG(dy && x && gamma && mean && rstd && dx && partial, "layernorm_bwd: null pointer");
+  MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_bwd: D must be <= 1024");
+  const unsigned nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
+  hipStream_t s = as_stream(stream);
+  if (D <= 768)
+    ln_bwd_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                        (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
+  else
+    ln_bwd_kernel<16><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                        (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
+  MIA_LAUNCH_CHECK("layernorm_bwd");
+  ln_partial_final_kernel<<<(unsigned)cdiv(D, 256), 256, 0, s>>>((const float*)partial, (int)nb, D, dgamma, dbeta);
+  MIA_LAUNCH_CHECK("layernorm_partial_final");
+  return 0;
+}

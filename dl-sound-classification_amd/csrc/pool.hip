@@ -1,0 +1,214 @@
+// Max-pool fused with the preceding BatchNorm-apply + ReLU, and its backward (gfx950).
+// nn.MaxPool2d(kernel == stride, floor) after BN+ReLU (envnet_v2.py:16-23, 32-37).
+// The pooled layers never materialise relu(bn(x)): the forward reads the raw conv output once and
+// writes only the pooled map (+ a u8 argmax per output), the backward scatters the pooled
+// gradient through the argmax, masks it with the recomputed ReLU and produces the BN backward
+// reductions in the same pass.  Ties keep the first maximum in row-major window order, like the
+// PyTorch CPU kernel.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ int64_t out_index(int layout, int b, int oy, int ox, int c, int OH, int OW, int C) {
+  if (layout == 0) return (((int64_t)b * OH + oy) * OW + ox) * C + c;
+  if (layout == 1) return ((int64_t)b * C + c) * OW + ox;                 // (n, c, ow), OH == 1
+  return (((int64_t)b * C + c) * OH + oy) * OW + ox;                       // NCHW flat
+}
+
+// one thread = one (output pixel, 8-channel group)
+__global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x, int dtype, int n, int H, int W,
+                                                      int C, int kh, int kw, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, void* out, int layout,
+                                                      uint8_t* __restrict__ argmax) {
+  const int OH = H / kh, OW = W / kw, G = C / 8;
+  const int64_t total = (int64_t)n * OH * OW * G;
+  for (int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * NT) {
+    const int cg = (int)(idx % G);
+    int64_t p = idx / G;
+    const int ox = (int)(p % OW);
+    p /= OW;
+    const int oy = (int)(p % OH);
+    const int b = (int)(p / OH);
+    float sc[8], sh[8], best[8];
+    int arg[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale ? scale[cg * 8 + i] : 1.f;
+      sh[i] = shift ? shift[cg * 8 + i] : 0.f;
+      best[i] = -INFINITY;
+      arg[i] = 0;
+    }
+    for (int dy = 0; dy < kh; ++dy) {
+      const int iy = oy * kh + dy;
+      for (int dx = 0; dx < kw; ++dx) {
+        const int ix = ox * kw + dx;
+        const int64_t off = (((int64_t)b * H + iy) * W + ix) * C + cg * 8;
+        float f[8];
+        if (dtype == MIA_BF16) {
+          uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(x) + off);
+          uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w4[i] << 16); f[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u); }
+        } else {
+          const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
+          float4 a = q[0], c4 = q[1];
+          f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c4.x; f[5] = c4.y; f[6] = c4.z; f[7] = c4.w;
+        }
+        const int pos = dy * kw + dx;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float v = fmaxf(fmaf(f[i], sc[i], sh[i]), 0.f);
+          if (v > best[i]) { best[i] = v; arg[i] = pos; }
+        }
+      }
+    }
+    const int64_t aoff = (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a0 |= (uint32_t)arg[i] << (8 * i); a1 |= (uint32_t)arg[i + 4] << (8 * i); }
+    *reinterpret_cast<uint2*>(argmax + aoff) = make_uint2(a0, a1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st_elem(out, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C), best[i]);
+  }
+}
+
+// one thread = one (input pixel, 8-channel group); block partial reductions like norm.hip
+__global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ dout, int layout,
+                                                      const uint8_t* __restrict__ argmax, const void* __restrict__ x,
+                                                      int dtype, int n, int H, int W, int C, int kh, int kw,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd, void* dz,
+                                                      float* __restrict__ partial) {
+  const int OH = H / kh, OW = W / kw, G = C / 8;
+  const int t = threadIdx.x;
+  const int cg = t % G, rs = t / G, rslots = NT / G;
+  float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[cg * 8 + i]; sh[i] = shift[cg * 8 + i]; mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i];
+  }
+  float s1[8] = {0}, s2[8] = {0};
+  const int64_t P = (int64_t)n * H * W;
+  for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
+    const int ix = (int)(r % W);
+    const int64_t q = r / W;
+    const int iy = (int)(q % H);
+    const int b = (int)(q / H);
+    const int64_t off = r * C + cg * 8;
+    float g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = 0.f;
+    const int oy = iy / kh, ox = ix / kw;
+    if (oy < OH && ox < OW) {
+      const int pos = (iy - oy * kh) * kw + (ix - ox * kw);
+      const int64_t aoff = (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8;
+      const uint2 am = *reinterpret_cast<const uint2*>(argmax + aoff);
+      float xv[8];
+      if (dtype == MIA_BF16) {
+        uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(x) + off);
+        uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { xv[2 * i] = __uint_as_float(w4[i] << 16); xv[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u); }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] = reinterpret_cast<const float*>(x)[off + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t word = i < 4 ? am.x : am.y;
+        const int a = (int)((word >> (8 * (i & 3))) & 0xffu);
+        if (a == pos && fmaf(xv[i], sc[i], sh[i]) > 0.f) {
+          g[i] = ld_elem(dout, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C));
+          s1[i] += g[i];
+          s2[i] = fmaf(g[i], (xv[i] - mu[i]) * is[i], s2[i]);
+        }
+      }
+    }
+    store8(dz, dtype, off, g);
+  }
+  __shared__ float red[NT * 16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[t * 16 + i] = s1[i]; red[t * 16 + 8 + i] = s2[i]; }
+  __syncthreads();
+  for (int e = t; e < 2 * C; e += NT) {
+    const int qq = e / C, c = e % C, g2 = c / 8, ci = c % 8;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < rslots; ++r2) acc += red[(r2 * G + g2) * 16 + qq * 8 + ci];
+    partial[((int64_t)blockIdx.x * C + c) * 2 + qq] = acc;
+  }
+}
+
+__global__ void partial_final_kernel(const float* __restrict__ partial, int nblk, int C, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0, b = 0;
+  for (int k = 0; k < nblk; ++k) { a += partial[((int64_t)k * C + c) * 2]; b += partial[((int64_t)k * C + c) * 2 + 1]; }
+  dbeta[c] = (float)a;
+  dgamma[c] = (float)b;
+}
+
+// out[b][ih][iw] = sum_ky p[b][ih-ky][iw][ky]
+__global__ void col2im_rows_kernel(const float* __restrict__ p, int n, int ph, int w, int kh, void* out, int dtype) {
+  const int H = ph + kh - 1;
+  const int64_t total = (int64_t)n * H * w;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int iw = (int)(idx % w);
+    const int64_t q = idx / w;
+    const int ih = (int)(q % H);
+    const int b = (int)(q / H);
+    float s = 0.f;
+    for (int ky = 0; ky < kh; ++ky) {
+      const int r = ih - ky;
+      if (r >= 0 && r < ph) s += p[(((int64_t)b * ph + r) * w + iw) * kh + ky];
+    }
+    st_elem(out, dtype, idx, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh,
+                            int32_t kw, const float* scale, const float* shift, void* out, int32_t out_layout,
+                            uint8_t* argmax, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && out && argmax, "pool_fwd: null pointer");
+  MIA_CHECK_ARG(c % 8 == 0 && kh > 0 && kw > 0 && kh * kw <= 256 && h >= kh && w >= kw, "pool_fwd: bad geometry");
+  MIA_CHECK_ARG(out_layout >= 0 && out_layout <= 2 && (out_layout != 1 || h / kh == 1), "pool_fwd: bad layout");
+  const int64_t total = (int64_t)n * (h / kh) * (w / kw) * (c / 8);
+  const int nb = (int)std::min<int64_t>(cdiv(total, NT), 16384);
+  pool_fwd_kernel<<<nb, NT, 0, as_stream(stream)>>>(x, dtype, n, h, w, c, kh, kw, scale, shift, out, out_layout, argmax);
+  MIA_LAUNCH_CHECK("pool_fwd");
+  return 0;
+}
+
+extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint8_t* argmax, const void* x,
+                                           int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh,
+                                           int32_t kw, const float* scale, const float* shift, const float* mean,
+                                           const float* invstd, void* dz, float* dgamma, float* dbeta, void* partial,
+                                           mia_stream_t stream) {
+  MIA_CHECK_ARG(dout && argmax && x && scale && shift && mean && invstd && dz && dgamma && dbeta && partial,
+                "pool_bwd: null pointer");
+  MIA_CHECK_ARG(c % 8 == 0 && c >= 8 && (NT % (c / 8)) == 0, "pool_bwd: channels");
+  const int rslots = NT / (c / 8);
+  const int64_t P = (int64_t)n * h * w;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
+  hipStream_t s = as_stream(stream);
+  pool_bwd_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean, invstd,
+                                    dz, (float*)partial);
+  MIA_LAUNCH_CHECK("pool_bwd");
+  partial_final_kernel<<<(unsigned)cdiv(c, 256), 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);
+  MIA_LAUNCH_CHECK("pool_bwd_final");
+  return 0;
+}
+
+extern "C" int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh, void* out, int32_t dtype,
+                               mia_stream_t stream) {
+  MIA_CHECK_ARG(p && out && n > 0 && ph > 0 && w > 0 && kh > 0, "col2im_rows: bad arguments");
+  const int64_t total = (int64_t)n * (ph + kh - 1) * w;
+  const int nb = (int)std::min<int64_t>(cdiv(total, 256), 16384);
+  col2im_rows_kernel<<<nb, 256, 0, as_stream(stream)>>>(p, n, ph, w, kh, out, dtype);
+  MIA_LAUNCH_CHECK("col2im_rows");
+  return 0;
+}

@@ -1,0 +1,36 @@
+// Error reporting + device queries for the C ABI.
+#include <stdarg.h>
+#include "common.h"
+
+namespace {
+thread_local char g_err[1024] = "";
+}
+
+namespace mia {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code < 0 ? code : -1;
+}
+}  // namespace mia
+
+extern "C" const char* mia_last_error_string(void) { return g_err; }
+
+extern "C" int mia_device_arch(char* buf, int32_t len) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return mia::fail(-(int)e, "hipGetDevice: %s", hipGetErrorString(e));
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return mia::fail(-(int)e, "hipGetDeviceProperties: %s", hipGetErrorString(e));
+  snprintf(buf, (size_t)len, "%s", prop.gcnArchName);
+  return 0;
+}

@@ -1,0 +1,248 @@
+"""Tensor-level wrappers over the C ABI (one function per kernel family).
+
+Every call enqueues on ``torch.cuda.current_stream()``; torch allocates all memory (outputs and
+workspaces).  Shapes are validated here, geometry is validated again in the library.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import lib as L
+
+_WS: dict = {}
+
+
+def workspace(nbytes: int, device, slot: str = "main") -> torch.Tensor:
+    """Stream-ordered scratch buffer reused across calls (grown on demand)."""
+    key = (str(device), slot)
+    buf = _WS.get(key)
+    nbytes = max(int(nbytes), 256)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _s():
+    return L.stream_ptr()
+
+
+# ------------------------------------------------------------------------------------ GEMM
+def dense(t: torch.Tensor, layout: int, rows: int, cols: int, ld: int | None = None,
+          pre: int = L.PRE_NONE, scale=None, shift=None, dtype: int | None = None) -> L.MiaOperand:
+    o = L.MiaOperand()
+    o.ptr = t.data_ptr()
+    o.kind = L.OP_DENSE
+    o.dtype = L.dtype_code(t) if dtype is None else dtype
+    o.layout = layout
+    o.pre = pre
+    o.rows, o.cols, o.ld = rows, cols, cols if ld is None else ld
+    o.pre_scale = L.ptr(scale)
+    o.pre_shift = L.ptr(shift)
+    o._keep = (t, scale, shift)  # the descriptor owns its tensors until the launch is enqueued
+    return o
+
+
+def conv(t: torch.Tensor, layout: int, n, h, w, c, oh, ow, kh, kw, sh=1, sw=1, ph=0, pw=0,
+         pre: int = L.PRE_NONE, scale=None, shift=None, row_kind: bool = False) -> L.MiaOperand:
+    o = L.MiaOperand()
+    o.ptr = t.data_ptr()
+    o.kind = L.OP_CONVROW if row_kind else L.OP_CONV
+    o.dtype = L.dtype_code(t)
+    o.layout = layout
+    o.pre = pre
+    o.n, o.h, o.w, o.c = n, h, w, c
+    o.oh, o.ow, o.kh, o.kw = oh, ow, kh, kw
+    o.sh, o.sw, o.ph, o.pw = sh, sw, ph, pw
+    o.pre_scale = L.ptr(scale)
+    o.pre_shift = L.ptr(shift)
+    o._keep = (t, scale, shift)
+    return o
+
+
+def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=None, ldaux: int = 0,
+             accumulate: bool = False, alpha: float = 1.0, act_scale: float = 1.0,
+             rowmap=None) -> L.MiaEpilogue:
+    e = L.MiaEpilogue()
+    e.ptr = out.data_ptr()
+    e.dtype = L.dtype_code(out)
+    e.act = act
+    e.accumulate = int(accumulate)
+    e.ldc = ldc
+    if rowmap is not None:
+        e.rm_inner, e.rm_outer, e.rm_istride, e.rm_offset = rowmap
+    e.bias = L.ptr(bias)
+    if aux is not None:
+        e.aux = aux.data_ptr()
+        e.aux_dtype = L.dtype_code(aux)
+        e.ldaux = ldaux
+    e.alpha = alpha
+    e.act_scale = act_scale
+    e._keep = (out, bias, aux)
+    return e
+
+
+def _tiles(M, N):
+    if M <= 32:
+        bm, bn = 32, 128
+    elif N <= 32:
+        bm, bn = 256, 32
+    elif N <= 64:
+        bm, bn = 128, 64
+    elif M <= 64:
+        bm, bn = 64, 128
+    else:
+        bm, bn = 128, 128
+    return math.ceil(M / bm) * math.ceil(N / bn)
+
+
+def auto_split(M: int, N: int, K: int, target_blocks: int = 1024, min_k: int = 1024) -> int:
+    tiles = _tiles(M, N)
+    if tiles >= target_blocks:
+        return 1
+    split = math.ceil(target_blocks / tiles)
+    split = min(split, max(1, K // min_k))
+    return max(1, min(split, 256))
+
+
+# Live kernel probe (bench.py): tag -> list of (start_event, end_event, flops, bytes).
+PROBE: dict | None = None
+
+
+def _operand_bytes(o: L.MiaOperand, M_or_N: int, K: int) -> int:
+    es = 4 if o.dtype == L.F32 else 2
+    if o.kind == L.OP_DENSE:
+        return o.rows * o.cols * es
+    return o.n * o.h * o.w * o.c * es  # each input element is read once from HBM (tile reuse on chip)
+
+
+def gemm(A: L.MiaOperand, B: L.MiaOperand, E: L.MiaEpilogue, M: int, N: int, K: int, compute: int,
+         split_k: int | None = None, device=None, tag: str | None = None):
+    if split_k is None:
+        split_k = auto_split(M, N, K)
+    lib = L.load()
+    ws = None
+    if split_k > 1:
+        ws = workspace(lib.mia_gemm_workspace_bytes(M, N, split_k), device or torch.cuda.current_device(), "gemm")
+    rec = PROBE is not None and tag in PROBE
+    if rec:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    L.check(lib.mia_gemm(A, B, E, M, N, K, compute, split_k, L.ptr(ws), _s()), "mia_gemm")
+    if rec:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        out_b = M * N * (4 if E.dtype == L.F32 else 2)
+        PROBE[tag].append((e0, e1, 2 * M * N * K, _operand_bytes(A, M, K) + _operand_bytes(B, N, K) + out_b))
+
+
+# ------------------------------------------------------------------------------------ BN / pool
+@dataclass
+class BNState:
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+
+
+def bn_fwd_stats(x: torch.Tensor, P: int, C: int, gamma, beta, running_mean, running_var, momentum: float,
+                 eps: float, training: bool) -> BNState:
+    dev = x.device
+    st = torch.empty(4, C, dtype=torch.float32, device=dev)
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(P, C), dev, "bn")
+    L.check(lib.mia_bn_fwd_stats(x.data_ptr(), L.dtype_code(x), P, C, L.ptr(gamma), L.ptr(beta),
+                                 L.ptr(running_mean), L.ptr(running_var), momentum, eps, int(training),
+                                 st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(),
+                                 ws.data_ptr(), _s()), "mia_bn_fwd_stats")
+    return BNState(st[0], st[1], st[2], st[3])
+
+
+def bn_relu_bwd_reduce(dact, dz, x, P, C, bn: BNState):
+    dev = x.device
+    g = torch.empty(2, C, dtype=torch.float32, device=dev)
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(P, C), dev, "bn")
+    L.check(lib.mia_bn_relu_bwd_reduce(dact.data_ptr(), dz.data_ptr(), x.data_ptr(), L.dtype_code(x), P, C,
+                                       bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
+                                       bn.invstd.data_ptr(), g[0].data_ptr(), g[1].data_ptr(), ws.data_ptr(),
+                                       _s()), "mia_bn_relu_bwd_reduce")
+    return g[0], g[1]  # dgamma, dbeta
+
+
+def bn_bwd_apply(dz, x, dx, P, C, gamma, bn: BNState, dgamma, dbeta, dbias=None):
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(P, C), x.device, "bn")
+    L.check(lib.mia_bn_bwd_apply(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), L.dtype_code(x), P, C,
+                                 L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(), dgamma.data_ptr(),
+                                 dbeta.data_ptr(), L.ptr(dbias), ws.data_ptr(), _s()), "mia_bn_bwd_apply")
+
+
+def pool_fwd(x, n, h, w, c, kh, kw, bn: BNState, out, out_layout, argmax):
+    L.check(L.load().mia_pool_fwd(x.data_ptr(), L.dtype_code(x), n, h, w, c, kh, kw, bn.scale.data_ptr(),
+                                  bn.shift.data_ptr(), out.data_ptr(), out_layout, argmax.data_ptr(), _s()),
+            "mia_pool_fwd")
+
+
+def pool_bwd_bn_relu_reduce(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn: BNState, dz):
+    g = torch.empty(2, c, dtype=torch.float32, device=x.device)
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(n * h * w, c), x.device, "bn")
+    L.check(lib.mia_pool_bwd_bn_relu_reduce(dout.data_ptr(), out_layout, argmax.data_ptr(), x.data_ptr(),
+                                            L.dtype_code(x), n, h, w, c, kh, kw, bn.scale.data_ptr(),
+                                            bn.shift.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                            dz.data_ptr(), g[0].data_ptr(), g[1].data_ptr(), ws.data_ptr(), _s()),
+            "mia_pool_bwd_bn_relu_reduce")
+    return g[0], g[1]
+
+
+def colsum(x, P, C, ld=None):
+    out = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = workspace(256 * C * 4, x.device, "colsum")
+    L.check(L.load().mia_colsum(x.data_ptr(), L.dtype_code(x), P, C, C if ld is None else ld, out.data_ptr(),
+                                ws.data_ptr(), _s()), "mia_colsum")
+    return out
+
+
+def col2im_rows(p, n, ph, w, kh, out):
+    L.check(L.load().mia_col2im_rows(p.data_ptr(), n, ph, w, kh, out.data_ptr(), L.dtype_code(out), _s()),
+            "mia_col2im_rows")
+
+
+def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:
+    cout, cin, kh, kw = src.shape
+    out = torch.empty(src.numel(), dtype=L.torch_dtype(dtype), device=src.device)
+    L.check(L.load().mia_pack_weight(src.data_ptr(), out.data_ptr(), dtype, cout, cin, kh, kw, mode, _s()),
+            "mia_pack_weight")
+    return out
+
+
+def unpack_ohwi_grad(src_ohwi: torch.Tensor, shape, out: torch.Tensor):
+    cout, cin, kh, kw = shape
+    L.check(L.load().mia_pack_weight(src_ohwi.data_ptr(), out.data_ptr(), L.F32, cout, cin, kh, kw, 4, _s()),
+            "mia_pack_weight(grad)")
+
+
+def dropout_(x: torch.Tensor, p: float, seed: int):
+    L.check(L.load().mia_dropout(x.data_ptr(), L.dtype_code(x), x.numel(), p, seed & ((1 << 64) - 1), _s()),
+            "mia_dropout")
+
+
+def soft_ce(logits: torch.Tensor, y: torch.Tensor, input_sigmoid: bool):
+    B, C = logits.shape
+    loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+    correct = torch.empty(1, dtype=torch.int32, device=logits.device)
+    dlogits = torch.empty_like(logits)
+    L.check(L.load().mia_soft_ce(logits.data_ptr(), y.data_ptr(), B, C, int(input_sigmoid), loss.data_ptr(),
+                                 dlogits.data_ptr(), correct.data_ptr(), _s()), "mia_soft_ce")
+    return loss[0], dlogits, correct[0]
+
+
+def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    out = torch.empty(src.shape, dtype=dtype, device=src.device)
+    L.check(L.load().mia_cast(src.data_ptr(), L.dtype_code(src), out.data_ptr(), L.dtype_code(out), src.numel(),
+                              _s()), "mia_cast")
+    return out

@@ -1,0 +1,348 @@
+"""EnvNet-v2 forward/backward on the MI355X kernels (one autograd node for the whole network).
+
+Data layout in HBM (B = batch):
+  x            (B, T) f32 waveform                       — read by conv1 as an NWC view with C=2
+  y1 / y2      (B*W1, 32) / (B*W2, 64) raw conv outputs  — channels-last, compute dtype
+  X0           (B, 64, 860)  pooled frontend, written transposed (= envnet_v2.py:82 transpose(1,2))
+  ya_k / yb_k  (B, H, W, C) raw trunk conv outputs       — NHWC
+  p_k          pooled trunk maps (NHWC; the last one NCHW-flat = nn.Flatten order)
+  h1, h2       (B, 4096) post-ReLU/dropout FC activations
+BatchNorm apply + ReLU is never materialised: it is fused into the next conv's operand loader
+(MIA_PRE_AFFINE_RELU) or into the pool kernel.  Backward recomputes it from the raw outputs.
+Reference op sequence: src/models/envnet_v2.py:14-85.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+
+from ..miaudio import kernels as K
+from ..miaudio import lib as L
+
+_SEED = itertools.count(0x5EED)
+
+# (conv module path, bn module path, cin, cout, kh, kw)
+TRUNK = [
+    (("trunk", 0, 0), ("trunk", 0, 1), 1, 32, 8, 8),
+    (("trunk", 0, 3), ("trunk", 0, 4), 32, 32, 8, 8),
+    (("trunk", 1, 0), ("trunk", 1, 1), 32, 64, 1, 4),
+    (("trunk", 1, 3), ("trunk", 1, 4), 64, 64, 1, 4),
+    (("trunk", 2, 0), ("trunk", 2, 1), 64, 128, 1, 2),
+    (("trunk", 2, 3), ("trunk", 2, 4), 128, 128, 1, 2),
+    (("trunk", 3, 0), ("trunk", 3, 1), 128, 256, 1, 2),
+    (("trunk", 3, 3), ("trunk", 3, 4), 256, 256, 1, 2),
+]
+TRUNK_POOL = [(5, 3), (1, 2), (1, 2), (1, 2)]
+
+
+def geometry(T: int):
+    W1 = (T - 64) // 2 + 1
+    W2 = (W1 - 16) // 2 + 1
+    Wp = W2 // 64
+    g = {"T": T, "W1": W1, "W2": W2, "Wp": Wp, "trunk": []}
+    H, W = 64, Wp
+    for blk in range(4):
+        ka = TRUNK[2 * blk]
+        ha, wa = H - ka[4] + 1, W - ka[5] + 1
+        kb = TRUNK[2 * blk + 1]
+        hb, wb = ha - kb[4] + 1, wa - kb[5] + 1
+        ph, pw = TRUNK_POOL[blk]
+        g["trunk"].append(((H, W), (ha, wa), (hb, wb), (hb // ph, wb // pw)))
+        H, W = hb // ph, wb // pw
+    g["flat"] = 256 * H * W
+    return g
+
+
+def _param_list(m):
+    """Flat parameter order handed to the autograd Function (also the grad order)."""
+    ps = [m.frontend[0].weight, m.frontend[0].bias, m.frontend[1].weight, m.frontend[1].bias,
+          m.frontend[3].weight, m.frontend[3].bias, m.frontend[4].weight, m.frontend[4].bias]
+    for blk in range(4):
+        seq = m.trunk[blk]
+        ps += [seq[0].weight, seq[0].bias, seq[1].weight, seq[1].bias,
+               seq[3].weight, seq[3].bias, seq[4].weight, seq[4].bias]
+    for idx in (1, 4, 7):
+        ps += [m.classifier[idx].weight, m.classifier[idx].bias]
+    return ps
+
+
+def _bns(m):
+    out = [m.frontend[1], m.frontend[4]]
+    for blk in range(4):
+        out += [m.trunk[blk][1], m.trunk[blk][4]]
+    return out
+
+
+class EnvNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, x, compute: int, *params):
+        if not x.is_cuda:
+            raise RuntimeError("EnvNetV2 runs on the MI355X HIP kernels only (input is on CPU)")
+        B = x.shape[0]
+        x = x.reshape(B, -1).contiguous().float()
+        T = x.shape[1]
+        if T % 2:
+            raise ValueError(f"EnvNetV2 expects an even clip length (got {T})")
+        g = geometry(T)
+        if g["flat"] != model.classifier[1].in_features:
+            raise ValueError(f"clip length {T} gives {g['flat']} trunk features, FC1 expects "
+                             f"{model.classifier[1].in_features} (envnet_v2.py:51)")
+        training = model.training
+        cd = compute
+        tdt = L.torch_dtype(cd)
+        dev = x.device
+        bns = _bns(model)
+        p = params
+        W1, W2, Wp = g["W1"], g["W2"], g["Wp"]
+        saved = {"g": g, "B": B, "cd": cd}
+
+        def bn(i, y, P, C):
+            mod = bns[i]
+            return K.bn_fwd_stats(y, P, C, mod.weight, mod.bias, mod.running_mean, mod.running_var,
+                                  mod.momentum if mod.momentum is not None else 0.1, mod.eps, training)
+
+        # ---- frontend conv1: CONVROW over the (B, T/2, 2) view of the waveform
+        w1 = K.pack_weight(p[0], cd, 0)
+        y1 = torch.empty(B * W1, 32, dtype=tdt, device=dev)
+        A = K.conv(x, L.KC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
+        Bo = K.dense(w1, L.KC, 32, 64)
+        K.gemm(A, Bo, K.epilogue(y1, 32, bias=p[1]), B * W1, 32, 64, cd, tag="conv1.fwd")
+        bn1 = bn(0, y1, B * W1, 32)
+        # ---- conv2 (stride 2) with BN1+ReLU fused into the operand load
+        w2 = K.pack_weight(p[4], cd, 0)
+        y2 = torch.empty(B * W2, 64, dtype=tdt, device=dev)
+        A = K.conv(y1, L.KC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU, scale=bn1.scale,
+                   shift=bn1.shift)
+        K.gemm(A, K.dense(w2, L.KC, 64, 512), K.epilogue(y2, 64, bias=p[5]), B * W2, 64, 512, cd,
+               tag="conv2.fwd")
+        bn2 = bn(1, y2, B * W2, 64)
+        # ---- maxpool (1,64) of relu(bn2(y2)), written as the transposed trunk image (B, 64, Wp)
+        X0 = torch.empty(B, 64, Wp, dtype=tdt, device=dev)
+        am0 = torch.empty(B, Wp, 64, dtype=torch.uint8, device=dev)
+        K.pool_fwd(y2, B, 1, W2, 64, 1, 64, bn2, X0, 1, am0)
+        saved.update(x=x, y1=y1, y2=y2, bn1=bn1, bn2=bn2, X0=X0, am0=am0)
+
+        # ---- trunk
+        inp = X0
+        trunk_saved = []
+        for blk in range(4):
+            (H, W), (ha, wa), (hb, wb), (hp, wp) = g["trunk"][blk]
+            _, _, cin, cout, kh, kw = TRUNK[2 * blk]
+            pa = 8 + 8 * blk
+            wa_ = K.pack_weight(p[pa], cd, 0)
+            ya = torch.empty(B * ha * wa, cout, dtype=tdt, device=dev)
+            if cin == 1:
+                A = K.conv(inp, L.KC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+            else:
+                A = K.conv(inp, L.KC, B, H, W, cin, ha, wa, kh, kw)
+            K.gemm(A, K.dense(wa_, L.KC, cout, kh * kw * cin), K.epilogue(ya, cout, bias=p[pa + 1]),
+                   B * ha * wa, cout, kh * kw * cin, cd, tag=f"t{blk}a.fwd")
+            bna = bn(2 + 2 * blk, ya, B * ha * wa, cout)
+            _, _, cin2, cout2, kh2, kw2 = TRUNK[2 * blk + 1]
+            wb_ = K.pack_weight(p[pa + 4], cd, 0)
+            yb = torch.empty(B * hb * wb, cout2, dtype=tdt, device=dev)
+            A = K.conv(ya, L.KC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU, scale=bna.scale,
+                       shift=bna.shift)
+            K.gemm(A, K.dense(wb_, L.KC, cout2, kh2 * kw2 * cin2), K.epilogue(yb, cout2, bias=p[pa + 5]),
+                   B * hb * wb, cout2, kh2 * kw2 * cin2, cd, tag=f"t{blk}b.fwd")
+            bnb = bn(3 + 2 * blk, yb, B * hb * wb, cout2)
+            ph, pw = TRUNK_POOL[blk]
+            last = blk == 3
+            pooled = torch.empty(B, cout2, hp, wp, dtype=tdt, device=dev) if last else \
+                torch.empty(B, hp, wp, cout2, dtype=tdt, device=dev)
+            am = torch.empty(B, hp, wp, cout2, dtype=torch.uint8, device=dev)
+            K.pool_fwd(yb, B, hb, wb, cout2, ph, pw, bnb, pooled, 2 if last else 0, am)
+            trunk_saved.append(dict(inp=inp, ya=ya, yb=yb, bna=bna, bnb=bnb, am=am))
+            inp = pooled
+        flat = inp.reshape(B, -1)
+        saved["trunk"] = trunk_saved
+        saved["flat"] = flat
+
+        # ---- classifier (FC weights streamed as f32 and converted while staging)
+        drop_p = model.classifier[3].p if training else 0.0
+        h = flat
+        hs = []
+        for li, idx in enumerate((1, 4, 7)):
+            Wt, bias = p[40 + 2 * li], p[41 + 2 * li]
+            fout, fin = Wt.shape
+            last = li == 2
+            out = torch.empty(B, fout, dtype=torch.float32 if last else tdt, device=dev)
+            K.gemm(K.dense(h, L.KC, B, fin), K.dense(Wt, L.KC, fout, fin),
+                   K.epilogue(out, fout, act=L.ACT_NONE if last else L.ACT_RELU, bias=bias), B, fout, fin, cd,
+                   tag=f"fc{li + 1}.fwd")
+            if not last and drop_p > 0:
+                K.dropout_(out, drop_p, next(_SEED) * 0x9E3779B1)
+            hs.append(out)
+            h = out
+        saved["h1"], saved["h2"] = hs[0], hs[1]
+        saved["drop_p"] = drop_p
+        if getattr(model, "_debug_capture", False):
+            model._debug = saved
+        ctx.saved = saved
+        ctx.model = model
+        ctx.params = params
+        return hs[2]
+
+    @staticmethod
+    def backward(ctx, glogits):
+        s = ctx.saved
+        p = ctx.params
+        g = s["g"]
+        B, cd = s["B"], s["cd"]
+        tdt = L.torch_dtype(cd)
+        dev = glogits.device
+        bns = _bns(ctx.model)
+        grads = [None] * len(p)
+        glogits = glogits.contiguous().float()
+        keep_scale = 1.0 / (1.0 - s["drop_p"]) if s["drop_p"] > 0 else 1.0
+        ready = getattr(ctx.model, "_grad_ready", None)
+
+        def emit(lo, hi):
+            # hand finished gradients to the data-parallel reducer now (overlaps the rest of the
+            # backward); autograd then gets None for them so it does not accumulate twice
+            if ready is None:
+                return
+            ready([(p[i], grads[i]) for i in range(lo, hi)])
+            for i in range(lo, hi):
+                grads[i] = None
+
+        # ---- classifier backward
+        acts = [s["flat"], s["h1"], s["h2"]]
+        dcur = glogits
+        for li in (2, 1, 0):
+            Wt = p[40 + 2 * li]
+            fout, fin = Wt.shape
+            hin = acts[li]
+            dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
+            K.gemm(K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), K.epilogue(dW, fin), fout, fin, B, cd,
+                   tag=f"fc{li + 1}.wgrad")
+            grads[40 + 2 * li] = dW
+            grads[41 + 2 * li] = K.colsum(dcur, B, fout)
+            if li > 0:
+                dprev = torch.empty(B, fin, dtype=tdt, device=dev)
+                K.gemm(K.dense(dcur, L.KC, B, fout), K.dense(Wt, L.RC, fout, fin),
+                       K.epilogue(dprev, fin, act=L.DACT_NZ, aux=hin, ldaux=fin, act_scale=keep_scale),
+                       B, fin, fout, cd, tag=f"fc{li + 1}.dgrad")
+            else:
+                dprev = torch.empty(B, fin, dtype=tdt, device=dev)
+                K.gemm(K.dense(dcur, L.KC, B, fout), K.dense(Wt, L.RC, fout, fin), K.epilogue(dprev, fin),
+                       B, fin, fout, cd, tag=f"fc{li + 1}.dgrad")
+            dcur = dprev
+            emit(40 + 2 * li, 42 + 2 * li)
+
+        # ---- trunk backward
+        dpool = dcur  # (B, 84480) in NCHW-flat order of the last pool
+        for blk in (3, 2, 1, 0):
+            ts = s["trunk"][blk]
+            (H, W), (ha, wa), (hb, wb), (hp, wp) = g["trunk"][blk]
+            _, _, cin, cout, kh, kw = TRUNK[2 * blk]
+            _, _, cin2, cout2, kh2, kw2 = TRUNK[2 * blk + 1]
+            pa = 8 + 8 * blk
+            ph, pw = TRUNK_POOL[blk]
+            Pb = B * hb * wb
+            dzb = torch.empty(Pb, cout2, dtype=tdt, device=dev)
+            dgb, dbb = K.pool_bwd_bn_relu_reduce(dpool, 2 if blk == 3 else 0, ts["am"], ts["yb"], B, hb, wb, cout2,
+                                                 ph, pw, ts["bnb"], dzb)
+            grads[pa + 6], grads[pa + 7] = dgb, dbb
+            dyb = dzb  # in place: dy overwrites dz
+            dbias_b = torch.empty(cout2, dtype=torch.float32, device=dev)
+            K.bn_bwd_apply(dzb, ts["yb"], dyb, Pb, cout2, bns[3 + 2 * blk].weight, ts["bnb"], dgb, dbb, dbias_b)
+            grads[pa + 5] = dbias_b
+            # wgrad b: dW[co][(ky,kx,ci)] = sum_pix dyb[pix][co] * relu(bn_a(ya))[pix + tap][ci]
+            Kb = kh2 * kw2 * cin2
+            dWb = torch.empty(cout2, Kb, dtype=torch.float32, device=dev)
+            K.gemm(K.dense(dyb, L.RC, Pb, cout2),
+                   K.conv(ts["ya"], L.RC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU,
+                          scale=ts["bna"].scale, shift=ts["bna"].shift),
+                   K.epilogue(dWb, Kb), cout2, Kb, Pb, cd, tag=f"t{blk}b.wgrad")
+            gwb = torch.empty_like(p[pa + 4])
+            K.unpack_ohwi_grad(dWb, p[pa + 4].shape, gwb)
+            grads[pa + 4] = gwb
+            # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
+            Pa = B * ha * wa
+            wbf = K.pack_weight(p[pa + 4], cd, 1)
+            da = torch.empty(Pa, cout, dtype=tdt, device=dev)
+            Kdb = kh2 * kw2 * cout2
+            K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
+                   K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd, tag=f"t{blk}b.dgrad")
+            dga, dba = K.bn_relu_bwd_reduce(da, da, ts["ya"], Pa, cout, ts["bna"])
+            grads[pa + 2], grads[pa + 3] = dga, dba
+            dbias_a = torch.empty(cout, dtype=torch.float32, device=dev)
+            K.bn_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba, dbias_a)
+            grads[pa + 1] = dbias_a
+            dya = da
+            # wgrad a
+            Ka = kh * kw * cin
+            dWa = torch.empty(cout, Ka, dtype=torch.float32, device=dev)
+            if cin == 1:
+                Bop = K.conv(ts["inp"], L.RC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+            else:
+                Bop = K.conv(ts["inp"], L.RC, B, H, W, cin, ha, wa, kh, kw)
+            K.gemm(K.dense(dya, L.RC, Pa, cout), Bop, K.epilogue(dWa, Ka), cout, Ka, Pa, cd, tag=f"t{blk}a.wgrad")
+            gwa = torch.empty_like(p[pa])
+            K.unpack_ohwi_grad(dWa, p[pa].shape, gwa)
+            grads[pa] = gwa
+            # dgrad a -> gradient of the block input (pooled map of the previous stage)
+            if cin == 1:
+                # 1-channel 8x8 conv: P[b][r][iw][ky] = sum_{j,co} dya[b][r][iw+j-7][co] W[co][0][ky][7-j]
+                wr = K.pack_weight(p[pa], cd, 3)
+                Pm = torch.empty(B * ha * W, kh, dtype=torch.float32, device=dev)
+                K.gemm(K.conv(dya, L.KC, B, ha, wa, cout, ha, W, 1, kw, pw=kw - 1),
+                       K.dense(wr, L.KC, kh, kw * cout), K.epilogue(Pm, kh), B * ha * W, kh, kw * cout, cd,
+                       tag=f"t{blk}a.dgrad")
+                dinp = torch.empty(B, H, W, dtype=tdt, device=dev)
+                K.col2im_rows(Pm, B, ha, W, kh, dinp)
+            else:
+                waf = K.pack_weight(p[pa], cd, 1)
+                dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
+                Kda = kh * kw * cout
+                K.gemm(K.conv(dya, L.KC, B, ha, wa, cout, H, W, kh, kw, ph=kh - 1, pw=kw - 1),
+                       K.dense(waf, L.KC, cin, Kda), K.epilogue(dinp, cin), B * H * W, cin, Kda, cd,
+                       tag=f"t{blk}a.dgrad")
+            dpool = dinp
+            emit(pa, pa + 8)
+
+        # ---- frontend backward
+        W1, W2, Wp = g["W1"], g["W2"], g["Wp"]
+        P2, P1 = B * W2, B * W1
+        dz2 = torch.empty(P2, 64, dtype=tdt, device=dev)
+        dg2, db2 = K.pool_bwd_bn_relu_reduce(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"], dz2)
+        grads[6], grads[7] = dg2, db2
+        dbias2 = torch.empty(64, dtype=torch.float32, device=dev)
+        K.bn_bwd_apply(dz2, s["y2"], dz2, P2, 64, bns[1].weight, s["bn2"], dg2, db2, dbias2)
+        grads[5] = dbias2
+        dy2 = dz2
+        dW2 = torch.empty(64, 512, dtype=torch.float32, device=dev)
+        K.gemm(K.dense(dy2, L.RC, P2, 64),
+               K.conv(s["y1"], L.RC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU,
+                      scale=s["bn1"].scale, shift=s["bn1"].shift),
+               K.epilogue(dW2, 512), 64, 512, P2, cd, tag="conv2.wgrad")
+        gw2 = torch.empty_like(p[4])
+        K.unpack_ohwi_grad(dW2, p[4].shape, gw2)
+        grads[4] = gw2
+        # stride-2 dgrad as two stride-1 parity convolutions
+        wpar = K.pack_weight(p[4], cd, 2).view(2, 32 * 8 * 64)
+        da1 = torch.empty(P1, 32, dtype=tdt, device=dev)
+        for par in (0, 1):
+            Tp = (W1 - par + 1) // 2
+            K.gemm(K.conv(dy2, L.KC, B, 1, W2, 64, 1, Tp, 1, 8, pw=7),
+                   K.dense(wpar[par], L.KC, 32, 512),
+                   K.epilogue(da1, 32, rowmap=(Tp, W1, 2, par)), B * Tp, 32, 512, cd, tag="conv2.dgrad")
+        dg1, db1 = K.bn_relu_bwd_reduce(da1, da1, s["y1"], P1, 32, s["bn1"])
+        grads[2], grads[3] = dg1, db1
+        dbias1 = torch.empty(32, dtype=torch.float32, device=dev)
+        K.bn_bwd_apply(da1, s["y1"], da1, P1, 32, bns[0].weight, s["bn1"], dg1, db1, dbias1)
+        grads[1] = dbias1
+        dW1 = torch.empty(32, 64, dtype=torch.float32, device=dev)
+        T = g["T"]
+        K.gemm(K.dense(da1, L.RC, P1, 32), K.conv(s["x"], L.RC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True),
+               K.epilogue(dW1, 64), 32, 64, P1, cd, tag="conv1.wgrad")
+        grads[0] = dW1.view_as(p[0])
+        emit(0, 8)
+        ctx.saved = None
+        return (None, None, None, *grads)
+
+
+def envnet_forward(model, x, compute: int):
+    return EnvNetFunction.apply(model, x, compute, *_param_list(model))

@@ -1,0 +1,79 @@
+"""EnvNet-v2 — drop-in for the reference ``src.models.envnet_v2.EnvNetV2``.
+
+Same Hydra target (configs/model/envnet_v2.yaml:10), same constructor kwargs
+(num_classes, dropout), same module tree and parameter names (so state_dicts interchange),
+same default-init -> ``_init_weights`` -> ``replace_head`` order (reference
+src/models/envnet_v2.py:10-90), same forward contract (B,1,T) or (B,1,1,T) -> (B, C) logits.
+The computation runs through the MI355X kernels in ``envnet_hip`` as one autograd node; there
+is no CPU path (inputs on the CPU raise).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..miaudio import lib as L
+from .envnet_hip import envnet_forward
+
+
+class EnvNetV2(nn.Module):
+    def __init__(self, num_classes: int = 50, dropout: float = 0.5, compute_dtype: str | None = None):
+        super().__init__()
+
+        def cbr(cin, cout, k, s=(1, 1)):
+            return [nn.Conv2d(cin, cout, kernel_size=k, stride=s), nn.BatchNorm2d(cout), nn.ReLU(inplace=True)]
+
+        self.frontend = nn.Sequential(*cbr(1, 32, (1, 64), (1, 2)), *cbr(32, 64, (1, 16), (1, 2)),
+                                      nn.MaxPool2d(kernel_size=(1, 64), stride=(1, 64)))
+
+        def block(cin, cout, k1, k2, pk):
+            return nn.Sequential(*cbr(cin, cout, k1), *cbr(cout, cout, k2), nn.MaxPool2d(pk, pk))
+
+        self.trunk = nn.Sequential(
+            block(1, 32, (8, 8), (8, 8), (5, 3)),
+            block(32, 64, (1, 4), (1, 4), (1, 2)),
+            block(64, 128, (1, 2), (1, 2), (1, 2)),
+            block(128, 256, (1, 2), (1, 2), (1, 2)),
+        )
+        self.classifier = nn.Sequential(
+            nn.Flatten(),
+            nn.Linear(256 * 10 * 33, 4096), nn.ReLU(inplace=True), nn.Dropout(dropout),
+            nn.Linear(4096, 4096), nn.ReLU(inplace=True), nn.Dropout(dropout),
+            nn.Linear(4096, num_classes),
+        )
+        self.compute_dtype = compute_dtype  # None: follow autocast (bf16) else f32
+        self._init_weights()
+
+    def _init_weights(self):
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.Linear):
+                nn.init.normal_(m.weight, mean=0.0, std=1.0 / math.sqrt(m.in_features))
+                nn.init.zeros_(m.bias)
+
+    def _compute_code(self) -> int:
+        cd = self.compute_dtype
+        if cd is None:
+            if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+                return L.BF16
+            return L.F32
+        return {"bf16": L.BF16, "bfloat16": L.BF16, "f32": L.F32, "fp32": L.F32, "32": L.F32}[str(cd)]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.ndim == 3:
+            x = x.unsqueeze(2)
+        if x.ndim != 4 or x.shape[1] != 1 or x.shape[2] != 1:
+            raise ValueError(f"EnvNetV2 expects (B,1,T) or (B,1,1,T), got {tuple(x.shape)}")
+        with torch.autocast("cuda", enabled=False):
+            return envnet_forward(self, x, self._compute_code())
+
+    def replace_head(self, num_classes: int) -> None:
+        in_feat = self.classifier[-1].in_features
+        self.classifier[-1] = nn.Linear(in_feat, num_classes).to(next(self.parameters()).device)

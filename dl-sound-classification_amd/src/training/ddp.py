@@ -1,0 +1,106 @@
+"""Data-parallel gradient exchange over RCCL (torch.distributed "nccl" backend = RCCL on ROCm).
+
+Replaces what Lightning's DDPStrategy -> torch DistributedDataParallel does on the reference path
+(configs/base_training.yaml:47-49, scripts/train.py:190-194): rank-0 parameter broadcast at wrap
+time, per-step fp32 gradient all-reduce averaged over ranks, and ``broadcast_buffers`` of the
+BatchNorm running statistics (BN itself stays per-rank: no SyncBN, as in the reference).
+
+Gradients are exchanged in buckets on a dedicated communication stream.  Models whose backward
+reports gradients as they become ready (EnvNetV2 does, through ``model._grad_ready``) get their
+buckets launched during the backward, so the transfer of the FC-head gradients (1.4 GB for
+EnvNet) overlaps the convolution backward; everything else is flushed in ``finish()``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+BUCKET_BYTES = 64 << 20
+
+
+class GradAllReducer:
+    def __init__(self, model: torch.nn.Module, world: int | None = None, bucket_bytes: int = BUCKET_BYTES,
+                 broadcast_buffers: bool = True):
+        self.model = model
+        self.world = world or dist.get_world_size()
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.bucket_bytes = bucket_bytes
+        self.broadcast_buffers = broadcast_buffers
+        self.cuda = self.params[0].is_cuda
+        self.stream = torch.cuda.Stream(self.params[0].device) if self.cuda else None
+        self.pending = []
+        self.done = set()
+        with torch.no_grad():
+            for p in self.params:
+                dist.broadcast(p.data, 0)
+            for b in model.buffers():
+                dist.broadcast(b.data, 0)
+        model._grad_ready = self.grad_ready
+
+    # ------------------------------------------------------------------ async launches
+    def _launch(self, tensors):
+        if self.cuda:
+            ev = torch.cuda.current_stream().record_event()
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                work = self._reduce(tensors)
+            for t in tensors:
+                t.record_stream(self.stream)
+        else:
+            work = self._reduce(tensors)
+        self.pending.append(work)
+
+    def _reduce(self, tensors):
+        if len(tensors) == 1:
+            flat = tensors[0]
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+            flat.mul_(1.0 / self.world)
+            return (flat, tensors, False)
+        flat = torch.cat([t.reshape(-1) for t in tensors])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.mul_(1.0 / self.world)
+        return (flat, tensors, True)
+
+    def grad_ready(self, params_and_grads):
+        """Called from inside the backward with a list of (param, grad) that are final."""
+        big, small = [], []
+        for p, g in params_and_grads:
+            if id(p) not in self.index or id(p) in self.done:
+                continue
+            p.grad = g
+            self.done.add(id(p))
+            (big if g.numel() * g.element_size() >= self.bucket_bytes // 4 else small).append(g)
+        for g in big:
+            self._launch([g])
+        if small:
+            self._launch(small)
+
+    def finish(self):
+        """Reduce every gradient not yet reduced, then wait for all buckets (on the compute stream)."""
+        rest = [p.grad for p in self.params if p.grad is not None and id(p) not in self.done]
+        bucket, size = [], 0
+        for g in rest:
+            bucket.append(g)
+            size += g.numel() * g.element_size()
+            if size >= self.bucket_bytes:
+                self._launch(bucket)
+                bucket, size = [], 0
+        if bucket:
+            self._launch(bucket)
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        for flat, tensors, copied in self.pending:
+            if copied:
+                off = 0
+                for t in tensors:
+                    n = t.numel()
+                    t.copy_(flat[off:off + n].view_as(t))
+                    off += n
+        self.pending.clear()
+        self.done.clear()
+        if self.broadcast_buffers:
+            with torch.no_grad():
+                for b in self.model.buffers():
+                    if b.dtype.is_floating_point:
+                        dist.broadcast(b.data, 0)

@@ -1,0 +1,67 @@
+"""Fused gradient-clip + Adam on the MI355X (one norm pass + one update pass over all tensors).
+
+Replaces Lightning's ``gradient_clip_val`` (torch clip_grad_norm_, configs/base_training.yaml:51)
+followed by ``torch.optim.Adam(lr, weight_decay)`` (base_training.yaml:56-59, instantiated at
+src/training/engine.py:300).  Numerics follow torch's single-tensor Adam: L2 decay added to the
+(clipped) gradient, ``exp_avg.lerp_(g, 1-beta1)``, ``exp_avg_sq = beta2*v + (1-beta2) g^2``,
+``p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)``.  The clip coefficient is computed on the device,
+so the step never synchronises with the host.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..miaudio import kernels as K
+from ..miaudio import lib as L
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, clip: float = 0.0, **unused):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.clip = float(clip or 0.0)
+        self.last_total_norm = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if len(self.param_groups) != 1:
+            raise RuntimeError("FusedAdam drives one parameter group (the reference configures one)")
+        grp = self.param_groups[0]
+        ps = [p for p in grp["params"] if p.grad is not None]
+        if not ps:
+            return loss
+        dev = ps[0].device
+        L.require_device(ps[0], "FusedAdam")
+        for p in ps:
+            if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                raise TypeError("FusedAdam keeps f32 master parameters and gradients")
+            st = self.state[p]
+            if not st:
+                st["step"] = torch.zeros((), dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] += 1
+        step = int(self.state[ps[0]]["step"].item())
+        gs = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
+        table = torch.tensor([[p.data_ptr() for p in ps], [g.data_ptr() for g in gs],
+                              [self.state[p]["exp_avg"].data_ptr() for p in ps],
+                              [self.state[p]["exp_avg_sq"].data_ptr() for p in ps],
+                              [p.numel() for p in ps]], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        n = len(ps)
+        lib = L.load()
+        ws = K.workspace(lib.mia_adam_workspace_bytes(n), dev, "adam")
+        tot = torch.empty(1, dtype=torch.float32, device=dev)
+        b1, b2 = grp["betas"]
+        L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
+                                  table[3].data_ptr(), table[4].data_ptr(), n, max(p.numel() for p in ps),
+                                  float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+                                  float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
+                                  L.stream_ptr()), "mia_clip_adam")
+        self.last_total_norm = tot
+        self._keep = (table, gs)  # keep the pointer table alive until the next step
+        return loss

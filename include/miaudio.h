@@ -1,0 +1,246 @@
+/*
+ * miaudio.h — C ABI of libmiaudio.so, the MI355X (gfx950) kernels behind the
+ * youssefg7/dl-sound-classification training hot path:
+ *   batched waveform -> STFT/log-mel -> EnvNet-v2 | AST fwd+bwd -> clip + Adam.
+ *
+ * The reference is pure Python and binds no native library; its "plugin API" is
+ * Hydra `_target_` instantiation of nn.Modules (configs/model/<name>.yaml:10) driven by
+ * LitClassifier (src/training/engine.py:67-310).  Each entry point below replaces a
+ * third-party op the reference reaches through PyTorch on that path; the comment
+ * on each names the reference call site (file:line, relative to the reference root).
+ * The Python side binds these with ctypes.
+ *
+ * Conventions:
+ *  - extern "C", plain pointers and sizes; no torch types.
+ *  - Stream-ordered: every call enqueues on `stream` (a hipStream_t) and never syncs.
+ *  - Caller owns ALL memory (inputs, outputs, workspaces); the library allocates nothing.
+ *  - Return 0 on success, a negative code on error; mia_last_error_string() explains.
+ *  - Reentrant and stateless (error string is thread-local).
+ *  - Activations are channels-last (NHWC) unless stated; dtype codes MIA_F32/MIA_BF16.
+ */
+#ifndef MIAUDIO_H
+#define MIAUDIO_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mia_stream_t; /* hipStream_t */
+
+enum { MIA_F32 = 0, MIA_BF16 = 1, MIA_U8 = 2 };
+enum { MIA_OP_DENSE = 0, MIA_OP_CONV = 1, MIA_OP_CONVROW = 2 };
+enum { MIA_LAYOUT_KC = 0, MIA_LAYOUT_RC = 1 };
+enum { MIA_PRE_NONE = 0, MIA_PRE_AFFINE = 1, MIA_PRE_AFFINE_RELU = 2, MIA_PRE_GELU = 3 };
+enum { MIA_ACT_NONE = 0, MIA_ACT_RELU = 1, MIA_ACT_GELU = 2, MIA_DACT_NZ = 3, MIA_DACT_GELU = 4 };
+
+/* A GEMM operand = a logical 2-D source S[i][j] whose j axis is contiguous in memory.
+ *  DENSE   : S[i][j] = ptr[i*ld + j], i < rows, j < cols (zero outside).
+ *  CONV    : im2col of an NHWC tensor (n,h,w,c), c % 8 == 0:
+ *            i = output pixel (b, y, x) over n*oh*ow, j = (ky, kx, ci) over kh*kw*c,
+ *            S[i][j] = in[b][y*sh+ky-ph][x*sw+kx-pw][ci] (zero padding).
+ *  CONVROW : same as CONV but for (kw*c) % 8 == 0 with pw == 0 (c may be 1 or 2):
+ *            one chunk = 8 consecutive (kx, ci) of one kernel row.
+ * layout KC: the operand's GEMM k axis is j (A: M x K stored [M][K]; B: stored [N][K]).
+ * layout RC: the operand's GEMM k axis is i (A stored [K][M]; B stored [K][N]).
+ * pre: optional per-channel transform applied while loading (BN affine [+ReLU]
+ *      of the previous layer, or GELU), channel = j (DENSE) / ci (CONV). */
+typedef struct MiaOperand {
+  const void* ptr;
+  int32_t kind, dtype, layout, pre;
+  int64_t rows, cols, ld;
+  int32_t n, h, w, c;
+  int32_t oh, ow, kh, kw, sh, sw, ph, pw;
+  const float* pre_scale;
+  const float* pre_shift;
+} MiaOperand;
+
+/* Epilogue of C[m][n] = alpha * sum_k A[m][k] B[k][n]:
+ *   v = alpha*acc (+ bias[n]); act; (v += old C if accumulate); store as dtype at
+ *   ptr[prow(m)*ldc + n] with prow(m) = m if rm_inner == 0 else
+ *   (m / rm_inner)*rm_outer + (m % rm_inner)*rm_istride + rm_offset.
+ *   DACT_NZ  : v *= (aux[m][n] != 0) * act_scale   (ReLU+dropout backward from saved output)
+ *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation) */
+typedef struct MiaEpilogue {
+  void* ptr;
+  int32_t dtype, act, accumulate, aux_dtype;
+  int64_t ldc;
+  int64_t rm_inner, rm_outer, rm_istride, rm_offset;
+  const float* bias;
+  const void* aux;
+  int64_t ldaux;
+  float alpha, act_scale;
+} MiaEpilogue;
+
+/* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16; f32: v_mfma_f32_32x32x2_f32).
+ * Replaces cuDNN conv2d fwd/dgrad/wgrad for every EnvNetV2 conv (envnet_v2.py:15,19,31,34),
+ * the nn.Linear layers (envnet_v2.py:51,55,59; ast.py:40 and timm Block qkv/proj/fc1/fc2,
+ * ast.py:38,60-61) and the AST patch-embed conv (ast.py:30,55).
+ * split_k > 1 needs a workspace of mia_gemm_workspace_bytes(M,N,split_k) bytes. */
+int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k);
+int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
+             int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
+             mia_stream_t stream);
+
+/* Fused log-mel: frame gather + 1024-pt real FFT (LDS) + |X|^2 + htk mel (sparse bands)
+ * + 10log10 + per-clip top_db clamp + per-clip mean/unbiased-std normalisation.
+ * Replaces ASTPreprocessor.preprocess (src/datasets/preprocessing.py:1013-1039,
+ * torchaudio MelSpectrogram/AmplitudeToDB at :988-998).
+ * wav: (B, T) f32 rows of stride ld_wav; out: (B, n_mels, frames) f32, frames = 1 + T/hop.
+ * Constant device tables built once by the caller: window[win_length] (periodic Hann),
+ * tw512[512] / tw1024[513] complex twiddles exp(-2 pi i q/512), exp(-2 pi i k/1024) as float2,
+ * mel bands: band_start/band_len/band_off[n_mels] into band_w[nnz] (htk filterbank, norm=None).
+ * workspace: mia_logmel_workspace_bytes(B, frames) bytes. */
+typedef struct MiaMelCfg {
+  int32_t sample_rate, n_fft, win_length, hop, n_mels, normalize;
+  float top_db, target_mean, target_std;
+} MiaMelCfg;
+int64_t mia_logmel_workspace_bytes(int64_t B, int64_t frames);
+int mia_logmel_fwd(const float* wav, int64_t B, int64_t T, int64_t ld_wav, const MiaMelCfg* cfg,
+                   const float* window, const void* tw512, const void* tw1024,
+                   const int32_t* band_start, const int32_t* band_len, const int32_t* band_off,
+                   const float* band_w, float* out, void* workspace, mia_stream_t stream);
+
+/* BatchNorm (train mode) — nn.BatchNorm2d after every conv (envnet_v2.py:16,20,32,35).
+ * x: (P, C) channels-last.  stats out: mean[C], invstd[C]; running stats updated with
+ * momentum and the unbiased variance; scale = gamma*invstd, shift = beta - mean*scale.
+ * partial: workspace of mia_bn_partial_bytes(P, C) bytes. */
+int64_t mia_bn_partial_bytes(int64_t P, int32_t C);
+int mia_bn_fwd_stats(const void* x, int32_t dtype, int64_t P, int32_t C, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var, float momentum,
+                     float eps, int32_t training, float* mean, float* invstd, float* scale,
+                     float* shift, void* partial, mia_stream_t stream);
+/* ReLU + BN backward reductions: dz = dact * (scale*x+shift > 0) (in place allowed),
+ * dgamma = sum dz*xhat, dbeta = sum dz (written, not accumulated). */
+int mia_bn_relu_bwd_reduce(const void* dact, void* dz, const void* x, int32_t dtype, int64_t P,
+                           int32_t C, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, float* dgamma, float* dbeta, void* partial,
+                           mia_stream_t stream);
+/* dx = gamma*invstd*(dz - dbeta/P - xhat*dgamma/P); optional dbias[c] = sum_rows dx (the
+ * gradient of the conv bias that precedes the BN, envnet_v2.py:15 bias=True). */
+int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t dtype, int64_t P, int32_t C,
+                     const float* gamma, const float* mean, const float* invstd,
+                     const float* dgamma, const float* dbeta, float* dbias, void* partial,
+                     mia_stream_t stream);
+
+/* Max-pool of relu(scale*x+shift) — nn.MaxPool2d (envnet_v2.py:23,37) fused with the
+ * preceding BN+ReLU.  x: (n, h, w, c) NHWC; window (kh,kw) == stride, floor mode.
+ * out layout: 0 = NHWC (n,oh,ow,c); 1 = "transposed frontend" (n, c, ow) for oh == 1
+ * (envnet_v2.py:82 transpose(1,2)); 2 = NCHW flattened (n, c, oh, ow) (classifier Flatten).
+ * argmax: (n, oh, ow, c) u8 window offset of the max. */
+int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c,
+                 int32_t kh, int32_t kw, const float* scale, const float* shift, void* out,
+                 int32_t out_layout, uint8_t* argmax, mia_stream_t stream);
+/* Backward of pool(relu(bn(x))) up to dz (the BN output grad) + BN reductions. */
+int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint8_t* argmax,
+                                const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w,
+                                int32_t c, int32_t kh, int32_t kw, const float* scale,
+                                const float* shift, const float* mean, const float* invstd,
+                                void* dz, float* dgamma, float* dbeta, void* partial,
+                                mia_stream_t stream);
+
+/* Column sums over rows of a (P, C) matrix: bias gradients. out f32[C] (overwritten). */
+int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, int64_t ld, float* out,
+               void* partial, mia_stream_t stream);
+
+/* out[b][ih][iw] = sum_{ky} p[b][ih-ky][iw][ky]   (dgrad of the 1-channel 8x8 trunk conv,
+ * envnet_v2.py:41 first conv). p: (n, ph, w, kh) f32; out (n, ph+kh-1, w) dtype. */
+int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh, void* out,
+                    int32_t dtype, mia_stream_t stream);
+
+/* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
+ * mode 0: OHWI (cout, kh, kw, cin)            — forward operand
+ * mode 1: flipped dgrad operand (cin, kh, kw, cout) with ky->kh-1-ky, kx->kw-1-kx
+ * mode 2: parity dgrad operand for stride-2 1-D convs: (2, cin, kw/2, cout),
+ *         [p][ci][j][co] = W[co][ci][0][2*(kw/2-1-j)+p]
+ * mode 3: row-split dgrad for cin==1: (kh, kw, cout) with [ky][j][co] = W[co][0][ky][kw-1-j]
+ * mode 4: inverse of mode 0 on f32 gradients: src (cout,kh,kw,cin) -> dst (cout,cin,kh,kw). */
+int mia_pack_weight(const float* src, void* dst, int32_t dtype, int32_t cout, int32_t cin,
+                    int32_t kh, int32_t kw, int32_t mode, mia_stream_t stream);
+
+/* out[m][n] = act(sum_s ws[s][m][n] * alpha + bias[n]) with MiaEpilogue semantics —
+ * split-K combine; exposed for the FC layers. */
+int mia_splitk_reduce(const float* ws, int32_t split_k, int64_t M, int64_t N,
+                      const MiaEpilogue* E, mia_stream_t stream);
+
+/* Inverted dropout on a (rows, cols) activation, in place, keep-mask = hash(seed, idx) >= p.
+ * nn.Dropout (envnet_v2.py:53,57).  Output scaled by 1/(1-p). */
+int mia_dropout(void* x, int32_t dtype, int64_t numel, float p, uint64_t seed,
+                mia_stream_t stream);
+
+/* Soft-label loss of LitClassifier._step (engine.py:175-176):
+ *   loss = -mean_b sum_c y*log(softmax(z)+1e-8);  dz written (scaled by grad_scale).
+ * If input_sigmoid, z = sigmoid(logits) first (ASTModel returns probabilities, ast.py:63)
+ * and dlogits includes the sigmoid backward.  loss: f32[1]; correct: i32[1] argmax hits. */
+int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32_t input_sigmoid,
+                float* loss, float* dlogits, int32_t* correct, mia_stream_t stream);
+
+/* Gradient clipping + Adam over a device-side table of tensors (Lightning
+ * gradient_clip_val=1.0 + torch.optim.Adam(lr, weight_decay), base_training.yaml:51,56-59).
+ * tables: f32* params[n], grads[n], m[n], v[n]; int64 sizes[n] (all device arrays).
+ * sqnorm_ws: f32 workspace of mia_adam_workspace_bytes(ntensors) bytes.
+ * clip <= 0 disables clipping. step is 1-based. */
+int64_t mia_adam_workspace_bytes(int32_t ntensors);
+int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
+                  void* const* exp_avg_sq, const int64_t* sizes, int32_t ntensors,
+                  int64_t max_numel, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, int32_t step, float clip, float* total_norm_out,
+                  void* sqnorm_ws, mia_stream_t stream);
+
+/* LayerNorm over the last dim (timm Block norm1/norm2 and final norm, eps 1e-6).
+ * x: (rows, D) -> y dtype; mean/rstd f32[rows] saved for backward. */
+int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gamma, const float* beta,
+                      void* y, int32_t ydtype, float* mean, float* rstd, int64_t rows,
+                      int32_t D, float eps, mia_stream_t stream);
+/* dx (+= if accumulate) and partial sums for dgamma/dbeta (f32 [nblk][2][D] in partial,
+ * reduced into dgamma/dbeta). */
+int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
+                      const float* gamma, const float* mean, const float* rstd, void* dx,
+                      int32_t dxdtype, int32_t accumulate, float* dgamma, float* dbeta,
+                      void* partial, int64_t rows, int32_t D, mia_stream_t stream);
+int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
+
+/* Fused multi-head attention (timm Attention with F.scaled_dot_product_attention,
+ * ast.py:60-61), bf16 MFMA, online softmax, head_dim 64.
+ * qkv: (B, N, 3, H, 64) bf16 (the qkv Linear output as is); out: (B, N, H, 64) bf16;
+ * lse: f32 (B, H, N) saved for backward. */
+int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t B, int32_t N, int32_t H,
+                 float scale, mia_stream_t stream);
+/* dqkv: (B, N, 3, H, 64) bf16; delta workspace f32 (B,H,N); dq_acc f32 (B,N,H,64). */
+int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                 void* dqkv, float* delta, float* dq_acc, int32_t B, int32_t N, int32_t H,
+                 float scale, mia_stream_t stream);
+
+/* AST token assembly (ast.py:56-59): x[b][0] = cls + pos[0]; x[b][1+p] = patches[b][p] + pos[1+p].
+ * patches: (B, Np, D) f32; out (B, Np+1, D) f32.  Backward: dpatch, dcls/dpos reductions. */
+int mia_tokens_fwd(const float* patches, const float* cls, const float* pos, float* out,
+                   int32_t B, int32_t Np, int32_t D, mia_stream_t stream);
+int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, float* dpos, int32_t B,
+                   int32_t Np, int32_t D, mia_stream_t stream);
+
+/* Elementwise helpers. */
+int mia_cast(const void* src, int32_t sdtype, void* dst, int32_t ddtype, int64_t numel,
+             mia_stream_t stream);
+/* x += y (f32) */
+int mia_add_inplace(float* x, const void* y, int32_t ydtype, int64_t numel, mia_stream_t stream);
+
+/* Between-class mixing on device (BCMixingDataset.apply_bc_mixing, preprocessing.py:564-609):
+ * out[b] = (p*x[b] + (1-p)*x[partner[b]]) / sqrt(p^2+(1-p)^2) where p is r[b] adjusted by
+ * the RMS-"SPL" rule (preprocessing.py:395-471); soft labels use r (not p). */
+int mia_bc_mix(const float* x, int64_t T, int32_t B, const int32_t* partner, const float* r,
+               const int64_t* labels, int32_t num_classes, float* out, float* yout,
+               float* p_out, mia_stream_t stream);
+/* SpecAugment zero masks + Mixup (preprocessing.py:1075-1104, esc50.py:52-76) on
+ * (B, F, T) spectrograms, parameters drawn by the caller. */
+int mia_spec_augment_mixup(const float* spec, float* out, int32_t B, int32_t F, int32_t T,
+                           const int32_t* t0, const int32_t* tlen, const int32_t* f0,
+                           const int32_t* flen, const int32_t* partner, const float* lam,
+                           mia_stream_t stream);
+
+const char* mia_last_error_string(void);
+int mia_device_arch(char* buf, int32_t len); /* gcnArchName of the current device */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIAUDIO_H */

@@ -1,0 +1,185 @@
+"""GPU: the implicit-GEMM MFMA kernel against a float64 PyTorch reference of the same op
+(dense GEMM in every layout, conv fwd / dgrad / wgrad gathers, pre-ops, epilogues, split-K).
+Tolerances: f32 compute 1e-5 rel (exact-f32 MFMA), bf16 compute 2e-2 rel (bf16 operands)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from src.miaudio import kernels as K
+from src.miaudio import lib as L
+
+pytestmark = pytest.mark.gpu
+TOL = {L.F32: 1e-5, L.BF16: 2e-2}
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+
+
+def _mat(layout, rows_logical, k, dt, dev, g):
+    """Return (tensor, operand) for a logical [rows][k] matrix stored per layout."""
+    src = torch.randn(rows_logical, k, generator=g).to(dt)
+    if layout == L.KC:
+        t = src.contiguous().to(dev)
+        return src, K.dense(t, L.KC, rows_logical, k), t
+    t = src.t().contiguous().to(dev)
+    return src, K.dense(t, L.RC, k, rows_logical), t
+
+
+@pytest.mark.parametrize("cd", [L.F32, L.BF16])
+@pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 96), (37, 50, 200), (300, 32, 64), (64, 600, 40), (130, 70, 8)])
+def test_dense_layouts(cuda, cd, la, lb, M, N, Kd):
+    g = torch.Generator().manual_seed(M * 7 + N + Kd)
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    a, A, ta = _mat(la, M, Kd, dt, cuda, g)
+    b, Bo, tb = _mat(lb, N, Kd, dt, cuda, g)
+    out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out, N), M, N, Kd, cd)
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double().t()
+    assert rel(out.cpu(), ref) < TOL[cd]
+
+
+@pytest.mark.parametrize("split", [1, 3, 8])
+def test_split_k_bias_relu_bf16_out(cuda, split):
+    g = torch.Generator().manual_seed(1)
+    M, N, Kd = 200, 300, 1000
+    a = torch.randn(M, Kd, generator=g)
+    w = torch.randn(N, Kd, generator=g)
+    bias = torch.randn(N, generator=g)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    ta, tw, tb = a.to(cuda), w.to(cuda), bias.to(cuda)
+    K.gemm(K.dense(ta, L.KC, M, Kd), K.dense(tw, L.KC, N, Kd), K.epilogue(out, N, act=L.ACT_RELU, bias=tb),
+           M, N, Kd, L.F32, split_k=split)
+    torch.cuda.synchronize()
+    ref = torch.relu(a.double() @ w.double().t() + bias.double())
+    assert rel(out.float().cpu(), ref) < 1e-2
+
+
+def test_dact_nz_and_accumulate(cuda):
+    g = torch.Generator().manual_seed(2)
+    M, N, Kd = 64, 96, 48
+    a = torch.randn(M, Kd, generator=g)
+    w = torch.randn(N, Kd, generator=g)
+    aux = torch.relu(torch.randn(M, N, generator=g))
+    base = torch.randn(M, N, generator=g)
+    out = base.clone().to(cuda)
+    K.gemm(K.dense(a.to(cuda), L.KC, M, Kd), K.dense(w.to(cuda), L.KC, N, Kd),
+           K.epilogue(out, N, act=L.DACT_NZ, aux=aux.to(cuda), ldaux=N, act_scale=2.0, accumulate=True), M, N, Kd,
+           L.F32)
+    torch.cuda.synchronize()
+    ref = base.double() + (a.double() @ w.double().t()) * (aux != 0).double() * 2.0
+    assert rel(out.cpu(), ref) < 1e-5
+
+
+def _conv_case(cuda, cd, n, cin, cout, h, w, kh, kw, sw, pre):
+    g = torch.Generator().manual_seed(n * 100 + cin + kw)
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    x = torch.randn(n, h, w, cin, generator=g).to(dt)
+    wt = torch.randn(cout, cin, kh, kw, generator=g) / (cin * kh * kw) ** 0.5
+    sc = torch.rand(cin, generator=g) + 0.5
+    sh = torch.randn(cin, generator=g) * 0.1
+    oh, ow = h - kh + 1, (w - kw) // sw + 1
+    xin = x.double()
+    if pre:
+        xin = torch.relu(xin * sc.double() + sh.double())
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), wt.double(), stride=(1, sw)).permute(0, 2, 3, 1)
+    return x, wt, sc, sh, oh, ow, ref
+
+
+@pytest.mark.parametrize("cd", [L.F32, L.BF16])
+@pytest.mark.parametrize("case", [
+    (2, 32, 32, 12, 40, 8, 8, 1, True),   # trunk 8x8 with fused BN+ReLU
+    (2, 32, 64, 1, 300, 1, 16, 2, True),  # frontend conv2 (stride 2)
+    (3, 64, 128, 4, 30, 1, 2, 1, False),  # trunk (1,2)
+    (2, 1, 32, 16, 60, 8, 8, 1, False),   # 1-channel 8x8 (CONVROW)
+])
+def test_conv_fwd_dgrad_wgrad(cuda, cd, case):
+    n, cin, cout, h, w, kh, kw, sw, pre = case
+    x, wt, sc, sh, oh, ow, ref = _conv_case(cuda, cd, n, cin, cout, h, w, kh, kw, sw, pre)
+    tx = x.contiguous().to(cuda)
+    tsc, tsh = sc.to(cuda), sh.to(cuda)
+    wp = K.pack_weight(wt.contiguous().to(cuda), cd, 0)
+    out = torch.empty(n * oh * ow, cout, dtype=torch.float32, device=cuda)
+    rowk = cin % 8 != 0
+    preop = L.PRE_AFFINE_RELU if pre else L.PRE_NONE
+    A = K.conv(tx, L.KC, n, h, w, cin, oh, ow, kh, kw, sw=sw, pre=preop, scale=tsc, shift=tsh, row_kind=rowk)
+    K.gemm(A, K.dense(wp, L.KC, cout, kh * kw * cin), K.epilogue(out, cout), n * oh * ow, cout, kh * kw * cin, cd)
+    torch.cuda.synchronize()
+    assert rel(out.view(n, oh, ow, cout).cpu(), ref) < TOL[cd] * 2
+
+    # wgrad: dW = dy^T im2col(x)
+    g = torch.Generator().manual_seed(7)
+    dy = torch.randn(n, oh, ow, cout, generator=g).to(x.dtype)
+    xin = x.double()
+    if pre:
+        xin = torch.relu(xin * sc.double() + sh.double())
+    xr = xin.permute(0, 3, 1, 2).requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=(1, sw))
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    P = n * oh * ow
+    tdy = dy.contiguous().to(cuda)
+    dW = torch.empty(cout, kh * kw * cin, dtype=torch.float32, device=cuda)
+    Bop = K.conv(tx, L.RC, n, h, w, cin, oh, ow, kh, kw, sw=sw, pre=preop, scale=tsc, shift=tsh, row_kind=rowk)
+    K.gemm(K.dense(tdy, L.RC, P, cout), Bop, K.epilogue(dW, kh * kw * cin), cout, kh * kw * cin, P, cd)
+    gw = torch.empty(cout, cin, kh, kw, device=cuda)
+    K.unpack_ohwi_grad(dW, (cout, cin, kh, kw), gw)
+    torch.cuda.synchronize()
+    assert rel(gw.cpu(), wr.grad) < TOL[cd] * 2
+
+    # dgrad (stride 1, cin % 8 == 0): conv of padded dy with the flipped kernel
+    if sw == 1 and cin % 8 == 0:
+        wf = K.pack_weight(wt.contiguous().to(cuda), cd, 1)
+        dx = torch.empty(n * h * w, cin, dtype=torch.float32, device=cuda)
+        Kd = kh * kw * cout
+        K.gemm(K.conv(tdy, L.KC, n, oh, ow, cout, h, w, kh, kw, ph=kh - 1, pw=kw - 1), K.dense(wf, L.KC, cin, Kd),
+               K.epilogue(dx, cin), n * h * w, cin, Kd, cd)
+        torch.cuda.synchronize()
+        gref = xr.grad.permute(0, 2, 3, 1)  # gradient w.r.t. the conv input (after the pre-op)
+        assert rel(dx.view(n, h, w, cin).cpu(), gref) < TOL[cd] * 2
+
+
+@pytest.mark.parametrize("cd", [L.F32, L.BF16])
+def test_stride2_parity_dgrad(cuda, cd):
+    """Frontend conv2 dgrad as two stride-1 parity convolutions with a row-map epilogue."""
+    g = torch.Generator().manual_seed(3)
+    n, cin, cout, W1, kw = 2, 32, 64, 301, 16
+    W2 = (W1 - kw) // 2 + 1
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    wt = torch.randn(cout, cin, 1, kw, generator=g) / 20
+    dy = torch.randn(n, 1, W2, cout, generator=g).to(dt)
+    xr = torch.zeros(n, cin, 1, W1, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wt.double(), stride=(1, 2)).backward(dy.double().permute(0, 3, 1, 2))
+    tdy = dy.contiguous().to(cuda)
+    wpar = K.pack_weight(wt.contiguous().to(cuda), cd, 2).view(2, -1)
+    dx = torch.empty(n * W1, cin, dtype=torch.float32, device=cuda)
+    for par in (0, 1):
+        Tp = (W1 - par + 1) // 2
+        K.gemm(K.conv(tdy, L.KC, n, 1, W2, cout, 1, Tp, 1, kw // 2, pw=kw // 2 - 1), K.dense(wpar[par], L.KC, cin, 512),
+               K.epilogue(dx, cin, rowmap=(Tp, W1, 2, par)), n * Tp, cin, 512, cd)
+    torch.cuda.synchronize()
+    assert rel(dx.view(n, W1, cin).cpu(), xr.grad[:, :, 0].permute(0, 2, 1)) < TOL[cd] * 2
+
+
+@pytest.mark.parametrize("cd", [L.F32, L.BF16])
+def test_single_channel_dgrad_rowsplit(cuda, cd):
+    """1-channel 8x8 conv dgrad via the (ky) row-split GEMM + col2im_rows."""
+    g = torch.Generator().manual_seed(4)
+    n, cout, H, W, kh, kw = 2, 32, 20, 50, 8, 8
+    ha, wa = H - kh + 1, W - kw + 1
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    wt = torch.randn(cout, 1, kh, kw, generator=g) / 8
+    dy = torch.randn(n, ha, wa, cout, generator=g).to(dt)
+    xr = torch.zeros(n, 1, H, W, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wt.double()).backward(dy.double().permute(0, 3, 1, 2))
+    tdy = dy.contiguous().to(cuda)
+    wr = K.pack_weight(wt.contiguous().to(cuda), cd, 3)
+    Pm = torch.empty(n * ha * W, kh, dtype=torch.float32, device=cuda)
+    K.gemm(K.conv(tdy, L.KC, n, ha, wa, cout, ha, W, 1, kw, pw=kw - 1), K.dense(wr, L.KC, kh, kw * cout),
+           K.epilogue(Pm, kh), n * ha * W, kh, kw * cout, cd)
+    dx = torch.empty(n, H, W, dtype=torch.float32, device=cuda)
+    K.col2im_rows(Pm, n, ha, W, kh, dx)
+    torch.cuda.synchronize()
+    assert rel(dx.cpu(), xr.grad[:, 0]) < TOL[cd] * 2

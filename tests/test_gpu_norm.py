@@ -1,0 +1,81 @@
+"""GPU: BatchNorm statistics / backward and the fused BN+ReLU+max-pool kernels against float64
+torch autograd on the same inputs (so the ReLU masks agree exactly)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from src.miaudio import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("C", [32, 64, 256])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_stats_and_backward(cuda, C, dt):
+    g = torch.Generator().manual_seed(C)
+    P = 5000
+    y = (torch.randn(P, C, generator=g) * 3 + 2).to(dt)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.2
+    rm, rv = torch.zeros(C), torch.ones(C)
+    ty = y.to(cuda)
+    trm, trv = rm.to(cuda), rv.to(cuda)
+    st = K.bn_fwd_stats(ty, P, C, gamma.to(cuda), beta.to(cuda), trm, trv, 0.1, 1e-5, True)
+    yd = y.double()
+    mu, var = yd.mean(0), yd.var(0, unbiased=False)
+    assert rel(st.mean, mu) < 1e-5
+    assert rel(1.0 / st.invstd.double() ** 2 - 1e-5, var) < 1e-4
+    assert rel(trv, 0.9 + 0.1 * yd.var(0, unbiased=True)) < 1e-4
+    # backward of relu(bn(y)) given dact
+    dact = torch.randn(P, C, generator=g).to(dt)
+    yr = yd.clone().requires_grad_(True)
+    gr = gamma.double().requires_grad_(True)
+    br = beta.double().requires_grad_(True)
+    z = F.batch_norm(yr, None, None, gr, br, True, 0.0, 1e-5)
+    torch.relu(z).backward(dact.double())
+    tact = dact.to(cuda)
+    dz = torch.empty_like(tact)
+    dg, db = K.bn_relu_bwd_reduce(tact, dz, ty, P, C, st)
+    dx = torch.empty_like(tact)
+    dbias = torch.empty(C, device=cuda)
+    K.bn_bwd_apply(dz, ty, dx, P, C, gamma.to(cuda), st, dg, db, dbias)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dt == torch.float32 else 2e-2
+    assert rel(dg, gr.grad) < tol * 5 and rel(db, br.grad) < tol * 5
+    assert rel(dx.float(), yr.grad) < tol * 10
+    assert float(dbias.abs().max()) < 1e-2 * float(yr.grad.abs().sum(0).max())
+
+
+@pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64, 1), (2, 50, 846, 32, 5, 3, 0), (3, 10, 66, 256, 1, 2, 2)])
+def test_pool_fwd_bwd(cuda, geom):
+    n, h, w, c, kh, kw, layout = geom
+    g = torch.Generator().manual_seed(h * w)
+    y = torch.randn(n, h, w, c, generator=g)
+    scale = torch.rand(c, generator=g) + 0.5
+    shift = torch.randn(c, generator=g) * 0.3
+    st = K.BNState(torch.zeros(c, device=cuda), torch.ones(c, device=cuda), scale.to(cuda), shift.to(cuda))
+    oh, ow = h // kh, w // kw
+    out = torch.empty({0: (n, oh, ow, c), 1: (n, c, ow), 2: (n, c, oh, ow)}[layout], device=cuda)
+    am = torch.empty(n, oh, ow, c, dtype=torch.uint8, device=cuda)
+    ty = y.to(cuda)
+    K.pool_fwd(ty, n, h, w, c, kh, kw, st, out, layout, am)
+    a = torch.relu(y.double() * scale.double() + shift.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(a, (kh, kw), (kh, kw))
+    ref_l = {0: ref.permute(0, 2, 3, 1), 1: ref[:, :, 0, :], 2: ref}[layout]
+    torch.cuda.synchronize()
+    assert rel(out, ref_l) < 1e-6
+    dout = torch.randn(ref_l.shape, generator=g)
+    ref_l.backward(dout.double())
+    # kernel gives dz (grad of the BN output z, relu-masked); torch gives grad of a = relu(z)
+    dz = torch.empty_like(ty)
+    dg, db = K.pool_bwd_bn_relu_reduce(dout.to(cuda), layout, am, ty, n, h, w, c, kh, kw, st, dz)
+    torch.cuda.synchronize()
+    zmask = (y.double() * scale.double() + shift.double() > 0).permute(0, 3, 1, 2)
+    gz = (a.grad * zmask).permute(0, 2, 3, 1)
+    assert rel(dz, gz) < 1e-6
+    assert rel(db, gz.sum(dim=(0, 1, 2))) < 1e-5
