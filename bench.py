@@ -146,6 +146,7 @@ def main():
         probe_tags = (args.probe.split(",") if args.probe else ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv2.fwd"])
         workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
     else:
+        sys.path.insert(0, str(REPO))
         from bench_ast import build_ast_step  # noqa: E402
         B = args.batch or 64
         step, flop_per_clip, probe_tags, workload = build_ast_step(args, dev, rank, world, B)
@@ -191,7 +192,9 @@ def main():
     roof = None
     if dom:
         ks = kstats[dom]
-        roof = {"bound": "mfma", "kernel": f"igemm_kernel [{dom}]", "achieved": round(ks["tflops"], 2),
+        kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel"}.get(
+            dom, "igemm_kernel")
+        roof = {"bound": "mfma", "kernel": f"{kname} [{dom}]", "achieved": round(ks["tflops"], 2),
                 "peak": peak_tf, "unit": "TFLOP/s", "frac": round(ks["tflops"] / peak_tf, 4), "traffic": None,
                 "algorithmic_per_launch": {"flop": ks["flop"], "bytes": ks["bytes"]},
                 "ms_per_launch": round(ks["ms"], 4)}

@@ -1,0 +1,516 @@
+// Fused multi-head attention, head_dim 64, bf16 MFMA (v_mfma_f32_32x32x16_bf16), gfx950.
+// timm Attention with F.scaled_dot_product_attention (reference src/models/ast.py:38,60-61).
+//
+// Layouts: qkv (B, N, 3, H, 64) bf16 = the qkv Linear output as is; out / dout (B, N, H, 64) bf16
+// (= the proj Linear input); lse (B, H, N) f32 in natural-log units of the scaled scores.
+//
+// Forward (q on the lane): each wave owns 32 queries; per 64-key tile staged in LDS it computes
+// S^T = K . Q^T (accumulator column = query = lane, 16 keys per lane in registers), so the online
+// softmax row max / sum are in-lane plus one lane^32 exchange; P^T is fed straight from the
+// accumulator registers as the B operand of O^T += V^T . P^T (V^T fragments by ds_read_b64_tr_b16),
+// so the rescale of O by exp(m_old - m_new) is per lane too.
+// Backward (deterministic, no atomics): a key-parallel kernel computes S and dP with the key on the
+// lane and accumulates dV^T, dK^T in registers while sweeping the query tiles; a query-parallel
+// kernel recomputes S^T, dP^T with the query on the lane and accumulates dQ^T.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int LROW = 72;  // LDS row stride in bf16 (144 B): conflict-free ds_read_b128 rows
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 64 rows x 64 bf16 from global (row stride `ld` elements) into LDS [64][LROW]; rows >= nvalid -> 0
+__device__ __forceinline__ void stage64(bf16* lds, const bf16* g, int64_t ld, int nvalid, int t) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = t + 256 * s;
+    const int row = c >> 3, c16 = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < nvalid) v = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
+    *reinterpret_cast<uint4*>(lds + row * LROW + c16 * 8) = v;
+  }
+}
+
+// Row fragment: tile[row][16ks + 8h + j], j = 0..7 (A operand rows / B operand columns).
+__device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(lds + row * LROW + ks * 16 + 8 * (lane >> 5));
+}
+
+// Transposed fragment in the accumulator k-order: element j = tile[k0 + 8(j>>2) + 4h + (j&3)][c0 + (lane&31)]
+// (two ds_read_b64_tr_b16: 4 consecutive tile rows x 16 columns per 16-lane group).
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int k0, int c0, int lane) {
+  const int i16 = lane & 15, g = lane >> 4, h = lane >> 5;
+  const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
+  const int r = k0 + 4 * h + (i16 >> 2);
+  const bf16* p0 = lds + r * LROW + col;
+  const bf16* p1 = p0 + 8 * LROW;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
+  s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+// accumulator registers 8s..8s+7 -> bf16 operand fragment
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (bf16)a[8 * s + j];
+  return f;
+}
+
+__device__ __forceinline__ bf16x8 load_frag_global(const bf16* row, int ks, int lane, bool valid) {
+  if (!valid) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+    return z;
+  }
+  return *reinterpret_cast<const bf16x8*>(row + ks * 16 + 8 * (lane >> 5));
+}
+
+// row index of accumulator register r for this lane half
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                       float* __restrict__ lse, int N, int H, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LROW];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int64_t ldt = (int64_t)3 * H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const int q = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const bool qvalid = q < N;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qvalid);
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = -INFINITY, l = 0.f;
+  const int ntiles = (N + 63) / 64;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * 64;
+    __syncthreads();
+    stage64(Ks, base + (int64_t)k0 * ldt + H * D, ldt, N - k0, t);
+    stage64(Vs, base + (int64_t)k0 * ldt + 2 * H * D, ldt, N - k0, t);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f32x16 s = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s = mfma(frag_row(Ks, st * 32 + (lane & 31), ks, lane), qf[ks], s);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + st * 32 + acc_row(r, lane);
+        s[r] = key < N ? s[r] * scale_log2 : -INFINITY;
+        mx = fmaxf(mx, s[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = mn == -INFINITY ? 0.f : exp2f(s[r] - mn);
+        ls += s[r];
+      }
+      l = l * alpha + ls;
+      m = mn;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const bf16x8 pf = acc_frag(s, sk);
+        o0 = mfma(frag_tr(Vs, st * 32 + 16 * sk, 0, lane), pf, o0);
+        o1 = mfma(frag_tr(Vs, st * 32 + 16 * sk, 32, lane), pf, o1);
+      }
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (qvalid) {
+    const float inv = 1.f / lt;
+    bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
+      const int d0 = 8 * g4 + 4 * (lane >> 5);
+      bf16x4 v0, v1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(o0[4 * g4 + i] * inv); v1[i] = (bf16)(o1[4 * g4 + i] * inv); }
+      *reinterpret_cast<bf16x4*>(orow + d0) = v0;
+      *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
+    }
+    if (lane < 32) lse[(int64_t)bh * N + q] = (m + log2f(lt)) / LOG2E;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// delta[b,h,q] = sum_d dO[q][d] * O[q][d]
+__global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout, float* __restrict__ delta,
+                                  int B, int N, int H) {
+  const int64_t total = (int64_t)B * N * H;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int hd = (int)(i % H);
+    const int64_t bq = i / H;
+    const int q = (int)(bq % N);
+    const int b = (int)(bq / N);
+    const bf16* o = out + i * D;
+    const bf16* g = dout + i * D;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(o + 8 * c);
+      const bf16x8 e = *reinterpret_cast<const bf16x8*>(g + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = fmaf((float)a[j], (float)e[j], s);
+    }
+    delta[((int64_t)b * H + hd) * N + q] = s;
+  }
+}
+
+// key on the lane: each wave owns 32 keys (128 per block); sweeps query tiles of 64.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                            int N, int H, float scale, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 Qs[64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Gs[64 * LROW];
+  __shared__ __attribute__((aligned(16))) float Ls[64];
+  __shared__ __attribute__((aligned(16))) float Ds[64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const bf16* gbase = dout + (int64_t)b * N * ldo + hd * D;
+  const int key = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const bool kvalid = key < N;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, kvalid);
+    vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, kvalid);
+  }
+  f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
+  const int ntiles = (N + 63) / 64;
+  for (int qt = 0; qt < ntiles; ++qt) {
+    const int q0 = qt * 64;
+    __syncthreads();
+    stage64(Qs, base + (int64_t)q0 * ldt, ldt, N - q0, t);
+    stage64(Gs, gbase + (int64_t)q0 * ldo, ldo, N - q0, t);
+    if (t < 64) {
+      const int q = q0 + t;
+      Ls[t] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;  // q >= N -> p = 0
+      Ds[t] = q < N ? delta[(int64_t)bh * N + q] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sq = 0; sq < 2; ++sq) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma(frag_row(Qs, sq * 32 + (lane & 31), ks, lane), kf[ks], s);
+        dp = mfma(frag_row(Gs, sq * 32 + (lane & 31), ks, lane), vf[ks], dp);
+      }
+      // rows of the accumulators are queries sq*32 + acc_row(r)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = sq * 32 + acc_row(r, lane);
+        const float p = exp2f(s[r] * scale_log2 - Ls[qi]);
+        s[r] = p;
+        dp[r] = p * (dp[r] - Ds[qi]);
+      }
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const bf16x8 pf = acc_frag(s, sk);
+        const bf16x8 df = acc_frag(dp, sk);
+        dv0 = mfma(frag_tr(Gs, sq * 32 + 16 * sk, 0, lane), pf, dv0);
+        dv1 = mfma(frag_tr(Gs, sq * 32 + 16 * sk, 32, lane), pf, dv1);
+        dk0 = mfma(frag_tr(Qs, sq * 32 + 16 * sk, 0, lane), df, dk0);
+        dk1 = mfma(frag_tr(Qs, sq * 32 + 16 * sk, 32, lane), df, dk1);
+      }
+    }
+  }
+  if (kvalid) {
+    bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
+    bf16* vrow = krow + H * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 8 * g4 + 4 * (lane >> 5);
+      bf16x4 a0, a1, c0, c1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a0[i] = (bf16)(dk0[4 * g4 + i] * scale);
+        a1[i] = (bf16)(dk1[4 * g4 + i] * scale);
+        c0[i] = (bf16)dv0[4 * g4 + i];
+        c1[i] = (bf16)dv1[4 * g4 + i];
+      }
+      *reinterpret_cast<bf16x4*>(krow + d0) = a0;
+      *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
+      *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
+      *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
+    }
+  }
+}
+
+// query on the lane: each wave owns 32 queries (128 per block); sweeps key tiles of 64.
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          bf16* __restrict__ dqkv, int N, int H, float scale,
+                                                          float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LROW];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const int q = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const bool qvalid = q < N;
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qvalid);
+    gf[ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qvalid);
+  }
+  const float lq = qvalid ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
+  const float dq_delta = qvalid ? delta[(int64_t)bh * N + q] : 0.f;
+  f32x16 a0 = zero16(), a1 = zero16();
+  const int ntiles = (N + 63) / 64;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * 64;
+    __syncthreads();
+    stage64(Ks, base + (int64_t)k0 * ldt + H * D, ldt, N - k0, t);
+    stage64(Vs, base + (int64_t)k0 * ldt + 2 * H * D, ldt, N - k0, t);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma(frag_row(Ks, st * 32 + (lane & 31), ks, lane), qf[ks], s);
+        dp = mfma(frag_row(Vs, st * 32 + (lane & 31), ks, lane), gf[ks], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + st * 32 + acc_row(r, lane);
+        const float p = key < N ? exp2f(s[r] * scale_log2 - lq) : 0.f;
+        dp[r] = p * (dp[r] - dq_delta);
+      }
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const bf16x8 df = acc_frag(dp, sk);
+        a0 = mfma(frag_tr(Ks, st * 32 + 16 * sk, 0, lane), df, a0);
+        a1 = mfma(frag_tr(Ks, st * 32 + 16 * sk, 32, lane), df, a1);
+      }
+    }
+  }
+  if (qvalid) {
+    bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 8 * g4 + 4 * (lane >> 5);
+      bf16x4 v0, v1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(a0[4 * g4 + i] * scale); v1[i] = (bf16)(a1[4 * g4 + i] * scale); }
+      *reinterpret_cast<bf16x4*>(qrow + d0) = v0;
+      *reinterpret_cast<bf16x4*>(qrow + 32 + d0) = v1;
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------------------ f32 path
+// Reference-precision kernels (exact f32 arithmetic, no flash tiling) used when the model runs
+// in f32 for parity; one wave per query (forward, dQ) or per key (dK/dV); scores staged in LDS.
+constexpr int MAXN = 3328;
+
+__global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                           float* __restrict__ lse, int N, int H, float scale) {
+  __shared__ float sc[4][MAXN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int q = blockIdx.x * 4 + wave;
+  if (q >= N) return;
+  const int64_t ldt = (int64_t)3 * H * D;
+  const float* base = qkv + (int64_t)b * N * ldt + hd * D;
+  float qv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) qv[d] = base[(int64_t)q * ldt + d] * scale;
+  float mx = -INFINITY;
+  for (int k = lane; k < N; k += 64) {
+    const float* kr = base + (int64_t)k * ldt + H * D;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) s = fmaf(qv[d], kr[d], s);
+    sc[wave][k] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int k = lane; k < N; k += 64) {
+    const float p = expf(sc[wave][k] - mx);
+    sc[wave][k] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float o = 0.f;
+  for (int k = 0; k < N; ++k) o = fmaf(sc[wave][k], base[(int64_t)k * ldt + 2 * H * D + lane], o);
+  out[((int64_t)b * N + q) * H * D + hd * D + lane] = o / sum;
+  if (lane == 0) lse[(int64_t)bh * N + q] = mx + logf(sum);
+}
+
+__global__ void attn_delta_f32_kernel(const float* __restrict__ out, const float* __restrict__ dout,
+                                      float* __restrict__ delta, int B, int N, int H) {
+  const int64_t total = (int64_t)B * N * H;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int hd = (int)(i % H);
+    const int64_t bq = i / H;
+    const int q = (int)(bq % N), b = (int)(bq / N);
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s = fmaf(out[i * D + d], dout[i * D + d], s);
+    delta[((int64_t)b * H + hd) * N + q] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ delta, float* __restrict__ dqkv,
+                                                              int N, int H, float scale) {
+  __shared__ float sc[4][MAXN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int q = blockIdx.x * 4 + wave;
+  if (q >= N) return;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const float* base = qkv + (int64_t)b * N * ldt + hd * D;
+  float qv[D], gv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    qv[d] = base[(int64_t)q * ldt + d] * scale;
+    gv[d] = dout[((int64_t)b * N + q) * ldo + hd * D + d];
+  }
+  const float L = lse[(int64_t)bh * N + q], dl = delta[(int64_t)bh * N + q];
+  for (int k = lane; k < N; k += 64) {
+    const float* kr = base + (int64_t)k * ldt + H * D;
+    const float* vr = kr + H * D;
+    float s = 0.f, dp = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) { s = fmaf(qv[d], kr[d], s); dp = fmaf(gv[d], vr[d], dp); }
+    const float p = expf(s - L);
+    sc[wave][k] = p * (dp - dl);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float a = 0.f;
+  for (int k = 0; k < N; ++k) a = fmaf(sc[wave][k], base[(int64_t)k * ldt + H * D + lane], a);
+  dqkv[((int64_t)b * N + q) * ldt + hd * D + lane] = a * scale;
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_kernel(const float* __restrict__ qkv,
+                                                                const float* __restrict__ dout,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ delta,
+                                                                float* __restrict__ dqkv, int N, int H, float scale) {
+  __shared__ float sp[4][MAXN];
+  __shared__ float sd[4][MAXN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int k = blockIdx.x * 4 + wave;
+  if (k >= N) return;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const float* base = qkv + (int64_t)b * N * ldt + hd * D;
+  float kv[D], vv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    kv[d] = base[(int64_t)k * ldt + H * D + d] * scale;
+    vv[d] = base[(int64_t)k * ldt + 2 * H * D + d];
+  }
+  for (int q = lane; q < N; q += 64) {
+    const float* qr = base + (int64_t)q * ldt;
+    const float* gr = dout + ((int64_t)b * N + q) * ldo + hd * D;
+    float s = 0.f, dp = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) { s = fmaf(kv[d], qr[d], s); dp = fmaf(vv[d], gr[d], dp); }
+    const float p = expf(s - lse[(int64_t)bh * N + q]);
+    sp[wave][q] = p;
+    sd[wave][q] = p * (dp - delta[(int64_t)bh * N + q]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float dv = 0.f, dk = 0.f;
+  for (int q = 0; q < N; ++q) {
+    dv = fmaf(sp[wave][q], dout[((int64_t)b * N + q) * ldo + hd * D + lane], dv);
+    dk = fmaf(sd[wave][q], base[(int64_t)q * ldt + lane], dk);
+  }
+  dqkv[((int64_t)b * N + k) * ldt + H * D + hd * D + lane] = dk * scale;
+  dqkv[((int64_t)b * N + k) * ldt + 2 * H * D + hd * D + lane] = dv;
+}
+
+}  // namespace
+
+extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtype, int32_t B, int32_t N, int32_t H,
+                            float scale, mia_stream_t stream) {
+  MIA_CHECK_ARG(qkv && out && lse, "attn_fwd: null pointer");
+  MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_fwd: bad shape");
+  if (dtype == MIA_F32) {
+    MIA_CHECK_ARG(N <= MAXN, "attn_fwd f32: N must be <= %d", MAXN);
+    attn_fwd_f32_kernel<<<dim3((unsigned)cdiv(N, 4), (unsigned)(B * H)), 256, 0, as_stream(stream)>>>(
+        (const float*)qkv, (float*)out, lse, N, H, scale);
+    MIA_LAUNCH_CHECK("attn_fwd_f32");
+    return 0;
+  }
+  MIA_CHECK_ARG(dtype == MIA_BF16, "attn_fwd: dtype");
+  dim3 grid((unsigned)cdiv(N, 128), (unsigned)(B * H));
+  attn_fwd_kernel<<<grid, 256, 0, as_stream(stream)>>>((const bf16*)qkv, (bf16*)out, lse, N, H, scale * LOG2E);
+  MIA_LAUNCH_CHECK("attn_fwd");
+  return 0;
+}
+
+extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                            float* delta, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
+                            mia_stream_t stream) {
+  MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && delta, "attn_bwd: null pointer");
+  MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_bwd: bad shape");
+  hipStream_t s = as_stream(stream);
+  const int64_t rows = (int64_t)B * N * H;
+  if (dtype == MIA_F32) {
+    MIA_CHECK_ARG(N <= MAXN, "attn_bwd f32: N must be <= %d", MAXN);
+    attn_delta_f32_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
+        (const float*)out, (const float*)dout, delta, B, N, H);
+    MIA_LAUNCH_CHECK("attn_delta_f32");
+    dim3 g4((unsigned)cdiv(N, 4), (unsigned)(B * H));
+    attn_bwd_dq_f32_kernel<<<g4, 256, 0, s>>>((const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv, N, H,
+                                              scale);
+    MIA_LAUNCH_CHECK("attn_bwd_dq_f32");
+    attn_bwd_dkdv_f32_kernel<<<g4, 256, 0, s>>>((const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv, N,
+                                                H, scale);
+    MIA_LAUNCH_CHECK("attn_bwd_dkdv_f32");
+    return 0;
+  }
+  MIA_CHECK_ARG(dtype == MIA_BF16, "attn_bwd: dtype");
+  attn_delta_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
+      (const bf16*)out, (const bf16*)dout, delta, B, N, H);
+  MIA_LAUNCH_CHECK("attn_delta");
+  dim3 grid((unsigned)cdiv(N, 128), (unsigned)(B * H));
+  attn_bwd_dkdv_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale,
+                                            scale * LOG2E);
+  MIA_LAUNCH_CHECK("attn_bwd_dkdv");
+  attn_bwd_dq_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale,
+                                          scale * LOG2E);
+  MIA_LAUNCH_CHECK("attn_bwd_dq");
+  return 0;
+}

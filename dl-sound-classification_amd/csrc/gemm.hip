@@ -407,6 +407,7 @@ __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n,
       break;
     }
     case MIA_DACT_GELU: v *= gelu_erf_grad(ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n)); break;
+    case MIA_ACT_ADD_AUX: v += ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n); break;
     default: break;
   }
   int64_t prow = m;
@@ -619,7 +620,8 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   if (int r = check_operand(*B, "B")) return r;
   MIA_CHECK_ARG(E->ptr != nullptr, "gemm: output is null");
   MIA_CHECK_ARG(compute_dtype == MIA_F32 || compute_dtype == MIA_BF16, "gemm: compute dtype");
-  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU) MIA_CHECK_ARG(E->aux != nullptr, "gemm: dact needs aux");
+  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU || E->act == MIA_ACT_ADD_AUX)
+    MIA_CHECK_ARG(E->aux != nullptr, "gemm: this epilogue needs aux");
   if (split_k < 1) split_k = 1;
   if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");
   if (M == 0 || N == 0) return 0;

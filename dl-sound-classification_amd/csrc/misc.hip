@@ -238,8 +238,15 @@ __global__ void tokens_bwd_kernel(const float* __restrict__ dout, float* __restr
 }
 
 // ------------------------------------------------------------------ BC mixing
-__global__ __launch_bounds__(NT) void clip_ms_kernel(const float* __restrict__ x, int64_t T, float* __restrict__ ms) {
-  const float* r = x + (int64_t)blockIdx.x * T;
+// mean square of row idx[blockIdx.x] (or blockIdx.x) of x
+__global__ __launch_bounds__(NT) void clip_ms_kernel(const float* __restrict__ x, int64_t T, const int* __restrict__ idx,
+                                                     float* __restrict__ ms) {
+  int row = blockIdx.x;
+  if (idx) {
+    row = idx[blockIdx.x];
+    if (row < 0) { if (threadIdx.x == 0) ms[blockIdx.x] = 0.f; return; }
+  }
+  const float* r = x + (int64_t)row * T;
   double s = 0.0;
   for (int64_t i = threadIdx.x; i < T; i += NT) s += (double)r[i] * r[i];
   s = wave_sum_d(s);
@@ -254,17 +261,19 @@ __device__ __forceinline__ float spl_db(float ms) {  // BCMixingUtils.a_weighted
   return rms > 0.f ? 20.f * log10f(rms) + 94.f : -80.f;
 }
 
-// single block: every thread reads the mean squares it needs before any thread overwrites them
-__global__ void bc_coef_kernel(float* ms_then_p, const int* __restrict__ partner, const float* __restrict__ r,
-                               const int64_t* __restrict__ labels, int B, int C, float* __restrict__ yout) {
-  const int b = threadIdx.x;
-  const bool act = b < B;
-  const int q = act ? partner[b] : -1;
-  const float rr = act ? r[b] : 0.f;
+// one thread per clip: ms[b] (own clip) and msq[b] (partner) -> p, soft labels
+__global__ void bc_coef_kernel(const float* __restrict__ ms, const float* __restrict__ msq,
+                               const int* __restrict__ partner, const float* __restrict__ r,
+                               const int64_t* __restrict__ labels, const int64_t* __restrict__ pool_labels, int B,
+                               int C, float* __restrict__ p_out, float* __restrict__ yout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int q = partner[b];
+  const float rr = r[b];
   float p = 1.f;
-  if (act && q >= 0) {
+  if (q >= 0) {
     // perceptual_mixing_coefficient (preprocessing.py:418-446)
-    const float d = spl_db(ms_then_p[b]) - spl_db(ms_then_p[q]);
+    const float d = spl_db(ms[b]) - spl_db(msq[b]);
     p = rr;
     if (fabsf(d) > 10.f) {
       const float adj = fminf(fabsf(d) / 40.f, 0.3f);
@@ -272,37 +281,35 @@ __global__ void bc_coef_kernel(float* ms_then_p, const int* __restrict__ partner
     }
     p = fminf(fmaxf(p, 0.f), 1.f);
   }
-  __syncthreads();
-  if (!act) return;
-  ms_then_p[b] = p;
+  p_out[b] = p;
   if (yout) {
     for (int c = 0; c < C; ++c) yout[(int64_t)b * C + c] = 0.f;
     if (q >= 0) {
       yout[(int64_t)b * C + labels[b]] = rr;                   // create_soft_labels: uses r, not p
-      yout[(int64_t)b * C + labels[q]] = 1.f - rr;
+      yout[(int64_t)b * C + pool_labels[q]] = 1.f - rr;
     } else {
       yout[(int64_t)b * C + labels[b]] = 1.f;
     }
   }
 }
 
-__global__ void bc_mix_kernel(const float* __restrict__ x, int64_t T, int B, const int* __restrict__ partner,
-                              const float* __restrict__ p_in, float* __restrict__ out) {
+__global__ void bc_mix_kernel(const float* __restrict__ x, const float* __restrict__ pool, int64_t T, int B,
+                              const int* __restrict__ partner, const float* __restrict__ p_in, float* __restrict__ out) {
   const int b = blockIdx.y;
   const int q = partner[b];
   const float p = p_in[b];
   const float norm = sqrtf(p * p + (1.f - p) * (1.f - p));
   const float* xa = x + (int64_t)b * T;
-  const float* xb = x + (int64_t)(q >= 0 ? q : b) * T;
+  const float* xb = pool + (int64_t)(q >= 0 ? q : 0) * T;
   float* o = out + (int64_t)b * T;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x)
     o[i] = q >= 0 ? (p * xa[i] + (1.f - p) * xb[i]) / norm : xa[i];
 }
 
 // ------------------------------------------------------------------ SpecAugment + Mixup
-__global__ void specaug_mixup_kernel(const float* __restrict__ spec, float* __restrict__ out, int B, int F, int T,
-                                     const int* t0, const int* tl, const int* f0, const int* fl, const int* partner,
-                                     const float* lam) {
+__global__ void specaug_mixup_kernel(const float* __restrict__ spec, const float* __restrict__ pool,
+                                     float* __restrict__ out, int B, int F, int T, const int* t0, const int* tl,
+                                     const int* f0, const int* fl, const int* partner, const float* lam) {
   const int b = blockIdx.y;
   const int64_t per = (int64_t)F * T;
   const int q = partner ? partner[b] : -1;
@@ -313,7 +320,7 @@ __global__ void specaug_mixup_kernel(const float* __restrict__ spec, float* __re
     const int t = (int)(i % T), f = (int)(i / T);
     float v = spec[(int64_t)b * per + i];
     if ((t >= ts && t < te) || (f >= fs && f < fe)) v = 0.f;
-    if (q >= 0) v = l * v + (1.f - l) * spec[(int64_t)q * per + i];
+    if (q >= 0) v = l * v + (1.f - l) * pool[(int64_t)q * per + i];
     out[(int64_t)b * per + i] = v;
   }
 }
@@ -414,31 +421,36 @@ extern "C" int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, f
   return 0;
 }
 
-extern "C" int mia_bc_mix(const float* x, int64_t T, int32_t B, const int32_t* partner, const float* r,
-                          const int64_t* labels, int32_t num_classes, float* out, float* yout, float* p_out,
-                          mia_stream_t stream) {
-  MIA_CHECK_ARG(x && partner && r && labels && out && p_out && B > 0 && T > 0, "bc_mix: args");
+extern "C" int mia_bc_mix(const float* x, const float* pool, int64_t T, int32_t B, const int32_t* partner,
+                          const float* r, const int64_t* labels, const int64_t* pool_labels, int32_t num_classes,
+                          float* out, float* yout, float* p_out, void* workspace, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && pool && partner && r && labels && pool_labels && out && p_out && workspace && B > 0 && T > 0,
+                "bc_mix: args");
+  MIA_CHECK_ARG(out != x && out != pool, "bc_mix: out must not alias the inputs");
   hipStream_t s = as_stream(stream);
-  // mean squares are parked in p_out first (overwritten by the coefficients)
-  clip_ms_kernel<<<B, NT, 0, s>>>(x, T, p_out);
+  float* ms = reinterpret_cast<float*>(workspace);
+  float* msq = ms + B;
+  clip_ms_kernel<<<B, NT, 0, s>>>(x, T, nullptr, ms);
   MIA_LAUNCH_CHECK("clip_ms");
-  // coefficient kernel reads ms from p_out and writes p into p_out: run it in a single block,
-  // reading everything before writing (B <= 1024)
-  MIA_CHECK_ARG(B <= 1024, "bc_mix: B must be <= 1024");
-  bc_coef_kernel<<<1, 1024, 0, s>>>(p_out, partner, r, labels, B, num_classes, yout);
+  clip_ms_kernel<<<B, NT, 0, s>>>(pool, T, partner, msq);
+  MIA_LAUNCH_CHECK("clip_ms(partner)");
+  bc_coef_kernel<<<(unsigned)cdiv(B, 256), 256, 0, s>>>(ms, msq, partner, r, labels, pool_labels, B, num_classes,
+                                                        p_out, yout);
   MIA_LAUNCH_CHECK("bc_coef");
-  bc_mix_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 512), B), 256, 0, s>>>(x, T, B, partner, p_out, out);
+  bc_mix_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 512), B), 256, 0, s>>>(x, pool, T, B, partner, p_out,
+                                                                                      out);
   MIA_LAUNCH_CHECK("bc_mix");
   return 0;
 }
 
-extern "C" int mia_spec_augment_mixup(const float* spec, float* out, int32_t B, int32_t F, int32_t T, const int32_t* t0,
-                                      const int32_t* tlen, const int32_t* f0, const int32_t* flen,
-                                      const int32_t* partner, const float* lam, mia_stream_t stream) {
+extern "C" int mia_spec_augment_mixup(const float* spec, const float* pool, float* out, int32_t B, int32_t F,
+                                      int32_t T, const int32_t* t0, const int32_t* tlen, const int32_t* f0,
+                                      const int32_t* flen, const int32_t* partner, const float* lam,
+                                      mia_stream_t stream) {
   MIA_CHECK_ARG(spec && out && B > 0 && F > 0 && T > 0, "spec_augment_mixup: args");
-  MIA_CHECK_ARG(spec != out || partner == nullptr, "spec_augment_mixup: in-place mixup is not allowed");
+  MIA_CHECK_ARG(!partner || (pool && pool != out), "spec_augment_mixup: mixup needs a pool distinct from out");
   specaug_mixup_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv((int64_t)F * T, 256), 512), B), 256, 0,
-                         as_stream(stream)>>>(spec, out, B, F, T, t0, tlen, f0, flen, partner, lam);
+                         as_stream(stream)>>>(spec, pool ? pool : spec, out, B, F, T, t0, tlen, f0, flen, partner, lam);
   MIA_LAUNCH_CHECK("spec_augment_mixup");
   return 0;
 }

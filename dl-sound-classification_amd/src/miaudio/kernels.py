@@ -112,6 +112,28 @@ def auto_split(M: int, N: int, K: int, target_blocks: int = 1024, min_k: int = 1
 PROBE: dict | None = None
 
 
+class probe:
+    """Times the enclosed launches with HIP events on the current stream when ``tag`` is being probed
+    (bench.py's live per-kernel roofline); ``flop`` / ``nbytes`` are the algorithmic work of the launch."""
+
+    def __init__(self, tag: str, flop: float, nbytes: float):
+        self.tag, self.flop, self.nbytes = tag, flop, nbytes
+        self.on = PROBE is not None and tag in PROBE
+
+    def __enter__(self):
+        if self.on:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on and exc[0] is None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            PROBE[self.tag].append((self.e0, e1, self.flop, self.nbytes))
+        return False
+
+
 def _operand_bytes(o: L.MiaOperand, M_or_N: int, K: int) -> int:
     es = 4 if o.dtype == L.F32 else 2
     if o.kind == L.OP_DENSE:

@@ -19,7 +19,7 @@ F32, BF16, U8 = 0, 1, 2
 OP_DENSE, OP_CONV, OP_CONVROW = 0, 1, 2
 KC, RC = 0, 1
 PRE_NONE, PRE_AFFINE, PRE_AFFINE_RELU, PRE_GELU = 0, 1, 2, 3
-ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU = 0, 1, 2, 3, 4
+ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU, ACT_ADD_AUX = 0, 1, 2, 3, 4, 5
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -74,14 +74,14 @@ SIGNATURES = {
     "mia_layernorm_fwd": (C.c_int, [vp, i32, vp, vp, vp, i32, vp, vp, i64, i32, f32, vp]),
     "mia_layernorm_bwd": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, i64, i32, vp]),
     "mia_layernorm_partial_bytes": (i64, [i64, i32]),
-    "mia_attn_fwd": (C.c_int, [vp, vp, vp, i32, i32, i32, f32, vp]),
-    "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
+    "mia_attn_fwd": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, f32, vp]),
+    "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_tokens_fwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_tokens_bwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_cast": (C.c_int, [vp, i32, vp, i32, i64, vp]),
     "mia_add_inplace": (C.c_int, [vp, vp, i32, i64, vp]),
-    "mia_bc_mix": (C.c_int, [vp, i64, i32, vp, vp, vp, i32, vp, vp, vp, vp]),
-    "mia_spec_augment_mixup": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mia_bc_mix": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
+    "mia_spec_augment_mixup": (C.c_int, [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mia_last_error_string": (C.c_char_p, []),
     "mia_device_arch": (C.c_int, [C.c_char_p, i32]),
 }

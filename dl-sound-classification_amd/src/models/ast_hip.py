@@ -1,0 +1,201 @@
+"""AST forward/backward on the MI355X kernels (one autograd node for the whole transformer).
+
+Reference op sequence: src/models/ast.py:50-63 + timm 1.0.16 Block (pre-LN, qkv Linear with bias,
+SDPA, proj, LN, fc1, exact-erf GELU, fc2), LN eps 1e-6, sigmoid head on the CLS token.
+HBM layout per block (T = B*1645 tokens, D = 768): residual stream x (T, 768) f32; LN outputs,
+qkv (T, 3, 12, 64), attention output (T, 12, 64) and fc1 pre-activation (T, 3072) in the compute
+dtype.  GELU is never materialised: fc2 applies it while staging its operand (MIA_PRE_GELU) and the
+fc1 backward applies gelu' in the epilogue of the dgrad GEMM (MIA_DACT_GELU); residual adds are GEMM
+epilogues (MIA_ACT_ADD_AUX / accumulate).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..miaudio import kernels as K
+from ..miaudio import lib as L
+
+EPS = 1e-6
+
+
+def _ln(x, g, b, out_dtype, rows, D):
+    y = torch.empty(rows, D, dtype=out_dtype, device=x.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    L.check(L.load().mia_layernorm_fwd(x.data_ptr(), L.dtype_code(x), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                       L.dtype_code(y), mean.data_ptr(), rstd.data_ptr(), rows, D, EPS, L.stream_ptr()),
+            "mia_layernorm_fwd")
+    return y, mean, rstd
+
+
+def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool):
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    lib = L.load()
+    ws = K.workspace(lib.mia_layernorm_partial_bytes(rows, D), x.device, "ln")
+    L.check(lib.mia_layernorm_bwd(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x), g.data_ptr(),
+                                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), L.dtype_code(dx), int(accumulate),
+                                  dg.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, D, L.stream_ptr()),
+            "mia_layernorm_bwd")
+    return dg, db
+
+
+def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, tag=None):
+    """out[M, N] = act(x[M, K] @ W[N, K]^T + bias)"""
+    Nf, Kf = W.shape
+    K.gemm(K.dense(x, L.KC, M, Kf, pre=pre), K.dense(W, L.KC, Nf, Kf),
+           K.epilogue(out, Nf, act=act, bias=bias, aux=aux, ldaux=Nf), M, Nf, Kf, cd, tag=tag)
+
+
+def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag=""):
+    """dW = dy^T x (f32), db = colsum(dy), dx = dy @ W (optionally with an activation backward)."""
+    Nf, Kf = W.shape
+    dW = torch.empty(Nf, Kf, dtype=torch.float32, device=dy.device)
+    K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf), Nf, Kf, M, cd,
+           tag=tag + ".wgrad")
+    db = K.colsum(dy, M, Nf)
+    if dx_out is not None:
+        K.gemm(K.dense(dy, L.KC, M, Nf), K.dense(W, L.RC, Nf, Kf),
+               K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf),
+               M, Kf, Nf, cd, tag=tag + ".dgrad")
+    return dW, db
+
+
+class ASTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, spec, compute: int, *params):
+        if not spec.is_cuda:
+            raise RuntimeError("ASTModel runs on the MI355X HIP kernels only (input is on CPU)")
+        cd = compute
+        tdt = L.torch_dtype(cd)
+        dev = spec.device
+        B, Fm, Tf = spec.shape
+        spec = spec.contiguous().float()
+        D, Hh = model.emb_dim, model.num_heads
+        ps, st = model.patch_size, model.patch_stride
+        gh, gw = (Fm - ps) // st + 1, (Tf - ps) // st + 1
+        Np = gh * gw
+        N = Np + 1
+        if N > model.pos_embed.shape[1]:
+            raise ValueError(f"{N} tokens exceed the positional table ({model.pos_embed.shape[1]})")
+        Tt = B * N
+        pw, pb, cls, pos = params[0], params[1], params[2], params[3]
+        # patch embedding: Conv2d(1, D, 16, stride 10) as an implicit GEMM over the 1-channel spectrogram
+        patches = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
+        K.gemm(K.conv(spec, L.KC, B, Fm, Tf, 1, gh, gw, ps, ps, sh=st, sw=st, row_kind=True),
+               K.dense(pw.reshape(D, -1), L.KC, D, ps * ps), K.epilogue(patches, D, bias=pb), B * Np, D, ps * ps, cd,
+               tag="patch.fwd")
+        x = torch.empty(Tt, D, dtype=torch.float32, device=dev)
+        L.check(L.load().mia_tokens_fwd(patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), x.data_ptr(), B, Np, D,
+                                        L.stream_ptr()), "mia_tokens_fwd")
+        saved_blocks = []
+        nb = len(model.transformer)
+        scale = (D // Hh) ** -0.5
+        for i in range(nb):
+            g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = params[4 + 12 * i: 16 + 12 * i]
+            h, m1, r1 = _ln(x, g1, b1, tdt, Tt, D)
+            qkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
+            _linear(h, wqkv, bqkv, qkv, Tt, cd, tag="qkv.fwd")
+            a = torch.empty(Tt, D, dtype=tdt, device=dev)
+            lse = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
+            with K.probe("attn.fwd", 4.0 * B * Hh * N * N * (D // Hh), (qkv.numel() + a.numel()) * qkv.element_size()):
+                L.check(L.load().mia_attn_fwd(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(), cd, B, N, Hh, scale,
+                                              L.stream_ptr()), "mia_attn_fwd")
+            xm = torch.empty(Tt, D, dtype=torch.float32, device=dev)
+            _linear(a, wproj, bproj, xm, Tt, cd, act=L.ACT_ADD_AUX, aux=x, tag="proj.fwd")
+            h2, m2, r2 = _ln(xm, g2, b2, tdt, Tt, D)
+            u = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
+            _linear(h2, w1, bb1, u, Tt, cd, tag="fc1.fwd")
+            xo = torch.empty(Tt, D, dtype=torch.float32, device=dev)
+            _linear(u, w2, bb2, xo, Tt, cd, act=L.ACT_ADD_AUX, aux=xm, pre=L.PRE_GELU, tag="fc2.fwd")
+            saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u))
+            x = xo
+        # final norm only matters for the CLS rows (ast.py:62-63 takes x[:, 0])
+        gn, bn_, wh, bh = params[4 + 12 * nb: 8 + 12 * nb]
+        xc = x.view(B, N, D)[:, 0].contiguous()
+        hc, mc, rc = _ln(xc, gn, bn_, torch.float32, B, D)
+        z = torch.empty(B, wh.shape[0], dtype=torch.float32, device=dev)
+        _linear(hc, wh, bh, z, B, cd, tag="head.fwd")
+        probs = torch.sigmoid(z)
+        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec, gh=gh, gw=gw, blocks=saved_blocks, xc=xc,
+                     mc=mc, rc=rc, hc=hc, probs=probs, scale=scale)
+        ctx.model = model
+        ctx.params = params
+        return probs
+
+    @staticmethod
+    def backward(ctx, dprobs):
+        s, p, model = ctx.s, ctx.params, ctx.model
+        B, N, Np, D, Hh, cd = s["B"], s["N"], s["Np"], s["D"], s["H"], s["cd"]
+        tdt = L.torch_dtype(cd)
+        dev = dprobs.device
+        Tt = B * N
+        nb = len(model.transformer)
+        grads = [None] * len(p)
+        ready = getattr(model, "_grad_ready", None)
+
+        def emit(lo, hi):
+            if ready is None:
+                return
+            ready([(p[i], grads[i]) for i in range(lo, hi)])
+            for i in range(lo, hi):
+                grads[i] = None
+
+        pr = s["probs"]
+        dz = (dprobs.float() * pr * (1.0 - pr)).contiguous()  # sigmoid backward (B x classes)
+        gn, bn_, wh, bh = p[4 + 12 * nb: 8 + 12 * nb]
+        dhc = torch.empty(B, D, dtype=torch.float32, device=dev)
+        dWh, dbh = _linear_bwd(dz, s["hc"], wh, B, cd, dx_out=dhc, tag="head")
+        dxc = torch.empty(B, D, dtype=torch.float32, device=dev)
+        dgn, dbn = _ln_bwd(dhc, s["xc"], gn, s["mc"], s["rc"], dxc, B, D, False)
+        grads[4 + 12 * nb: 8 + 12 * nb] = [dgn, dbn, dWh, dbh]
+        emit(4 + 12 * nb, 8 + 12 * nb)
+        dx = torch.zeros(Tt, D, dtype=torch.float32, device=dev)
+        dx.view(B, N, D)[:, 0] = dxc
+        for i in reversed(range(nb)):
+            sb = s["blocks"][i]
+            g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = p[4 + 12 * i: 16 + 12 * i]
+            # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
+            du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
+            dW2, db2_ = _linear_bwd(dx, sb["u"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
+                                    x_pre=L.PRE_GELU, tag="fc2")
+            dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
+            dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1")
+            dg2, dbt2 = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True)  # dx now = d(xm)
+            da = torch.empty(Tt, D, dtype=tdt, device=dev)
+            dWp, dbp = _linear_bwd(dx, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj")
+            dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
+            delta = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
+            with K.probe("attn.bwd", 10.0 * B * Hh * N * N * (D // Hh),
+                         (2 * dqkv.numel() + 2 * da.numel()) * dqkv.element_size()):
+                L.check(L.load().mia_attn_bwd(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
+                                              sb["lse"].data_ptr(), dqkv.data_ptr(), delta.data_ptr(), cd, B, N, Hh,
+                                              s["scale"], L.stream_ptr()), "mia_attn_bwd")
+            dh = torch.empty(Tt, D, dtype=tdt, device=dev)
+            dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")
+            dg1, dbt1 = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True)  # dx now = d(block input)
+            grads[4 + 12 * i: 16 + 12 * i] = [dg1, dbt1, dWq, dbq, dWp, dbp, dg2, dbt2, dW1, db1_, dW2, db2_]
+            emit(4 + 12 * i, 16 + 12 * i)
+            s["blocks"][i] = None
+        # tokens: dcls, dpos (first N rows of the table), dpatches
+        pos = p[3]
+        dpos = torch.zeros_like(pos)
+        dcls = torch.empty(1, 1, D, dtype=torch.float32, device=dev)
+        dpatch = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
+        L.check(L.load().mia_tokens_bwd(dx.data_ptr(), dpatch.data_ptr(), dcls.data_ptr(), dpos.data_ptr(), B, Np, D,
+                                        L.stream_ptr()), "mia_tokens_bwd")
+        pw = p[0]
+        ps, st = model.patch_size, model.patch_stride
+        spec = s["spec"]
+        Fm, Tf = spec.shape[1], spec.shape[2]
+        dWpe = torch.empty(D, ps * ps, dtype=torch.float32, device=dev)
+        K.gemm(K.dense(dpatch, L.RC, B * Np, D),
+               K.conv(spec, L.RC, B, Fm, Tf, 1, s["gh"], s["gw"], ps, ps, sh=st, sw=st, row_kind=True),
+               K.epilogue(dWpe, ps * ps), D, ps * ps, B * Np, cd, tag="patch.wgrad")
+        grads[0] = dWpe.view_as(pw)
+        grads[1] = K.colsum(dpatch, B * Np, D)
+        grads[2] = dcls
+        grads[3] = dpos
+        emit(0, 4)
+        ctx.s = None
+        return (None, None, None, *grads)

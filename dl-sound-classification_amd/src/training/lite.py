@@ -1,0 +1,295 @@
+"""The slice of the Lightning 2.5 API the reference drives (lightning is not installed here):
+``LightningModule`` (log, current_epoch, save_hyperparameters, hparams, trainer/logger handles) and a
+``Trainer(max_epochs, accelerator, precision, devices, gradient_clip_val, log_every_n_steps, ...)``
+with ``fit(module, datamodule, ckpt_path)`` / ``test(ckpt_path="best", datamodule)``, top-1
+ModelCheckpoint + EarlyStopping on a monitored metric (reference callbacks.py:32-63,
+base_training.yaml:109-123) and a CSV/JSON metrics logger in place of MLflow.
+
+Data parallelism: with ``devices > 1`` the script is launched one process per GPU
+(torch.distributed.run); the trainer joins the RCCL process group, shards the clips across ranks
+(DistributedSampler semantics) and exchanges gradients with ``GradAllReducer`` (ddp.py).
+Precision: "32" -> f32 kernels; "bf16-mixed" -> bf16 MFMA compute with f32 master weights, f32
+gradients and f32 Adam state (Lightning bf16-mixed semantics).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+
+class LightningModule(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.trainer = None
+        self.logger = None
+        self.datamodule = None
+        self.current_epoch = 0
+        self.global_step = 0
+        self.hparams = {}
+        self._epoch_logs: dict = {}
+
+    def save_hyperparameters(self, d=None, logger=True):
+        if isinstance(d, dict):
+            self.hparams.update(d)
+
+    def log(self, name, value, prog_bar=False, on_step=None, on_epoch=True, sync_dist=False, **kw):
+        v = value.detach() if isinstance(value, torch.Tensor) else torch.tensor(float(value))
+        self._epoch_logs.setdefault(name, []).append(v)
+
+    def _flush_logs(self):
+        out = {k: float(torch.stack([x.float().cpu() for x in v]).mean()) for k, v in self._epoch_logs.items()}
+        self._epoch_logs = {}
+        return out
+
+
+class CSVLogger:
+    def __init__(self, save_dir="outputs", experiment_name="default"):
+        self.log_dir = str(Path(save_dir) / experiment_name / time.strftime("%Y%m%d-%H%M%S"))
+        self.run_id = Path(self.log_dir).name
+        self.rows = []
+
+    def log_metrics(self, metrics: dict, step: int):
+        self.rows.append({"step": step, **metrics})
+        Path(self.log_dir).mkdir(parents=True, exist_ok=True)
+        with open(Path(self.log_dir) / "metrics.jsonl", "a") as f:
+            f.write(json.dumps({"step": step, **metrics}) + "\n")
+
+    def log_hyperparams(self, params: dict):
+        Path(self.log_dir).mkdir(parents=True, exist_ok=True)
+        with open(Path(self.log_dir) / "hparams.json", "w") as f:
+            json.dump(params, f, indent=1, default=str)
+
+    def save_tensor(self, name, t):
+        Path(self.log_dir).mkdir(parents=True, exist_ok=True)
+        torch.save(t.cpu(), Path(self.log_dir) / name)
+
+
+class ModelCheckpoint:
+    def __init__(self, monitor="val/acc", mode="max", dirpath="checkpoints", save_top_k=1,
+                 filename="epoch-{epoch:02d}", **kw):
+        self.monitor, self.mode, self.dirpath, self.filename = monitor, mode, dirpath, filename
+        self.best_score, self.best_model_path = None, ""
+
+    def _better(self, v):
+        return self.best_score is None or (v > self.best_score if self.mode == "max" else v < self.best_score)
+
+    def on_epoch_end(self, trainer, module, metrics):
+        if self.monitor not in metrics or not trainer.is_global_zero:
+            return
+        v = metrics[self.monitor]
+        if self._better(v):
+            self.best_score = v
+            fmt = {k.replace("/", "_"): val for k, val in metrics.items()}
+            fmt["epoch"] = module.current_epoch
+            name = self.filename
+            for k in metrics:
+                name = name.replace("{" + k, "{" + k.replace("/", "_"))
+            name = name.format(**fmt)
+            Path(self.dirpath).mkdir(parents=True, exist_ok=True)
+            path = str(Path(self.dirpath) / f"{name}.ckpt")
+            if self.best_model_path and os.path.exists(self.best_model_path):
+                os.remove(self.best_model_path)
+            trainer.save_checkpoint(path)
+            self.best_model_path = path
+
+
+class EarlyStopping:
+    def __init__(self, monitor="val/acc", mode="max", patience=40, min_delta=0.0, **kw):
+        self.monitor, self.mode, self.patience, self.min_delta = monitor, mode, patience, min_delta
+        self.best, self.wait = None, 0
+
+    def on_epoch_end(self, trainer, module, metrics):
+        if self.monitor not in metrics:
+            return
+        v = metrics[self.monitor]
+        improved = self.best is None or (v > self.best + self.min_delta if self.mode == "max"
+                                         else v < self.best - self.min_delta)
+        if improved:
+            self.best, self.wait = v, 0
+        else:
+            self.wait += 1
+            if self.wait >= self.patience:
+                trainer.should_stop = True
+
+
+def _to(batch, dev):
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(_to(b, dev) for b in batch)
+    if isinstance(batch, dict):
+        return {k: _to(v, dev) for k, v in batch.items()}
+    if isinstance(batch, torch.Tensor):
+        return batch.to(dev, non_blocking=True)
+    return batch
+
+
+class Trainer:
+    def __init__(self, max_epochs=1, accelerator="auto", precision=32, devices=1, log_every_n_steps=50,
+                 gradient_clip_val=0.0, logger=None, callbacks=None, limit_train_batches=None,
+                 limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, **unused):
+        self.max_epochs = int(max_epochs)
+        self.gradient_clip_val = float(gradient_clip_val or 0.0)
+        self.precision = str(precision)
+        self.devices = devices
+        self.log_every_n_steps = log_every_n_steps
+        self.logger = logger
+        self.callbacks = list(callbacks or [])
+        self.limits = {"train": limit_train_batches, "val": limit_val_batches, "test": limit_test_batches}
+        self.should_stop = False
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        use_gpu = accelerator in ("gpu", "cuda") or (accelerator == "auto" and torch.cuda.is_available())
+        if accelerator == "cpu":
+            use_gpu = False
+        self.device = torch.device("cuda", self.local_rank) if use_gpu else torch.device("cpu")
+        if self.world > 1 and not dist.is_initialized():
+            if use_gpu:
+                torch.cuda.set_device(self.device)
+                dist.init_process_group("nccl", device_id=self.device)
+            else:
+                dist.init_process_group("gloo")
+        self.is_global_zero = self.rank == 0
+        self.ddp = None
+        self.optimizer = None
+        self.scheduler = None
+        self.callback_metrics = {}
+        self.datamodule = None
+
+    # ------------------------------------------------------------------ helpers
+    def _prepare(self, module, datamodule):
+        self.datamodule = datamodule
+        module.trainer = self
+        module.logger = self.logger
+        module.datamodule = datamodule
+        if hasattr(datamodule, "attach"):
+            datamodule.attach(self.device, self.world, self.rank)
+        module.to(self.device)
+        cd = "bf16" if "bf16" in self.precision else "f32"
+        for m in module.modules():
+            if hasattr(m, "compute_dtype"):
+                m.compute_dtype = cd
+
+    def _limit(self, stage, n):
+        lim = self.limits[stage]
+        if lim is None:
+            return n
+        return int(lim) if (isinstance(lim, int) or float(lim) > 1) else max(1, int(math.ceil(float(lim) * n)))
+
+    def save_checkpoint(self, path):
+        m = self._module
+        torch.save({"state_dict": m.state_dict(), "epoch": m.current_epoch, "global_step": m.global_step,
+                    "optimizer_states": [self.optimizer.state_dict()] if self.optimizer else [],
+                    "hyper_parameters": m.hparams}, path)
+
+    def _load(self, module, path):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        module.load_state_dict(ck["state_dict"])
+        return ck
+
+    def _run_eval(self, module, loader, stage):
+        module.eval()
+        n = self._limit(stage, len(loader))
+        with torch.no_grad():
+            for i, batch in enumerate(loader):
+                if i >= n:
+                    break
+                batch = _to(batch, self.device)
+                (module.validation_step if stage == "val" else module.test_step)(batch, i)
+        getattr(module, f"on_{'validation' if stage == 'val' else 'test'}_epoch_end")()
+        return module._flush_logs()
+
+    # ------------------------------------------------------------------ fit / test
+    def fit(self, module, datamodule=None, ckpt_path=None):
+        self._module = module
+        self._prepare(module, datamodule)
+        datamodule.setup("fit")
+        opt_cfg = module.configure_optimizers()
+        if isinstance(opt_cfg, dict):
+            self.optimizer = opt_cfg["optimizer"]
+            sch = opt_cfg.get("lr_scheduler")
+            self.scheduler = sch["scheduler"] if isinstance(sch, dict) else sch
+        else:
+            self.optimizer = opt_cfg
+        start_epoch = 0
+        if ckpt_path:
+            ck = self._load(module, ckpt_path)
+            if ck.get("optimizer_states"):
+                self.optimizer.load_state_dict(ck["optimizer_states"][0])
+            start_epoch = ck.get("epoch", -1) + 1
+        if self.world > 1:
+            from .ddp import GradAllReducer
+            self.ddp = GradAllReducer(module, self.world)
+        if self.logger is not None and self.is_global_zero:
+            self.logger.log_hyperparams(module.hparams)
+        fused_clip = getattr(self.optimizer, "handles_clipping", False)
+        for epoch in range(start_epoch, self.max_epochs):
+            module.current_epoch = epoch
+            module.train()
+            loader = datamodule.train_dataloader()
+            if hasattr(loader, "set_epoch"):
+                loader.set_epoch(epoch)
+            n = self._limit("train", len(loader))
+            for i, batch in enumerate(loader):
+                if i >= n:
+                    break
+                batch = _to(batch, self.device)
+                loss = module.training_step(batch, i)
+                loss.backward()
+                if self.ddp is not None:
+                    self.ddp.finish()
+                if self.gradient_clip_val > 0 and not fused_clip:
+                    torch.nn.utils.clip_grad_norm_(module.parameters(), self.gradient_clip_val)
+                self.optimizer.step()
+                self.optimizer.zero_grad(set_to_none=True)
+                module.global_step += 1
+            train_logs = module._flush_logs()
+            val_logs = {}
+            if hasattr(datamodule, "val_dataloader"):
+                val_logs = self._run_eval(module, datamodule.val_dataloader(), "val")
+                module.train()
+            module.on_train_epoch_end()
+            train_logs.update(module._flush_logs())
+            if self.scheduler is not None:
+                self.scheduler.step()
+            metrics = {**train_logs, **val_logs, "epoch": epoch,
+                       "lr": self.optimizer.param_groups[0]["lr"]}
+            self.callback_metrics = metrics
+            if self.logger is not None and self.is_global_zero:
+                self.logger.log_metrics(metrics, module.global_step)
+            if self.is_global_zero:
+                print(json.dumps({k: round(v, 5) if isinstance(v, float) else v for k, v in metrics.items()}),
+                      flush=True)
+            for cb in self.callbacks:
+                cb.on_epoch_end(self, module, metrics)
+            if self.world > 1:
+                stop = torch.tensor([1.0 if self.should_stop else 0.0], device=self.device)
+                dist.all_reduce(stop)
+                self.should_stop = bool(stop.item() > 0)
+            if self.should_stop:
+                break
+
+    def test(self, module=None, ckpt_path=None, datamodule=None):
+        module = module or self._module
+        datamodule = datamodule or self.datamodule
+        self._module = module
+        self._prepare(module, datamodule)
+        if ckpt_path == "best":
+            best = next((cb.best_model_path for cb in self.callbacks if isinstance(cb, ModelCheckpoint)), "")
+            if best and os.path.exists(best):
+                self._load(module, best)
+        elif ckpt_path:
+            self._load(module, ckpt_path)
+        datamodule.setup("test")
+        logs = self._run_eval(module, datamodule.test_dataloader(), "test")
+        if self.logger is not None and self.is_global_zero:
+            self.logger.log_metrics(logs, module.global_step)
+        if self.is_global_zero:
+            print(json.dumps({k: round(v, 5) for k, v in logs.items()}), flush=True)
+        return [logs]

@@ -32,7 +32,8 @@ enum { MIA_F32 = 0, MIA_BF16 = 1, MIA_U8 = 2 };
 enum { MIA_OP_DENSE = 0, MIA_OP_CONV = 1, MIA_OP_CONVROW = 2 };
 enum { MIA_LAYOUT_KC = 0, MIA_LAYOUT_RC = 1 };
 enum { MIA_PRE_NONE = 0, MIA_PRE_AFFINE = 1, MIA_PRE_AFFINE_RELU = 2, MIA_PRE_GELU = 3 };
-enum { MIA_ACT_NONE = 0, MIA_ACT_RELU = 1, MIA_ACT_GELU = 2, MIA_DACT_NZ = 3, MIA_DACT_GELU = 4 };
+enum { MIA_ACT_NONE = 0, MIA_ACT_RELU = 1, MIA_ACT_GELU = 2, MIA_DACT_NZ = 3, MIA_DACT_GELU = 4,
+       MIA_ACT_ADD_AUX = 5 };
 
 /* A GEMM operand = a logical 2-D source S[i][j] whose j axis is contiguous in memory.
  *  DENSE   : S[i][j] = ptr[i*ld + j], i < rows, j < cols (zero outside).
@@ -60,7 +61,8 @@ typedef struct MiaOperand {
  *   ptr[prow(m)*ldc + n] with prow(m) = m if rm_inner == 0 else
  *   (m / rm_inner)*rm_outer + (m % rm_inner)*rm_istride + rm_offset.
  *   DACT_NZ  : v *= (aux[m][n] != 0) * act_scale   (ReLU+dropout backward from saved output)
- *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation) */
+ *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation)
+ *   ADD_AUX  : v += aux[m][n]                       (residual connection into a new tensor) */
 typedef struct MiaEpilogue {
   void* ptr;
   int32_t dtype, act, accumulate, aux_dtype;
@@ -201,14 +203,17 @@ int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xd
 int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
 
 /* Fused multi-head attention (timm Attention with F.scaled_dot_product_attention,
- * ast.py:60-61), bf16 MFMA, online softmax, head_dim 64.
- * qkv: (B, N, 3, H, 64) bf16 (the qkv Linear output as is); out: (B, N, H, 64) bf16;
+ * ast.py:60-61), head_dim 64.  dtype MIA_BF16: flash kernel on bf16 MFMA with online softmax;
+ * dtype MIA_F32: exact-f32 reference-precision kernels (parity mode, N <= 3328).
+ * qkv: (B, N, 3, H, 64) (the qkv Linear output as is); out: (B, N, H, 64);
  * lse: f32 (B, H, N) saved for backward. */
-int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t B, int32_t N, int32_t H,
-                 float scale, mia_stream_t stream);
-/* dqkv: (B, N, 3, H, 64) bf16; delta workspace f32 (B,H,N); dq_acc f32 (B,N,H,64). */
+int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtype, int32_t B, int32_t N,
+                 int32_t H, float scale, mia_stream_t stream);
+/* Deterministic backward (key-parallel dK/dV kernel + query-parallel dQ kernel, no atomics).
+ * dout: (B, N, H, 64) bf16; dqkv: (B, N, 3, H, 64) bf16 (fully written);
+ * delta: f32 (B, H, N) workspace (rowsum(dO * O)). */
 int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
-                 void* dqkv, float* delta, float* dq_acc, int32_t B, int32_t N, int32_t H,
+                 void* dqkv, float* delta, int32_t dtype, int32_t B, int32_t N, int32_t H,
                  float scale, mia_stream_t stream);
 
 /* AST token assembly (ast.py:56-59): x[b][0] = cls + pos[0]; x[b][1+p] = patches[b][p] + pos[1+p].
@@ -225,15 +230,20 @@ int mia_cast(const void* src, int32_t sdtype, void* dst, int32_t ddtype, int64_t
 int mia_add_inplace(float* x, const void* y, int32_t ydtype, int64_t numel, mia_stream_t stream);
 
 /* Between-class mixing on device (BCMixingDataset.apply_bc_mixing, preprocessing.py:564-609):
- * out[b] = (p*x[b] + (1-p)*x[partner[b]]) / sqrt(p^2+(1-p)^2) where p is r[b] adjusted by
- * the RMS-"SPL" rule (preprocessing.py:395-471); soft labels use r (not p). */
-int mia_bc_mix(const float* x, int64_t T, int32_t B, const int32_t* partner, const float* r,
-               const int64_t* labels, int32_t num_classes, float* out, float* yout,
-               float* p_out, mia_stream_t stream);
-/* SpecAugment zero masks + Mixup (preprocessing.py:1075-1104, esc50.py:52-76) on
- * (B, F, T) spectrograms, parameters drawn by the caller. */
-int mia_spec_augment_mixup(const float* spec, float* out, int32_t B, int32_t F, int32_t T,
-                           const int32_t* t0, const int32_t* tlen, const int32_t* f0,
+ * partner clips come from a resident pool (the preloaded training set, or the batch itself):
+ * out[b] = (p*x[b] + (1-p)*pool[partner[b]]) / sqrt(p^2+(1-p)^2), p = r[b] adjusted by the
+ * RMS-"SPL" rule (preprocessing.py:395-471); soft labels use r (not p) at labels[b] and
+ * pool_labels[partner[b]]; partner < 0 keeps the clip (one-hot label).
+ * workspace: 2*B floats. */
+int mia_bc_mix(const float* x, const float* pool, int64_t T, int32_t B, const int32_t* partner,
+               const float* r, const int64_t* labels, const int64_t* pool_labels,
+               int32_t num_classes, float* out, float* yout, float* p_out, void* workspace,
+               mia_stream_t stream);
+/* SpecAugment zero masks then Mixup with an un-augmented partner from `pool`
+ * (preprocessing.py:1075-1104, esc50.py:52-76) on (B, F, T) spectrograms; masks and partners
+ * (partner < 0: no mixup) drawn by the caller. */
+int mia_spec_augment_mixup(const float* spec, const float* pool, float* out, int32_t B, int32_t F,
+                           int32_t T, const int32_t* t0, const int32_t* tlen, const int32_t* f0,
                            const int32_t* flen, const int32_t* partner, const float* lam,
                            mia_stream_t stream);
 

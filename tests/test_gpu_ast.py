@@ -1,0 +1,155 @@
+"""GPU: attention / LayerNorm kernels vs float64 torch, and ASTModel (HIP path) vs the reference's
+golden outputs (reference ASTModel code run with the offline timm restatement + hash DeiT weights).
+f32 compute: probabilities within 1e-3 rel, argmax exact.  bf16 compute: argmax exact, 5e-2."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ast as oast
+from oracle.synth import hash_uniform
+from src.miaudio import lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _attn_ref(qkv, B, N, H):
+    q, k, v = qkv.double().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)
+    q.requires_grad_(True), k.requires_grad_(True), v.requires_grad_(True)
+    o = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ v
+    return q, k, v, o
+
+
+@pytest.mark.parametrize("dt", [L.BF16, L.F32])
+@pytest.mark.parametrize("B,N,H", [(2, 100, 2), (1, 257, 3), (2, 1645, 1)])
+def test_attention_fwd_bwd(cuda, dt, B, N, H):
+    g = torch.Generator().manual_seed(N + H)
+    tdt = torch.bfloat16 if dt == L.BF16 else torch.float32
+    qkv = (torch.randn(B, N, 3 * H * 64, generator=g) * 1.5).to(tdt)
+    dout = torch.randn(B, N, H * 64, generator=g).to(tdt)
+    q, k, v, o = _attn_ref(qkv, B, N, H)
+    o.backward(dout.double().view(B, N, H, 64).permute(0, 2, 1, 3))
+    tq = qkv.to(cuda)
+    out = torch.empty(B, N, H * 64, dtype=tdt, device=cuda)
+    lse = torch.empty(B, H, N, device=cuda)
+    lib = L.load()
+    L.check(lib.mia_attn_fwd(tq.data_ptr(), out.data_ptr(), lse.data_ptr(), dt, B, N, H, 0.125, L.stream_ptr()), "fwd")
+    dq = torch.empty_like(tq)
+    delta = torch.empty(B, H, N, device=cuda)
+    L.check(lib.mia_attn_bwd(tq.data_ptr(), out.data_ptr(), dout.to(cuda).data_ptr(), lse.data_ptr(), dq.data_ptr(),
+                             delta.data_ptr(), dt, B, N, H, 0.125, L.stream_ptr()), "bwd")
+    torch.cuda.synchronize()
+    tol = 2e-2 if dt == L.BF16 else 1e-5
+    assert rel(out.view(B, N, H, 64).permute(0, 2, 1, 3), o) < tol
+    dqkv = dq.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    assert rel(dqkv[0], q.grad) < 3 * tol
+    assert rel(dqkv[1], k.grad) < 3 * tol
+    assert rel(dqkv[2], v.grad) < 3 * tol
+
+
+@pytest.mark.parametrize("D", [768, 384])
+def test_layernorm(cuda, D):
+    from src.models.ast_hip import _ln, _ln_bwd
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(300, D, generator=g) * 2 + 1
+    w = torch.rand(D, generator=g) + 0.5
+    b = torch.randn(D, generator=g)
+    xr = x.double().requires_grad_(True)
+    wr, br = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    y = F.layer_norm(xr, (D,), wr, br, 1e-6)
+    dy = torch.randn(300, D, generator=g)
+    y.backward(dy.double())
+    tx, tw, tb = x.to(cuda), w.to(cuda), b.to(cuda)
+    yo, m, r = _ln(tx, tw, tb, torch.float32, 300, D)
+    dx = torch.ones(300, D, device=cuda)
+    dg, db = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx, 300, D, True)
+    torch.cuda.synchronize()
+    assert rel(yo, y) < 1e-5
+    assert rel(dx - 1.0, xr.grad) < 1e-4
+    assert rel(dg, wr.grad) < 1e-4 and rel(db, br.grad) < 1e-4
+
+
+def _ast(cuda, compute):
+    import os
+    os.environ["MIA_QUIET"] = "1"
+    from src.models.ast import ASTModel
+    m = ASTModel(num_classes=50, compute_dtype=compute)
+    m.load_vit_state(oast.deit_hash_state(300))
+    hw, hb = oast.head_hash(900, 50)
+    with torch.no_grad():
+        m.head.weight.copy_(torch.from_numpy(hw))
+        m.head.bias.copy_(torch.from_numpy(hb))
+    return m.to(cuda)
+
+
+def test_ast_param_count_and_names(cuda, golden):
+    m = _ast(cuda, "f32")
+    assert sum(p.numel() for p in m.parameters()) == int(golden["ast_nparams"])
+    assert "transformer.11.mlp.fc2.weight" in m.state_dict()
+    pe = m.pos_embed.detach().double().cpu()
+    np.testing.assert_allclose([float(pe.sum()), float((pe ** 2).sum())], golden["ast_pos_embed_cs"], rtol=1e-5)
+
+
+def test_ast_forward_f32_vs_golden(cuda, golden):
+    m = _ast(cuda, "f32").eval()
+    x = torch.from_numpy(hash_uniform(31, (2, 128, 1379))).to(cuda)
+    with torch.no_grad():
+        p = m(x).cpu().numpy()
+    ref = golden["ast_probs"]
+    assert np.abs(p - ref).max() / np.abs(ref).max() < 1e-3
+    assert np.array_equal(p.argmax(1), ref.argmax(1))
+
+
+def test_ast_forward_bf16(cuda, golden):
+    m = _ast(cuda, "bf16").eval()
+    x = torch.from_numpy(hash_uniform(31, (2, 128, 1379))).to(cuda)
+    with torch.no_grad():
+        p = m(x).cpu().numpy()
+    ref = golden["ast_probs"]
+    assert np.abs(p - ref).max() / np.abs(ref).max() < 5e-2
+    assert np.array_equal(p.argmax(1), ref.argmax(1))
+
+
+def test_ast_backward_f32_vs_oracle(cuda):
+    """Two transformer blocks (depth override) so the CPU autograd reference stays fast."""
+    import os
+    os.environ["MIA_QUIET"] = "1"
+    from src.models.ast import ASTModel
+    torch.set_num_threads(16)
+    m = ASTModel(num_classes=10, compute_dtype="f32", depth=2)
+    st = oast.deit_hash_state(300, depth=2)
+    m.load_vit_state(st)
+    hw, hb = oast.head_hash(901, 10)
+    with torch.no_grad():
+        m.head.weight.copy_(torch.from_numpy(hw))
+        m.head.bias.copy_(torch.from_numpy(hb))
+    m = m.to(cuda)
+    x = hash_uniform(32, (2, 128, 1379))
+    y = torch.zeros(2, 10)
+    y[0, 3], y[1, 5], y[1, 2] = 1.0, 0.6, 0.4
+    p = m(torch.from_numpy(x).to(cuda))
+    loss = -torch.sum(y.to(cuda) * torch.log(torch.softmax(p, 1) + 1e-8), 1).mean()
+    loss.backward()
+    ref = oast.model_params(st, hw, hb, depth=2)
+    for v in ref.values():
+        v.requires_grad_(True)
+    pr = oast.forward(ref, torch.from_numpy(x), depth=2)
+    lr = -torch.sum(y * torch.log(torch.softmax(pr, 1) + 1e-8), 1).mean()
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-4
+    names = {"patch_embed.weight": "patch_embed.weight", "cls_token": "cls_token", "pos_embed": "pos_embed",
+             "transformer.0.attn.qkv.weight": "transformer.0.attn.qkv.weight",
+             "transformer.1.mlp.fc1.weight": "transformer.1.mlp.fc1.weight",
+             "transformer.1.norm2.weight": "transformer.1.norm2.weight", "head.weight": "head.weight"}
+    sd = dict(m.named_parameters())
+    for mine, theirs in names.items():
+        got, want = sd[mine].grad.cpu().double(), ref[theirs].grad.double()
+        l2 = float((got - want).norm() / want.norm().clamp_min(1e-30))
+        assert l2 < 1e-3, (mine, l2)
