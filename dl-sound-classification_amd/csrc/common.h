@@ -68,6 +68,23 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Deterministic block-wide sum (blockDim.x == 256) of p[k * stride] over k < n, in double.
+// Fixed per-thread strided order + fixed tree: bit-identical across runs.
+__device__ __forceinline__ double block_sum_strided(const float* __restrict__ p, int n, int64_t stride) {
+  __shared__ double red_bss[256];
+  double s = 0.0;
+  for (int k = threadIdx.x; k < n; k += 256) s += (double)p[(int64_t)k * stride];
+  red_bss[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red_bss[threadIdx.x] += red_bss[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double r = red_bss[0];
+  __syncthreads();
+  return r;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -417,6 +417,54 @@ __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n,
   st_elem(e.ptr, e.dtype, idx, v);
 }
 
+// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no row map / aux / accumulate,
+// act none|relu, 16-B aligned destination): bias as float4, 16-B stores.  Otherwise per element.
+__device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t n0, int64_t N, const float* v) {
+  const int64_t idx = m * e.ldc + n0;
+  const bool fast = n0 + 16 <= N && !e.rm_inner && !e.accumulate &&
+                    (e.act == MIA_ACT_NONE || e.act == MIA_ACT_RELU) &&
+                    ((idx * (e.dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(e.ptr)) & 15) == 0;
+  if (!fast) {
+    for (int c = 0; c < 16; ++c)
+      if (n0 + c < N) epi_store(e, m, n0 + c, v[c]);
+    return;
+  }
+  float o[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) o[c] = v[c] * e.alpha;
+  if (e.bias) {
+    const float4* b4 = reinterpret_cast<const float4*>(e.bias + n0);
+    const bool ba = ((reinterpret_cast<uintptr_t>(e.bias + n0)) & 15) == 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 bb;
+      if (ba) bb = b4[q];
+      else bb = make_float4(e.bias[n0 + 4 * q], e.bias[n0 + 4 * q + 1], e.bias[n0 + 4 * q + 2], e.bias[n0 + 4 * q + 3]);
+      o[4 * q] += bb.x; o[4 * q + 1] += bb.y; o[4 * q + 2] += bb.z; o[4 * q + 3] += bb.w;
+    }
+  }
+  if (e.act == MIA_ACT_RELU) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) o[c] = fmaxf(o[c], 0.f);
+  }
+  if (e.dtype == MIA_BF16) {
+    uint32_t w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16 lo = (bf16)o[2 * c], hi = (bf16)o[2 * c + 1];
+      w[c] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(e.ptr) + idx);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(e.ptr) + idx);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+}
+
 template <typename T, int BM, int BN, int WM, int LA, int LB>
 __global__ __launch_bounds__(NT) void igemm_kernel(GemmArgs g) {
   constexpr int WN = 4 / WM;
@@ -512,9 +560,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(GemmArgs g) {
           float* dst = g.ws + ((int64_t)z * g.M + m) * g.N;
           for (int c = 0; c < 16; ++c)
             if (nb + c < g.N) dst[nb + c] = stage[row * 33 + c0 + c];
-        } else {
-          for (int c = 0; c < 16; ++c)
-            if (nb + c < g.N) epi_store(g.e, m, nb + c, stage[row * 33 + c0 + c]);
+        } else if (nb < g.N) {
+          float v[16];
+#pragma unroll
+          for (int c = 0; c < 16; ++c) v[c] = stage[row * 33 + c0 + c];
+          epi_store16(g.e, m, nb, g.N, v);
         }
       }
       __syncthreads();
@@ -529,6 +579,528 @@ __global__ void splitk_reduce_kernel(const float* ws, int split, int64_t M, int6
     for (int z = 0; z < split; ++z) s += ws[z * total + idx];
     epi_store(e, idx / N, idx % N, s);
   }
+}
+
+// -------------------------------------------------------------------------- row-window conv
+// Direct convolution for the EnvNet-v2 trunk/frontend shapes (stride (1, S), C in {32, 64},
+// N = Cout in {32, 64}): a block owns BM consecutive output pixels of ONE output row and, per
+// kernel row ky, stages the input row segment they read — (BM-1)*S + KW pixels x C channels —
+// once in LDS (BN affine + ReLU of the producer applied while staging, zero padding after it).
+// Every im2col element (KW*C per output pixel) is then a ds_read_b128 of that window: the 8-tap
+// x C reuse that a gathered im2col tile re-fetches from L2 stays on chip.  S = 2 windows are
+// stored de-interleaved (even | odd pixels) so a fragment read is unit-stride in either case.
+// The weight tile (N x 128 of the packed [N][KH][KW][C] matrix) is double-buffered; the window
+// is single-buffered and swapped only when ky advances.  MFMA 32x32x16 bf16, 4 waves, each
+// owning BM/4 output pixels x all N channels.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct RowArgs {
+  const char* x;
+  int xdt, pre;
+  int n, h, w, oh, ow, kh, kw, ph, pw;
+  const float* ps;
+  const float* pt;
+  const bf16* wt;
+  int64_t ldw, N, M;
+  EpiDev e;
+};
+
+template <int BM, int NB, int S, int C, int KWMAX>
+struct RowCfg {
+  static constexpr int CG = C / 8;                       // 16-B chunks per pixel
+  static constexpr int WPX = (BM - 1) * S + KWMAX;       // window pixels
+  static constexpr int HALF = (WPX + 1) / 2;
+  static constexpr int NSLOT = S == 1 ? WPX : 2 * HALF;
+  static constexpr int PSB = C * 2 + 16;                 // LDS bytes per pixel (conflict-free b128 reads)
+  static constexpr int WBYTES = NSLOT * PSB;
+  static constexpr int RSB = 128 * 2 + 16;               // weight tile row stride
+  static constexpr int BBYTES = NB * RSB;
+  static constexpr int WCH = (WPX * CG + NT - 1) / NT;   // window chunks per thread
+  static constexpr int BCH = NB * 16 / NT;               // weight chunks per thread
+  static constexpr int LDS = WBYTES + 2 * BBYTES;
+};
+
+template <int S, int HALF>
+__device__ __forceinline__ int win_slot(int p) {
+  if constexpr (S == 1) return p;
+  else return (p & 1) * HALF + (p >> 1);
+}
+
+template <typename TS, int BM, int NB, int S, int C, int KWMAX, bool PRE>
+__global__ __launch_bounds__(NT) void rowconv_kernel(RowArgs g) {
+  using Cfg = RowCfg<BM, NB, S, C, KWMAX>;
+  constexpr int TM = BM / 128, TN = NB / 32;
+  __shared__ __attribute__((aligned(16))) char smem[Cfg::LDS > 4 * 32 * 33 * 4 ? Cfg::LDS : 4 * 32 * 33 * 4];
+  char* win = smem;
+  char* bbuf = smem + Cfg::WBYTES;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int x0 = blockIdx.x * BM, oy = blockIdx.y, b = blockIdx.z;
+  const int KT = g.kw * C / 128;            // k-tiles per kernel row
+  const int nk = g.kh * KT;
+  const int px0 = x0 * S - g.pw;            // input column of window pixel 0
+  const int cg = t % Cfg::CG;               // this thread's channel chunk (constant: CG | NT)
+
+  float sc[8], sh[8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = g.ps[cg * 8 + i]; sh[i] = g.pt[cg * 8 + i]; }
+  }
+
+  u32x4 wreg[Cfg::WCH];
+  u32x4 breg[Cfg::BCH];
+
+  auto load_window = [&](int ky) __attribute__((always_inline)) {
+    const int iy = oy + ky - g.ph;
+    const bool rowok = iy >= 0 && iy < g.h;
+    const TS* xs = reinterpret_cast<const TS*>(g.x);
+#pragma unroll
+    for (int s = 0; s < Cfg::WCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / Cfg::CG;
+      const int ix = px0 + p;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (p < Cfg::WPX && rowok && ix >= 0 && ix < g.w) {
+        const int64_t off = ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8;
+        float f[8];
+        if constexpr (sizeof(TS) == 2) {
+          const u32x4 u = *reinterpret_cast<const u32x4*>(xs + off);
+          if constexpr (!PRE) {
+            v = u;
+          } else {
+            const uint32_t w4[4] = {u[0], u[1], u[2], u[3]};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              f[2 * i] = __uint_as_float(w4[i] << 16);
+              f[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+            }
+          }
+        } else {
+          const float4 a = reinterpret_cast<const float4*>(xs + off)[0];
+          const float4 c = reinterpret_cast<const float4*>(xs + off)[1];
+          f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
+        }
+        if constexpr (PRE || sizeof(TS) == 4) {
+          if constexpr (PRE) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              f[i] = fmaf(f[i], sc[i], sh[i]);
+              if (g.pre == MIA_PRE_AFFINE_RELU) f[i] = fmaxf(f[i], 0.f);
+            }
+          }
+          uint32_t w4[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
+                    ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          }
+          v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        }
+      }
+      wreg[s] = v;
+    }
+  };
+  auto store_window = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < Cfg::WCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / Cfg::CG;
+      if (p < Cfg::WPX)
+        *reinterpret_cast<u32x4*>(win + win_slot<S, Cfg::HALF>(p) * Cfg::PSB + cg * 16) = wreg[s];
+    }
+  };
+  auto load_b = [&](int kt) __attribute__((always_inline)) {
+    const int64_t k0 = (int64_t)kt * 128;
+#pragma unroll
+    for (int s = 0; s < Cfg::BCH; ++s) {
+      const int q = t + NT * s;
+      const int row = q >> 4, kc = q & 15;
+      breg[s] = *reinterpret_cast<const u32x4*>(g.wt + row * g.ldw + k0 + kc * 8);
+    }
+  };
+  auto store_b = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < Cfg::BCH; ++s) {
+      const int q = t + NT * s;
+      const int row = q >> 4, kc = q & 15;
+      *reinterpret_cast<u32x4*>(bbuf + buf * Cfg::BBYTES + row * Cfg::RSB + kc * 16) = breg[s];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_window(0);
+  load_b(0);
+  store_window();
+  store_b(0);
+  __syncthreads();
+
+  const int g2 = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    const bool newwin = more && ((kt + 1) % KT == 0);
+    if (more) load_b(kt + 1);
+    if (newwin) load_window((kt + 1) / KT);
+    const char* bs = bbuf + (kt & 1) * Cfg::BBYTES;
+    const int kk0 = (kt % KT) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int kk = kk0 + ks * 16 + 8 * g2;
+      const int kx = kk / C, ci = kk % C;
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wave * (BM / 4) + i * 32 + (lane & 31);
+        int slot;
+        if constexpr (S == 1) slot = r + kx;
+        else slot = (kx & 1) * Cfg::HALF + r + (kx >> 1);
+        fa[i] = *reinterpret_cast<const bf16x8*>(win + slot * Cfg::PSB + ci * 2);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(bs + (j * 32 + (lane & 31)) * Cfg::RSB + (ks * 16 + 8 * g2) * 2);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store_b((kt + 1) & 1);
+    if (newwin) {
+      __syncthreads();
+      store_window();
+    }
+    __syncthreads();
+  }
+
+  // epilogue through LDS, 16 contiguous output channels per lane
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
+  const int64_t mrow0 = ((int64_t)b * g.oh + oy) * g.ow;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = acc[i][j][r];
+      __syncthreads();
+      const int row = lane >> 1, c0 = (lane & 1) * 16;
+      const int ox = x0 + wave * (BM / 4) + i * 32 + row;
+      if (ox < g.ow) {
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = stage[row * 33 + c0 + c];
+        epi_store16(g.e, mrow0 + ox, j * 32 + c0, g.N, v);
+      }
+      __syncthreads();
+    }
+}
+
+// -------------------------------------------------------------------------- row-window wgrad
+// dW[n][ky][kx][ci] = sum_{b,oy,ox} dY[b,oy,ox,n] * X'[b, oy+ky-ph, ox*S+kx-pw, ci]  (X' = pre-op(X))
+// for the same conv shapes.  Block (ky, z) walks output-row chunks of BP pixels (chunk ids
+// z, z+Z, ...): it stages the dY chunk [BP px][NOUT] and the input window it touches
+// [(BP-1)*S+KW px][C] in LDS, and both MFMA operands are ds_read_b64_tr_b16 transposed reads
+// (dY^T rows = output channels; im2col rows = (kx, ci) columns of the window, pixel-strided).
+// Accumulators stay in registers across all chunks; each block writes one f32 partial slab
+// ws[z][NOUT][KH*KW*C] (its ky columns) and splitk_reduce sums the Z slabs + applies the epilogue.
+struct RowWArgs {
+  const char* x;
+  const char* dy;
+  int pre;
+  int n, h, w, oh, ow, kh, kw, ph, pw;
+  const float* ps;
+  const float* pt;
+  int Z;
+  int64_t Ntot;
+  float* ws;
+};
+
+template <typename T, int NOUT, int S, int C, int KWMAX, bool PRE>
+__global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
+  constexpr int BP = 128;
+  constexpr int CG = C / 8;
+  constexpr int WPX = (BP - 1) * S + KWMAX;
+  constexpr int HALF = (WPX + 1) / 2;
+  constexpr int NSLOT = S == 1 ? WPX : 2 * HALF;
+  constexpr int PSB = C == 32 ? 64 : 192;          // 16 / 48 dwords: conflict-free transposed reads
+  constexpr int DSB = NOUT == 32 ? 64 : 192;
+  constexpr int WBYTES = NSLOT * PSB;
+  constexpr int DBYTES = BP * DSB;
+  constexpr int WCH = (WPX * CG + NT - 1) / NT;
+  constexpr int DCH = BP * NOUT / 8 / NT;           // 2 or 4
+  constexpr int MT = NOUT / 32;
+  constexpr int TPW = MT * (KWMAX * C / 32) / 4;    // accumulator tiles per wave (upper bound)
+  constexpr int ES = sizeof(T);
+  __shared__ __attribute__((aligned(16))) char smem[WBYTES + DBYTES];
+  char* win = smem;
+  char* dyt = smem + WBYTES;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ky = blockIdx.x, z = blockIdx.y;
+  const int NC = g.kw * C;                 // columns of this ky
+  const int NCT = NC / 32;
+  const int ntiles = MT * NCT;
+  const int CPR = (g.ow + BP - 1) / BP;
+  const int64_t nchunks = (int64_t)g.n * g.oh * CPR;
+  const int cg = t % CG;
+
+  float sc[8], sh[8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = g.ps[cg * 8 + i]; sh[i] = g.pt[cg * 8 + i]; }
+  }
+
+  u32x4 wreg[WCH];
+  u32x4 dreg[DCH];
+
+  auto pack8 = [&](const float* f) __attribute__((always_inline)) {
+    uint32_t w4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+      w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    return u32x4{w4[0], w4[1], w4[2], w4[3]};
+  };
+  auto load8f = [&](const T* p, float* f) __attribute__((always_inline)) {
+    if constexpr (ES == 2) {
+      const u32x4 u = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(u[i] << 16); f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u); }
+    } else {
+      const float4 a = reinterpret_cast<const float4*>(p)[0];
+      const float4 c = reinterpret_cast<const float4*>(p)[1];
+      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
+    }
+  };
+  auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
+    const int64_t row = c / CPR;
+    const int x0 = (int)(c - row * CPR) * BP;
+    const int b = (int)(row / g.oh), oy = (int)(row - (int64_t)b * g.oh);
+    const T* dys = reinterpret_cast<const T*>(g.dy) + ((int64_t)row * g.ow + x0) * NOUT;
+#pragma unroll
+    for (int s = 0; s < DCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / (NOUT / 8), cc = q % (NOUT / 8);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (x0 + p < g.ow) {
+        if constexpr (ES == 2) {
+          v = *reinterpret_cast<const u32x4*>(dys + p * NOUT + cc * 8);
+        } else {
+          float f[8];
+          load8f(dys + p * NOUT + cc * 8, f);
+          v = pack8(f);
+        }
+      }
+      dreg[s] = v;
+    }
+    const int iy = oy + ky - g.ph;
+    const bool rowok = iy >= 0 && iy < g.h;
+    const int px0 = x0 * S - g.pw;
+    const T* xs = reinterpret_cast<const T*>(g.x);
+#pragma unroll
+    for (int s = 0; s < WCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / CG;
+      const int ix = px0 + p;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (p < WPX && rowok && ix >= 0 && ix < g.w) {
+        const T* src = xs + ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8;
+        if constexpr (ES == 2 && !PRE) {
+          v = *reinterpret_cast<const u32x4*>(src);
+        } else {
+          float f[8];
+          load8f(src, f);
+          if constexpr (PRE) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              f[i] = fmaf(f[i], sc[i], sh[i]);
+              if (g.pre == MIA_PRE_AFFINE_RELU) f[i] = fmaxf(f[i], 0.f);
+            }
+          }
+          v = pack8(f);
+        }
+      }
+      wreg[s] = v;
+    }
+  };
+  auto store_chunk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < DCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / (NOUT / 8), cc = q % (NOUT / 8);
+      *reinterpret_cast<u32x4*>(dyt + p * DSB + cc * 16) = dreg[s];
+    }
+#pragma unroll
+    for (int s = 0; s < WCH; ++s) {
+      const int q = t + NT * s;
+      const int p = q / CG;
+      if (p < WPX) *reinterpret_cast<u32x4*>(win + win_slot<S, HALF>(p) * PSB + cg * 16) = wreg[s];
+    }
+  };
+
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int q = 0; q < TPW; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+
+  const int i16 = lane & 15, gq = lane >> 4;
+  int64_t c = z;
+  if (c < nchunks) {
+    load_chunk(c);
+    store_chunk();
+  }
+  __syncthreads();
+  for (; c < nchunks; c += g.Z) {
+    const int64_t cn = c + g.Z;
+    const bool more = cn < nchunks;
+    if (more) load_chunk(cn);
+#pragma unroll
+    for (int ks = 0; ks < BP / 16; ++ks) {
+      const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
+      bf16x8 fa[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int col = mt * 32 + 16 * (gq & 1) + 4 * (i16 & 3);
+        const char* p0 = dyt + kr * DSB + col * 2;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * DSB));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[mt] = __builtin_bit_cast(bf16x8, cc);
+      }
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        const int tile = wave + 4 * q;
+        if (tile < ntiles) {
+          const int mt = tile / NCT, nt = tile - mt * NCT;
+          const int col = nt * 32 + 16 * (gq & 1);
+          const int kx = col / C, ci = col % C + 4 * (i16 & 3);
+          int slot;
+          if constexpr (S == 1) slot = kr + kx;
+          else slot = (kx & 1) * HALF + kr + (kx >> 1);
+          const char* p0 = win + slot * PSB + ci * 2;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * PSB));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 fb = __builtin_bit_cast(bf16x8, cc);
+          bf16x8 a = fa[0];
+          if constexpr (MT > 1) if (mt == 1) a = fa[1];
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, fb, acc[q], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_chunk();
+      __syncthreads();
+    }
+  }
+
+  // partial slab: ws[z][m][ky*NC + n]
+  float* dst = g.ws + (int64_t)z * NOUT * g.Ntot + (int64_t)ky * NC;
+#pragma unroll
+  for (int q = 0; q < TPW; ++q) {
+    const int tile = wave + 4 * q;
+    if (tile < ntiles) {
+      const int mt = tile / NCT, nt = tile - mt * NCT;
+      const int n = nt * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        dst[(int64_t)m * g.Ntot + n] = acc[q][r];
+      }
+    }
+  }
+}
+
+bool rowwgrad_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
+  if (compute != MIA_BF16 || split < 2) return false;
+  if (A.kind != MIA_OP_DENSE || A.layout != MIA_LAYOUT_RC || A.pre != MIA_PRE_NONE) return false;
+  if (B.kind != MIA_OP_CONV || B.layout != MIA_LAYOUT_RC || B.sh != 1 || (B.sw != 1 && B.sw != 2)) return false;
+  if (A.dtype != B.dtype || (A.dtype != MIA_BF16 && A.dtype != MIA_F32)) return false;
+  if (M != 32 && M != 64) return false;
+  if (A.rows != K || A.cols != M || A.ld != M) return false;
+  if (B.c != 32 && B.c != 64) return false;
+  if (B.c == 64 && B.sw != 1) return false;
+  if (B.kw > (B.sw == 1 ? 8 : 16) || (B.kw * B.c) % 128 != 0) return false;
+  if (B.pre != MIA_PRE_NONE && B.pre != MIA_PRE_AFFINE && B.pre != MIA_PRE_AFFINE_RELU) return false;
+  if (N != (int64_t)B.kh * B.kw * B.c || K != (int64_t)B.n * B.oh * B.ow) return false;
+  if (B.kh > 65535 || split > 65535) return false;
+  if ((reinterpret_cast<uintptr_t>(A.ptr) | reinterpret_cast<uintptr_t>(B.ptr)) & 15) return false;
+  return true;
+}
+
+template <typename T, int NOUT, int S, int C, int KWMAX>
+hipError_t rowwgrad_launch2(const RowWArgs& r, bool pre, hipStream_t s) {
+  dim3 grid((unsigned)r.kh, (unsigned)r.Z);
+  if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, true><<<grid, NT, 0, s>>>(r);
+  else rowwgrad_kernel<T, NOUT, S, C, KWMAX, false><<<grid, NT, 0, s>>>(r);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t rowwgrad_launch1(const RowWArgs& r, int NOUT, int S, int C, bool pre, hipStream_t s) {
+  if (S == 2) {
+    if (NOUT == 64) return rowwgrad_launch2<T, 64, 2, 32, 16>(r, pre, s);
+    return rowwgrad_launch2<T, 32, 2, 32, 16>(r, pre, s);
+  }
+  if (C == 64) {
+    if (NOUT == 64) return rowwgrad_launch2<T, 64, 1, 64, 8>(r, pre, s);
+    return rowwgrad_launch2<T, 32, 1, 64, 8>(r, pre, s);
+  }
+  if (NOUT == 64) return rowwgrad_launch2<T, 64, 1, 32, 8>(r, pre, s);
+  return rowwgrad_launch2<T, 32, 1, 32, 8>(r, pre, s);
+}
+
+// Row-window conv applies when: bf16 compute, no split, A = CONV/KC with stride (1, 1|2),
+// C in {32, 64}, KW*C a multiple of 128, B = the packed [N][KH*KW*C] bf16 weights, N in {32, 64}.
+bool rowconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
+  if (compute != MIA_BF16 || split > 1) return false;
+  if (A.kind != MIA_OP_CONV || A.layout != MIA_LAYOUT_KC || A.sh != 1 || (A.sw != 1 && A.sw != 2)) return false;
+  if (A.c != 32 && A.c != 64) return false;
+  if ((A.kw * A.c) % 128 != 0 || A.kw > (A.sw == 1 ? 8 : 16)) return false;
+  if (A.pre != MIA_PRE_NONE && A.pre != MIA_PRE_AFFINE && A.pre != MIA_PRE_AFFINE_RELU) return false;
+  if (A.dtype != MIA_BF16 && A.dtype != MIA_F32) return false;
+  if (B.kind != MIA_OP_DENSE || B.layout != MIA_LAYOUT_KC || B.dtype != MIA_BF16) return false;
+  if (B.rows != N || B.cols != K || B.ld % 8 != 0 || (reinterpret_cast<uintptr_t>(B.ptr) & 15)) return false;
+  if (N != 32 && N != 64) return false;
+  if (K != (int64_t)A.kh * A.kw * A.c || M != (int64_t)A.n * A.oh * A.ow) return false;
+  if (A.c == 64 && A.sw != 1) return false;
+  if ((reinterpret_cast<uintptr_t>(A.ptr) & 15)) return false;
+  return true;
+}
+
+template <typename TS, int BM, int NB, int S, int C, int KWMAX>
+hipError_t rowconv_launch2(const RowArgs& r, bool pre, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(r.ow, BM), (unsigned)r.oh, (unsigned)r.n);
+  if (pre) rowconv_kernel<TS, BM, NB, S, C, KWMAX, true><<<grid, NT, 0, s>>>(r);
+  else rowconv_kernel<TS, BM, NB, S, C, KWMAX, false><<<grid, NT, 0, s>>>(r);
+  return hipGetLastError();
+}
+
+template <typename TS>
+hipError_t rowconv_launch1(const RowArgs& r, int S, int C, bool pre, hipStream_t s) {
+  if (S == 2) {
+    if (r.N == 64) return rowconv_launch2<TS, 128, 64, 2, 32, 16>(r, pre, s);
+    return rowconv_launch2<TS, 128, 32, 2, 32, 16>(r, pre, s);
+  }
+  if (C == 64) {
+    if (r.N == 64) return rowconv_launch2<TS, 128, 64, 1, 64, 8>(r, pre, s);
+    return rowconv_launch2<TS, 256, 32, 1, 64, 8>(r, pre, s);
+  }
+  if (r.N == 64) return rowconv_launch2<TS, 128, 64, 1, 32, 8>(r, pre, s);
+  return rowconv_launch2<TS, 256, 32, 1, 32, 8>(r, pre, s);
 }
 
 OpDev to_dev(const MiaOperand& o) {
@@ -625,6 +1197,40 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   if (split_k < 1) split_k = 1;
   if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");
   if (M == 0 || N == 0) return 0;
+  if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
+    RowArgs r;
+    r.x = reinterpret_cast<const char*>(A->ptr);
+    r.xdt = A->dtype; r.pre = A->pre;
+    r.n = A->n; r.h = A->h; r.w = A->w; r.oh = A->oh; r.ow = A->ow; r.kh = A->kh; r.kw = A->kw;
+    r.ph = A->ph; r.pw = A->pw; r.ps = A->pre_scale; r.pt = A->pre_shift;
+    r.wt = reinterpret_cast<const bf16*>(B->ptr); r.ldw = B->ld; r.N = N; r.M = M;
+    r.e = to_dev(*E);
+    const bool pre = A->pre != MIA_PRE_NONE;
+    hipStream_t s = as_stream(stream);
+    hipError_t err = A->dtype == MIA_BF16 ? rowconv_launch1<bf16>(r, A->sw, A->c, pre, s)
+                                          : rowconv_launch1<float>(r, A->sw, A->c, pre, s);
+    if (err != hipSuccess) return mia::fail(-(int)err, "rowconv launch: %s", hipGetErrorString(err));
+    return 0;
+  }
+  if (workspace && rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
+    RowWArgs r;
+    r.x = reinterpret_cast<const char*>(B->ptr);
+    r.dy = reinterpret_cast<const char*>(A->ptr);
+    r.pre = B->pre;
+    r.n = B->n; r.h = B->h; r.w = B->w; r.oh = B->oh; r.ow = B->ow; r.kh = B->kh; r.kw = B->kw;
+    r.ph = B->ph; r.pw = B->pw; r.ps = B->pre_scale; r.pt = B->pre_shift;
+    r.Z = split_k; r.Ntot = N; r.ws = reinterpret_cast<float*>(workspace);
+    const bool pre = B->pre != MIA_PRE_NONE;
+    hipStream_t s = as_stream(stream);
+    hipError_t err = A->dtype == MIA_BF16 ? rowwgrad_launch1<bf16>(r, (int)M, B->sw, B->c, pre, s)
+                                          : rowwgrad_launch1<float>(r, (int)M, B->sw, B->c, pre, s);
+    if (err != hipSuccess) return mia::fail(-(int)err, "rowwgrad launch: %s", hipGetErrorString(err));
+    const int64_t total = M * N;
+    int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(r.ws, split_k, M, N, to_dev(*E));
+    MIA_LAUNCH_CHECK("splitk_reduce");
+    return 0;
+  }
   GemmArgs g;
   g.a = to_dev(*A);
   g.b = to_dev(*B);
@@ -643,6 +1249,14 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g.ws, split_k, M, N, g.e);
     MIA_LAUNCH_CHECK("splitk_reduce");
   }
+  return 0;
+}
+
+extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
+                             int32_t compute_dtype, int32_t split_k) {
+  if (!A || !B) return -1;
+  if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
+  if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;
   return 0;
 }
 

@@ -109,20 +109,33 @@ __global__ __launch_bounds__(NT) void soft_ce_kernel(const float* __restrict__ l
 }
 
 // ------------------------------------------------------------------ clip + Adam
-constexpr int ADAM_PARTS = 512;
+constexpr int ADAM_PARTS = 4096;
 
+// Squared L2 norm partials of every gradient tensor: 16-B loads (tensor storage is 16-B aligned
+// torch allocations; a misaligned one takes the scalar path), f32 accumulation flushed to double.
 __global__ __launch_bounds__(NT) void sqnorm_kernel(void* const* __restrict__ grads, const int64_t* __restrict__ sizes,
                                                     float* __restrict__ ws) {
   const int tsr = blockIdx.y;
   const float* g = reinterpret_cast<const float*>(grads[tsr]);
   const int64_t n = sizes[tsr];
+  const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nthr = (int64_t)gridDim.x * NT;
   double s = 0.0;
   float fs = 0.f;
   int cnt = 0;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const float v = g[i];
-    fs = fmaf(v, v, fs);
-    if (++cnt == 256) { s += fs; fs = 0.f; cnt = 0; }
+  if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    const int64_t n4 = n >> 2;
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int64_t i = tid; i < n4; i += nthr) {
+      const float4 v = g4[i];
+      fs = fmaf(v.x, v.x, fs); fs = fmaf(v.y, v.y, fs); fs = fmaf(v.z, v.z, fs); fs = fmaf(v.w, v.w, fs);
+      if (++cnt == 64) { s += fs; fs = 0.f; cnt = 0; }
+    }
+    for (int64_t i = (n4 << 2) + tid; i < n; i += nthr) fs = fmaf(g[i], g[i], fs);
+  } else {
+    for (int64_t i = tid; i < n; i += nthr) {
+      fs = fmaf(g[i], g[i], fs);
+      if (++cnt == 256) { s += fs; fs = 0.f; cnt = 0; }
+    }
   }
   s += fs;
   s = wave_sum_d(s);
@@ -137,7 +150,7 @@ __global__ __launch_bounds__(NT) void sqnorm_kernel(void* const* __restrict__ gr
 __global__ __launch_bounds__(NT) void norm_final_kernel(double* ws, int ntensors, int nparts, float clip, float* total_out,
                                                         float* coef_out) {
   double s = 0.0;
-  for (int i = threadIdx.x; i < ntensors * nparts; i += NT) {
+  for (int i = threadIdx.x; i < ntensors * nparts; i += NT) {  // fixed order: deterministic
     const int tsr = i / nparts, p = i % nparts;
     s += ws[(int64_t)tsr * ADAM_PARTS + p];
   }
@@ -170,16 +183,37 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
   float* v = reinterpret_cast<float*>(m2[tsr]);
   const int64_t n = sizes[tsr];
   const float coef = coef_p[0];
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const float pv = p[i];
-    float gv = g[i] * coef;
-    gv = fmaf(wd, pv, gv);
-    float mv = m[i];
+  auto upd = [&](float pv, float gv, float& mv, float& vv) {
+    gv = fmaf(wd, pv, gv * coef);
     mv = mv + (1.f - beta1) * (gv - mv);           // exp_avg.lerp_(grad, 1 - beta1)
-    float vv = v[i] * beta2;
-    vv = fmaf((1.f - beta2) * gv, gv, vv);          // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
+    vv = fmaf((1.f - beta2) * gv, gv, vv * beta2);  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
     const float denom = sqrtf(vv) / bc2_sqrt + eps;
-    p[i] = pv - lr_over_bc1 * (mv / denom);
+    return pv - lr_over_bc1 * (mv / denom);
+  };
+  const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nthr = (int64_t)gridDim.x * NT;
+  const bool al = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                    reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  int64_t done = 0;
+  if (al) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = tid; i < n4; i += nthr) {
+      float4 pv = reinterpret_cast<float4*>(p)[i];
+      const float4 gv = reinterpret_cast<const float4*>(g)[i];
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      float4 vv = reinterpret_cast<float4*>(v)[i];
+      pv.x = upd(pv.x, gv.x, mv.x, vv.x);
+      pv.y = upd(pv.y, gv.y, mv.y, vv.y);
+      pv.z = upd(pv.z, gv.z, mv.z, vv.z);
+      pv.w = upd(pv.w, gv.w, mv.w, vv.w);
+      reinterpret_cast<float4*>(p)[i] = pv;
+      reinterpret_cast<float4*>(m)[i] = mv;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    done = n4 << 2;
+  }
+  for (int64_t i = done + tid; i < n; i += nthr) {
+    float mv = m[i], vv = v[i];
+    p[i] = upd(p[i], g[i], mv, vv);
     m[i] = mv;
     v[i] = vv;
   }
@@ -239,21 +273,35 @@ __global__ void tokens_bwd_kernel(const float* __restrict__ dout, float* __restr
 
 // ------------------------------------------------------------------ BC mixing
 // mean square of row idx[blockIdx.x] (or blockIdx.x) of x
-__global__ __launch_bounds__(NT) void clip_ms_kernel(const float* __restrict__ x, int64_t T, const int* __restrict__ idx,
-                                                     float* __restrict__ ms) {
+constexpr int MS_NT = 1024;
+__global__ __launch_bounds__(MS_NT) void clip_ms_kernel(const float* __restrict__ x, int64_t T, const int* __restrict__ idx,
+                                                        float* __restrict__ ms) {
   int row = blockIdx.x;
   if (idx) {
     row = idx[blockIdx.x];
     if (row < 0) { if (threadIdx.x == 0) ms[blockIdx.x] = 0.f; return; }
   }
   const float* r = x + (int64_t)row * T;
-  double s = 0.0;
-  for (int64_t i = threadIdx.x; i < T; i += NT) s += (double)r[i] * r[i];
-  s = wave_sum_d(s);
-  __shared__ double red[4];
+  float fs = 0.f;
+  if ((reinterpret_cast<uintptr_t>(r) & 15) == 0) {
+    const int64_t n4 = T >> 2;
+    for (int64_t i = threadIdx.x; i < n4; i += MS_NT) {
+      const float4 v = reinterpret_cast<const float4*>(r)[i];
+      fs = fmaf(v.x, v.x, fs); fs = fmaf(v.y, v.y, fs); fs = fmaf(v.z, v.z, fs); fs = fmaf(v.w, v.w, fs);
+    }
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < T; i += MS_NT) fs = fmaf(r[i], r[i], fs);
+  } else {
+    for (int64_t i = threadIdx.x; i < T; i += MS_NT) fs = fmaf(r[i], r[i], fs);
+  }
+  double s = wave_sum_d((double)fs);
+  __shared__ double red[MS_NT / 64];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) ms[blockIdx.x] = (float)((red[0] + red[1] + red[2] + red[3]) / (double)T);
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < MS_NT / 64; ++w) t += red[w];
+    ms[blockIdx.x] = (float)(t / (double)T);
+  }
 }
 
 __device__ __forceinline__ float spl_db(float ms) {  // BCMixingUtils.a_weighted_spl (preprocessing.py:395-415)
@@ -366,14 +414,14 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   hipStream_t s = as_stream(stream);
   double* ws = reinterpret_cast<double*>(sqnorm_ws);
   float* coef = reinterpret_cast<float*>(ws + (int64_t)ntensors * ADAM_PARTS);
-  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 16)));
+  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 64)));
   sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, reinterpret_cast<float*>(ws));
   MIA_LAUNCH_CHECK("sqnorm");
   norm_final_kernel<<<1, NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);
   MIA_LAUNCH_CHECK("norm_final");
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  const int ablocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, cdiv(max_numel, 256 * 8)));
+  const int ablocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(max_numel, 256 * 16)));
   adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, sizes, coef,
                                                      (float)(lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
                                                      weight_decay);
@@ -430,9 +478,9 @@ extern "C" int mia_bc_mix(const float* x, const float* pool, int64_t T, int32_t 
   hipStream_t s = as_stream(stream);
   float* ms = reinterpret_cast<float*>(workspace);
   float* msq = ms + B;
-  clip_ms_kernel<<<B, NT, 0, s>>>(x, T, nullptr, ms);
+  clip_ms_kernel<<<B, MS_NT, 0, s>>>(x, T, nullptr, ms);
   MIA_LAUNCH_CHECK("clip_ms");
-  clip_ms_kernel<<<B, NT, 0, s>>>(pool, T, partner, msq);
+  clip_ms_kernel<<<B, MS_NT, 0, s>>>(pool, T, partner, msq);
   MIA_LAUNCH_CHECK("clip_ms(partner)");
   bc_coef_kernel<<<(unsigned)cdiv(B, 256), 256, 0, s>>>(ms, msq, partner, r, labels, pool_labels, B, num_classes,
                                                         p_out, yout);

@@ -57,13 +57,10 @@ __global__ void bn_finalize_kernel(const void* __restrict__ x, int dtype, const 
                                    int nblk, int64_t P, int C, const float* gamma, const float* beta,
                                    float* running_mean, float* running_var, float momentum, float eps,
                                    float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += partial[((int64_t)b * C + c) * 2];
-    s2 += partial[((int64_t)b * C + c) * 2 + 1];
-  }
+  const int c = blockIdx.x;  // one block per channel
+  const double s1 = block_sum_strided(partial + (int64_t)c * 2, nblk, (int64_t)C * 2);
+  const double s2 = block_sum_strided(partial + (int64_t)c * 2 + 1, nblk, (int64_t)C * 2);
+  if (threadIdx.x != 0) return;
   const double n = (double)P;
   const double K = ld_elem(x, dtype, c);
   const double dm = s1 / n;
@@ -131,13 +128,10 @@ __global__ __launch_bounds__(NT) void bn_relu_bwd_reduce_kernel(const void* __re
 // partial [nblk][C][2] -> out0[c] = sum q0, out1[c] = sum q1
 __global__ void channel_partial_sum_kernel(const float* __restrict__ partial, int nblk, int C,
                                            float* out_q1, float* out_q0) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0;
-  for (int k = 0; k < nblk; ++k) {
-    a += partial[((int64_t)k * C + c) * 2];
-    b += partial[((int64_t)k * C + c) * 2 + 1];
-  }
+  const int c = blockIdx.x;  // one block per channel
+  const double a = block_sum_strided(partial + (int64_t)c * 2, nblk, (int64_t)C * 2);
+  const double b = block_sum_strided(partial + (int64_t)c * 2 + 1, nblk, (int64_t)C * 2);
+  if (threadIdx.x != 0) return;
   if (out_q0) out_q0[c] = (float)a;
   if (out_q1) out_q1[c] = (float)b;
 }
@@ -189,11 +183,9 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const void* __restrict__ x, 
   partial[(int64_t)blockIdx.x * C + c] = s;
 }
 __global__ void colsum_final_kernel(const float* __restrict__ partial, int nblk, int C, float* out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0;
-  for (int k = 0; k < nblk; ++k) s += partial[(int64_t)k * C + c];
-  out[c] = (float)s;
+  const int c = blockIdx.x;  // one block per column
+  const double s = block_sum_strided(partial + c, nblk, C);
+  if (threadIdx.x == 0) out[c] = (float)s;
 }
 
 int nblocks_for(int64_t P, int C) {
@@ -304,10 +296,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy,
 }
 
 __global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, float* dgamma, float* dbeta) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  double a = 0, b = 0;
-  for (int k = 0; k < nblk; ++k) { a += partial[(int64_t)k * 2 * D + d]; b += partial[(int64_t)k * 2 * D + D + d]; }
+  const int d = blockIdx.x;  // one block per feature
+  const double a = block_sum_strided(partial + d, nblk, 2 * (int64_t)D);
+  const double b = block_sum_strided(partial + D + d, nblk, 2 * (int64_t)D);
+  if (threadIdx.x != 0) return;
   if (dgamma) dgamma[d] = (float)a;
   if (dbeta) dbeta[d] = (float)b;
 }
@@ -339,7 +331,7 @@ extern "C" int mia_bn_fwd_stats(const void* x, int32_t dtype, int64_t P, int32_t
   const int nb = nblocks_for(P, C);
   bn_stats_kernel<<<nb, NT, 0, s>>>(x, dtype, P, C, (float*)partial);
   MIA_LAUNCH_CHECK("bn_stats");
-  bn_finalize_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>(x, dtype, (const float*)partial, nb, P, C, gamma, beta,
+  bn_finalize_kernel<<<(unsigned)C, 256, 0, s>>>(x, dtype, (const float*)partial, nb, P, C, gamma, beta,
                                                             running_mean, running_var, momentum, eps, mean, invstd,
                                                             scale, shift);
   MIA_LAUNCH_CHECK("bn_finalize");
@@ -357,7 +349,7 @@ extern "C" int mia_bn_relu_bwd_reduce(const void* dact, void* dz, const void* x,
   const int nb = nblocks_for(P, C);
   bn_relu_bwd_reduce_kernel<<<nb, NT, 0, s>>>(dact, dz, x, dtype, P, C, scale, shift, mean, invstd, (float*)partial);
   MIA_LAUNCH_CHECK("bn_relu_bwd_reduce");
-  channel_partial_sum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, dgamma, dbeta);
+  channel_partial_sum_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, dgamma, dbeta);
   MIA_LAUNCH_CHECK("channel_partial_sum");
   return 0;
 }
@@ -374,7 +366,7 @@ extern "C" int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t
                                         dbias ? (float*)partial : nullptr);
   MIA_LAUNCH_CHECK("bn_bwd_apply");
   if (dbias) {
-    channel_partial_sum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, nullptr, dbias);
+    channel_partial_sum_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, nullptr, dbias);
     MIA_LAUNCH_CHECK("channel_partial_sum");
   }
   return 0;
@@ -387,7 +379,7 @@ extern "C" int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, in
   hipStream_t s = as_stream(stream);
   colsum_kernel<<<dim3(nb, (unsigned)cdiv(C, NT)), NT, 0, s>>>(x, dtype, P, C, ld, (float*)partial);
   MIA_LAUNCH_CHECK("colsum");
-  colsum_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, s>>>((const float*)partial, nb, C, out);
+  colsum_final_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, out);
   MIA_LAUNCH_CHECK("colsum_final");
   return 0;
 }
@@ -424,7 +416,7 @@ extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x,
     ln_bwd_kernel<16><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
                                         (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
   MIA_LAUNCH_CHECK("layernorm_bwd");
-  ln_partial_final_kernel<<<(unsigned)cdiv(D, 256), 256, 0, s>>>((const float*)partial, (int)nb, D, dgamma, dbeta);
+  ln_partial_final_kernel<<<(unsigned)D, 256, 0, s>>>((const float*)partial, (int)nb, D, dgamma, dbeta);
   MIA_LAUNCH_CHECK("layernorm_partial_final");
   return 0;
 }

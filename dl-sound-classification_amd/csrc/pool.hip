@@ -142,10 +142,10 @@ __global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ d
 }
 
 __global__ void partial_final_kernel(const float* __restrict__ partial, int nblk, int C, float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0;
-  for (int k = 0; k < nblk; ++k) { a += partial[((int64_t)k * C + c) * 2]; b += partial[((int64_t)k * C + c) * 2 + 1]; }
+  const int c = blockIdx.x;  // one block per channel
+  const double a = block_sum_strided(partial + (int64_t)c * 2, nblk, (int64_t)C * 2);
+  const double b = block_sum_strided(partial + (int64_t)c * 2 + 1, nblk, (int64_t)C * 2);
+  if (threadIdx.x != 0) return;
   dbeta[c] = (float)a;
   dgamma[c] = (float)b;
 }
@@ -198,7 +198,7 @@ extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout,
   pool_bwd_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean, invstd,
                                     dz, (float*)partial);
   MIA_LAUNCH_CHECK("pool_bwd");
-  partial_final_kernel<<<(unsigned)cdiv(c, 256), 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);
+  partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);
   MIA_LAUNCH_CHECK("pool_bwd_final");
   return 0;
 }

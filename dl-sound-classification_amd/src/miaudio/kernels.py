@@ -143,9 +143,12 @@ def _operand_bytes(o: L.MiaOperand, M_or_N: int, K: int) -> int:
 
 def gemm(A: L.MiaOperand, B: L.MiaOperand, E: L.MiaEpilogue, M: int, N: int, K: int, compute: int,
          split_k: int | None = None, device=None, tag: str | None = None):
-    if split_k is None:
-        split_k = auto_split(M, N, K)
     lib = L.load()
+    if split_k is None:
+        if compute == L.BF16 and lib.mia_gemm_path(A, B, M, N, K, compute, 2) == 2:
+            split_k = max(2, min(1024, 2048 // max(1, B.kh)))  # row-window wgrad: KH x split blocks
+        else:
+            split_k = auto_split(M, N, K)
     ws = None
     if split_k > 1:
         ws = workspace(lib.mia_gemm_workspace_bytes(M, N, split_k), device or torch.cuda.current_device(), "gemm")

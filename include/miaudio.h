@@ -83,6 +83,12 @@ int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k);
 int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
              int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
              mia_stream_t stream);
+/* Which kernel mia_gemm runs for these operands: 0 = implicit-GEMM tile kernel, 1 = row-window
+ * direct conv (bf16 compute, stride (1,1|2), C in {32,64}, N in {32,64}: the EnvNet-v2 8x8 trunk
+ * convs, the frontend conv2 and their dgrads), 2 = row-window weight gradient (A = dY as RC,
+ * B = the conv input as RC, M = Cout in {32,64}, split_k >= 2 partial slabs: blocks = KH x split). */
+int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
+                  int32_t compute_dtype, int32_t split_k);
 
 /* Fused log-mel: frame gather + 1024-pt real FFT (LDS) + |X|^2 + htk mel (sparse bands)
  * + 10log10 + per-clip top_db clamp + per-clip mean/unbiased-std normalisation.

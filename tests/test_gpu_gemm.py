@@ -183,3 +183,96 @@ def test_single_channel_dgrad_rowsplit(cuda, cd):
     K.col2im_rows(Pm, n, ha, W, kh, dx)
     torch.cuda.synchronize()
     assert rel(dx.cpu(), xr.grad[:, 0]) < TOL[cd] * 2
+
+
+@pytest.mark.parametrize("case", [
+    # n, cin, cout, h, w, kh, kw, sw, pre, src dtype
+    (2, 32, 32, 10, 600, 8, 8, 1, True, torch.bfloat16),    # conv4 shape: several 256-px tiles + tail
+    (2, 32, 32, 9, 300, 8, 8, 1, False, torch.float32),     # f32 storage, bf16 compute
+    (2, 32, 64, 1, 3001, 1, 16, 2, True, torch.bfloat16),   # conv2: stride 2, de-interleaved window
+    (2, 32, 32, 1, 1001, 1, 16, 2, False, torch.float32),   # stride 2, N = 32
+    (2, 64, 64, 3, 700, 1, 8, 1, False, torch.bfloat16),    # C = 64, N = 64
+    (2, 64, 32, 2, 555, 1, 8, 1, True, torch.bfloat16),     # C = 64, N = 32 (parity-dgrad shape)
+])
+def test_rowconv_path(cuda, case):
+    """The row-window direct conv (mia_gemm_path == 1) against a float64 conv2d."""
+    n, cin, cout, h, w, kh, kw, sw, pre, sdt = case
+    g = torch.Generator().manual_seed(h * w + cin)
+    x = torch.randn(n, h, w, cin, generator=g).to(torch.bfloat16).to(sdt)
+    wt = (torch.randn(cout, cin, kh, kw, generator=g) / (cin * kh * kw) ** 0.5).to(torch.bfloat16).float()
+    sc = torch.rand(cin, generator=g) + 0.5
+    sh = torch.randn(cin, generator=g) * 0.1
+    bias = torch.randn(cout, generator=g)
+    oh, ow = h - kh + 1, (w - kw) // sw + 1
+    xin = x.double()
+    if pre:
+        xin = torch.relu(xin * sc.double() + sh.double())
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), wt.double(), bias.double(), stride=(1, sw)).permute(0, 2, 3, 1)
+    tx = x.contiguous().to(cuda)
+    wp = K.pack_weight(wt.contiguous().to(cuda), L.BF16, 0)
+    preop = L.PRE_AFFINE_RELU if pre else L.PRE_NONE
+    A = K.conv(tx, L.KC, n, h, w, cin, oh, ow, kh, kw, sw=sw, pre=preop, scale=sc.to(cuda), shift=sh.to(cuda))
+    Bo = K.dense(wp, L.KC, cout, kh * kw * cin)
+    Kd = kh * kw * cin
+    assert L.load().mia_gemm_path(A, Bo, n * oh * ow, cout, Kd, L.BF16, 1) == 1
+    for odt in (torch.float32, torch.bfloat16):
+        out = torch.empty(n * oh * ow, cout, dtype=odt, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, cout, bias=bias.to(cuda)), n * oh * ow, cout, Kd, L.BF16)
+        torch.cuda.synchronize()
+        assert rel(out.float().view(n, oh, ow, cout).cpu(), ref) < 2e-2
+
+
+def test_rowconv_padded_dgrad(cuda):
+    """conv4 dgrad through the row-window path: padded dY (ph = pw = 7) x flipped weights."""
+    g = torch.Generator().manual_seed(11)
+    n, cin, cout, h, w, kh, kw = 2, 32, 32, 12, 400, 8, 8
+    oh, ow = h - kh + 1, w - kw + 1
+    wt = (torch.randn(cout, cin, kh, kw, generator=g) / 40).to(torch.bfloat16).float()
+    dy = torch.randn(n, oh, ow, cout, generator=g).to(torch.bfloat16)
+    xr = torch.zeros(n, cin, h, w, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wt.double()).backward(dy.double().permute(0, 3, 1, 2))
+    wf = K.pack_weight(wt.contiguous().to(cuda), L.BF16, 1)
+    A = K.conv(dy.contiguous().to(cuda), L.KC, n, oh, ow, cout, h, w, kh, kw, ph=kh - 1, pw=kw - 1)
+    Bo = K.dense(wf, L.KC, cin, kh * kw * cout)
+    assert L.load().mia_gemm_path(A, Bo, n * h * w, cin, kh * kw * cout, L.BF16, 1) == 1
+    dx = torch.empty(n * h * w, cin, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(dx, cin), n * h * w, cin, kh * kw * cout, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(dx.view(n, h, w, cin).cpu(), xr.grad.permute(0, 2, 3, 1)) < 2e-2
+
+
+@pytest.mark.parametrize("case", [
+    # n, cin, cout, h, w, kh, kw, sw, pre, dtype
+    (2, 32, 32, 12, 700, 8, 8, 1, True, torch.bfloat16),    # conv4 wgrad
+    (2, 32, 64, 1, 3001, 1, 16, 2, True, torch.bfloat16),   # conv2 wgrad (stride 2)
+    (3, 32, 64, 4, 300, 1, 4, 1, True, torch.bfloat16),     # trunk conv5 (1x4, 32 -> 64)
+    (3, 64, 64, 4, 300, 1, 4, 1, False, torch.bfloat16),    # trunk conv6 (1x4, 64 -> 64)
+    (2, 32, 32, 9, 333, 8, 8, 1, False, torch.float32),     # f32 storage
+    (2, 32, 32, 1, 901, 1, 16, 2, False, torch.bfloat16),   # stride 2, Cout 32
+])
+def test_rowwgrad_path(cuda, case):
+    """The row-window weight-gradient kernel (mia_gemm_path == 2) against float64 autograd."""
+    n, cin, cout, h, w, kh, kw, sw, pre, dt = case
+    g = torch.Generator().manual_seed(h * w + cout)
+    x = torch.randn(n, h, w, cin, generator=g).to(torch.bfloat16).to(dt)
+    sc = torch.rand(cin, generator=g) + 0.5
+    sh = torch.randn(cin, generator=g) * 0.1
+    oh, ow = h - kh + 1, (w - kw) // sw + 1
+    dy = torch.randn(n, oh, ow, cout, generator=g).to(torch.bfloat16).to(dt)
+    xin = x.double()
+    if pre:
+        xin = torch.relu(xin * sc.double() + sh.double())
+    wr = torch.zeros(cout, cin, kh, kw, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xin.permute(0, 3, 1, 2), wr, stride=(1, sw)).backward(dy.double().permute(0, 3, 1, 2))
+    P, Kc = n * oh * ow, kh * kw * cin
+    preop = L.PRE_AFFINE_RELU if pre else L.PRE_NONE
+    A = K.dense(dy.contiguous().to(cuda), L.RC, P, cout)
+    Bo = K.conv(x.contiguous().to(cuda), L.RC, n, h, w, cin, oh, ow, kh, kw, sw=sw, pre=preop,
+                scale=sc.to(cuda), shift=sh.to(cuda))
+    assert L.load().mia_gemm_path(A, Bo, cout, Kc, P, L.BF16, 2) == 2
+    dW = torch.empty(cout, Kc, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(dW, Kc), cout, Kc, P, L.BF16)
+    gw = torch.empty(cout, cin, kh, kw, device=cuda)
+    K.unpack_ohwi_grad(dW, (cout, cin, kh, kw), gw)
+    torch.cuda.synchronize()
+    assert rel(gw.cpu(), wr.grad) < 2e-2
