@@ -1063,6 +1063,223 @@ hipError_t rowwgrad_launch1(const RowWArgs& r, int NOUT, int S, int C, bool pre,
   return rowwgrad_launch2<T, 32, 1, 32, 8>(r, pre, s);
 }
 
+// -------------------------------------------------------------------------- single-channel tap wgrad
+// dW[n][ky][kx] = sum_{b,oy,ox} dY[b,oy,ox,n] * X[b, oy+ky, S*ox+kx]  for the 1-channel convs of
+// EnvNet-v2 (frontend conv1: 1x64 taps, stride 2 over the waveform; trunk conv3: 8x8 taps over the
+// 64 x Wp image).  N = 32 output channels, KH*KW = 64 taps.  Per chunk of BP output pixels the
+// block stages the dY tile [BP][32] (transposed MFMA reads) and, for every (ky, parity) tap
+// sequence seq[i] = X[oy+ky][S*(x0+i)+par], 8 copies shifted by 0..7 elements so that the 8
+// consecutive output pixels an MFMA k-group needs (X[..][S*(ox..ox+7)+kx]) are one aligned
+// 16-byte LDS read whatever the tap offset.  The 4 waves split the chunk's k-steps; partials are
+// summed through LDS into one f32 slab per block (ws[z][32][64]) -> splitk_reduce.
+struct TapWArgs {
+  const char* x;
+  const char* dy;
+  int n, h, wx, oh, ow;
+  int Z;
+  float* ws;
+};
+
+template <typename TD, typename TX, int S, int KH, int KW>
+__global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
+  constexpr int BP = 256;
+  constexpr int NS = KW / S;                       // taps per parity sequence
+  constexpr int LP = (BP + NS + 7) / 8 * 8;        // copy length
+  constexpr int LR = LP + 8;                       // raw length (covers shift 7)
+  constexpr int NSEQ = KH * S;
+  constexpr int CPB = LP * 2;                      // bytes per shifted copy
+  constexpr int SQB = 8 * CPB + 16;                // bytes per sequence (+16: parity banks)
+  constexpr int DYB = BP * 64;                     // dY tile [BP][32] bf16
+  constexpr int RAWB = NSEQ * LR * 2;
+  constexpr int CPYB = NSEQ * SQB;
+  constexpr int MAINB = DYB + RAWB + CPYB;
+  constexpr int REDB = 4 * 32 * 64 * 4;
+  constexpr int RCH = (NSEQ * LR + NT - 1) / NT;
+  constexpr int DCH = BP * 32 / 8 / NT;            // 4
+  static_assert(KH * KW == 64, "64 taps");
+  __shared__ __attribute__((aligned(16))) char smem[MAINB > REDB ? MAINB : REDB];
+  char* dyt = smem;
+  bf16* raw = reinterpret_cast<bf16*>(smem + DYB);
+  char* cpy = smem + DYB + RAWB;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int z = blockIdx.x;
+  const int CPR = (g.ow + BP - 1) / BP;
+  const int64_t nchunks = (int64_t)g.n * g.oh * CPR;
+  const TD* dys = reinterpret_cast<const TD*>(g.dy);
+  const TX* xs = reinterpret_cast<const TX*>(g.x);
+
+  u32x4 dreg[DCH];
+  float rreg[RCH];
+
+  auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
+    const int64_t row = c / CPR;
+    const int x0 = (int)(c - row * CPR) * BP;
+    const int b = (int)(row / g.oh), oy = (int)(row - (int64_t)b * g.oh);
+    const TD* src = dys + ((int64_t)row * g.ow + x0) * 32;
+#pragma unroll
+    for (int s2 = 0; s2 < DCH; ++s2) {
+      const int q = t + NT * s2;
+      const int p = q >> 2, cc = q & 3;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (x0 + p < g.ow) {
+        if constexpr (sizeof(TD) == 2) {
+          v = *reinterpret_cast<const u32x4*>(src + p * 32 + cc * 8);
+        } else {
+          const float4 a = reinterpret_cast<const float4*>(src + p * 32 + cc * 8)[0];
+          const float4 d = reinterpret_cast<const float4*>(src + p * 32 + cc * 8)[1];
+          const float f[8] = {a.x, a.y, a.z, a.w, d.x, d.y, d.z, d.w};
+          uint32_t w4[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
+                    ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          }
+          v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        }
+      }
+      dreg[s2] = v;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < RCH; ++s2) {
+      const int e = t + NT * s2;
+      float v = 0.f;
+      if (e < NSEQ * LR) {
+        const int seq = e / LR, i = e - seq * LR;
+        const int ky = seq / S, par = seq - ky * S;
+        const int iy = oy + ky;
+        const int ix = S * (x0 + i) + par;
+        if (iy < g.h && ix < g.wx) v = (float)xs[((int64_t)b * g.h + iy) * g.wx + ix];
+      }
+      rreg[s2] = v;
+    }
+  };
+  auto store_chunk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s2 = 0; s2 < DCH; ++s2) {
+      const int q = t + NT * s2;
+      *reinterpret_cast<u32x4*>(dyt + (q >> 2) * 64 + (q & 3) * 16) = dreg[s2];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < RCH; ++s2) {
+      const int e = t + NT * s2;
+      if (e < NSEQ * LR) raw[e] = (bf16)rreg[s2];
+    }
+  };
+  auto build_copies = [&]() __attribute__((always_inline)) {
+    constexpr int PIECES = NSEQ * 8 * (LP / 8);
+    for (int pc = t; pc < PIECES; pc += NT) {
+      const int seq = pc / (8 * (LP / 8));
+      const int rem = pc - seq * 8 * (LP / 8);
+      const int sh = rem / (LP / 8), blk = rem - sh * (LP / 8);
+      const unsigned short* r = reinterpret_cast<const unsigned short*>(raw) + seq * LR + blk * 8 + sh;
+      uint32_t w4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w4[i] = (uint32_t)r[2 * i] | ((uint32_t)r[2 * i + 1] << 16);
+      *reinterpret_cast<u32x4*>(cpy + seq * SQB + sh * CPB + blk * 16) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+    }
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  const int i16 = lane & 15, gq = lane >> 4, g2 = lane >> 5;
+  // this lane's tap per n-tile: n = nt*32 + (lane&31) -> (ky, kx) -> (seq, j)
+  int bseq[2], bj[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = nt * 32 + (lane & 31);
+    const int ky = n / KW, kx = n - ky * KW;
+    bseq[nt] = ky * S + kx % S;
+    bj[nt] = kx / S;
+  }
+
+  int64_t c = z;
+  if (c < nchunks) {
+    load_chunk(c);
+    store_chunk();
+  }
+  __syncthreads();
+  if (c < nchunks) build_copies();
+  __syncthreads();
+  for (; c < nchunks; c += g.Z) {
+    const int64_t cn = c + g.Z;
+    const bool more = cn < nchunks;
+    if (more) load_chunk(cn);
+#pragma unroll
+    for (int kk = 0; kk < BP / 16 / 4; ++kk) {
+      const int ks = wave + 4 * kk;
+      const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
+      const int col = 16 * (gq & 1) + 4 * (i16 & 3);
+      const char* p0 = dyt + kr * 64 + col * 2;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * 64));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8 fa = __builtin_bit_cast(bf16x8, cc);
+      const int ox0 = ks * 16 + 8 * g2;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int q = ox0 + bj[nt];
+        const int sh = q & 7;
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(cpy + bseq[nt] * SQB + sh * CPB + (q - sh) * 2);
+        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[nt], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_chunk();
+      __syncthreads();
+      build_copies();
+      __syncthreads();
+    }
+  }
+
+  // sum the 4 waves' partials, write the block's slab ws[z][32][64]
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = (r & 3) + 8 * (r >> 2) + 4 * g2;
+      red[(wave * 32 + m) * 64 + nt * 32 + (lane & 31)] = acc[nt][r];
+    }
+  __syncthreads();
+  float* dst = g.ws + (int64_t)z * 32 * 64;
+  for (int e = t; e < 32 * 64; e += NT)
+    dst[e] = red[e] + red[2048 + e] + red[4096 + e] + red[6144 + e];
+}
+
+// 1-channel conv wgrad (path 3): A = dY [P][32] as RC, B = CONVROW/RC with c == 1 (any stride
+// (1,1), kh*kw == 64) or the c == 2 stride-1 pair view of a stride-2 1-D conv (kw*2 == 64).
+bool tapwgrad_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
+  if (compute != MIA_BF16 || split < 2 || M != 32 || N != 64) return false;
+  if (A.kind != MIA_OP_DENSE || A.layout != MIA_LAYOUT_RC || A.pre != MIA_PRE_NONE) return false;
+  if (A.dtype != MIA_BF16 && A.dtype != MIA_F32) return false;
+  if (A.rows != K || A.cols != 32 || A.ld != 32) return false;
+  if (B.kind != MIA_OP_CONVROW || B.layout != MIA_LAYOUT_RC || B.pre != MIA_PRE_NONE) return false;
+  if (B.dtype != MIA_BF16 && B.dtype != MIA_F32) return false;
+  if (B.sh != 1 || B.sw != 1 || B.ph != 0 || B.pw != 0) return false;
+  if (K != (int64_t)B.n * B.oh * B.ow) return false;
+  const bool conv1 = B.c == 2 && B.kh == 1 && B.kw == 32 && B.h == 1;
+  const bool conv3 = B.c == 1 && B.kh == 8 && B.kw == 8;
+  if (!conv1 && !conv3) return false;
+  if (conv1 && B.dtype != MIA_F32) return false;
+  if ((reinterpret_cast<uintptr_t>(A.ptr) & 15)) return false;
+  return true;
+}
+
+template <typename TD, typename TX, int S, int KH, int KW>
+hipError_t tapwgrad_launch(const TapWArgs& r, hipStream_t s) {
+  tapwgrad_kernel<TD, TX, S, KH, KW><<<(unsigned)r.Z, NT, 0, s>>>(r);
+  return hipGetLastError();
+}
+
 // Row-window conv applies when: bf16 compute, no split, A = CONV/KC with stride (1, 1|2),
 // C in {32, 64}, KW*C a multiple of 128, B = the packed [N][KH*KW*C] bf16 weights, N in {32, 64}.
 bool rowconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
@@ -1212,6 +1429,30 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     if (err != hipSuccess) return mia::fail(-(int)err, "rowconv launch: %s", hipGetErrorString(err));
     return 0;
   }
+  if (workspace && tapwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
+    TapWArgs r;
+    r.x = reinterpret_cast<const char*>(B->ptr);
+    r.dy = reinterpret_cast<const char*>(A->ptr);
+    r.n = B->n; r.h = B->h; r.wx = B->w * B->c; r.oh = B->oh; r.ow = B->ow;
+    r.Z = split_k; r.ws = reinterpret_cast<float*>(workspace);
+    hipStream_t s = as_stream(stream);
+    hipError_t err;
+    if (B->c == 2) {  // frontend conv1: stride 2 over the waveform
+      err = A->dtype == MIA_BF16 ? tapwgrad_launch<bf16, float, 2, 1, 64>(r, s)
+                                 : tapwgrad_launch<float, float, 2, 1, 64>(r, s);
+    } else if (B->dtype == MIA_BF16) {
+      err = A->dtype == MIA_BF16 ? tapwgrad_launch<bf16, bf16, 1, 8, 8>(r, s)
+                                 : tapwgrad_launch<float, bf16, 1, 8, 8>(r, s);
+    } else {
+      err = A->dtype == MIA_BF16 ? tapwgrad_launch<bf16, float, 1, 8, 8>(r, s)
+                                 : tapwgrad_launch<float, float, 1, 8, 8>(r, s);
+    }
+    if (err != hipSuccess) return mia::fail(-(int)err, "tapwgrad launch: %s", hipGetErrorString(err));
+    int blocks = (int)std::min<int64_t>(cdiv(M * N, 256), 8192);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(r.ws, split_k, M, N, to_dev(*E));
+    MIA_LAUNCH_CHECK("splitk_reduce");
+    return 0;
+  }
   if (workspace && rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
     RowWArgs r;
     r.x = reinterpret_cast<const char*>(B->ptr);
@@ -1257,6 +1498,7 @@ extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M
   if (!A || !B) return -1;
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
   if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;
+  if (tapwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 3;
   return 0;
 }
 

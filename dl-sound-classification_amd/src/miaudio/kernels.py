@@ -145,8 +145,13 @@ def gemm(A: L.MiaOperand, B: L.MiaOperand, E: L.MiaEpilogue, M: int, N: int, K: 
          split_k: int | None = None, device=None, tag: str | None = None):
     lib = L.load()
     if split_k is None:
-        if compute == L.BF16 and lib.mia_gemm_path(A, B, M, N, K, compute, 2) == 2:
-            split_k = max(2, min(1024, 2048 // max(1, B.kh)))  # row-window wgrad: KH x split blocks
+        path = lib.mia_gemm_path(A, B, M, N, K, compute, 2) if compute == L.BF16 else 0
+        if path == 2:  # row-window wgrad: KH x split blocks, >= ~32 chunks of 128 px per block
+            chunks = B.n * B.oh * -(-B.ow // 128)
+            split_k = max(2, min(2048 // max(1, B.kh), chunks // 32))
+        elif path == 3:  # single-channel tap wgrad: split blocks over chunks of 256 px
+            chunks = B.n * B.oh * -(-B.ow // 256)
+            split_k = max(2, min(1024, chunks // 16))
         else:
             split_k = auto_split(M, N, K)
     ws = None

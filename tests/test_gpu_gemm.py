@@ -276,3 +276,42 @@ def test_rowwgrad_path(cuda, case):
     K.unpack_ohwi_grad(dW, (cout, cin, kh, kw), gw)
     torch.cuda.synchronize()
     assert rel(gw.cpu(), wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dydt", [torch.bfloat16, torch.float32])
+def test_tapwgrad_conv1(cuda, dydt):
+    """Frontend conv1 weight gradient (1x64 taps, stride 2 over the waveform) through path 3."""
+    g = torch.Generator().manual_seed(21)
+    n, T = 3, 2 * 3001 + 64
+    W1 = (T - 64) // 2 + 1
+    x = torch.randn(n, T, generator=g)
+    dy = torch.randn(n, W1, 32, generator=g).to(torch.bfloat16).to(dydt)
+    wr = torch.zeros(32, 1, 1, 64, dtype=torch.float64, requires_grad=True)
+    xb = x.to(torch.bfloat16).double()  # the kernel rounds the waveform to bf16 like the fwd operand
+    F.conv2d(xb.view(n, 1, 1, T), wr, stride=(1, 2)).backward(dy.double().permute(0, 2, 1).unsqueeze(2))
+    A = K.dense(dy.contiguous().to(cuda), L.RC, n * W1, 32)
+    Bo = K.conv(x.to(cuda), L.RC, n, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
+    assert L.load().mia_gemm_path(A, Bo, 32, 64, n * W1, L.BF16, 2) == 3
+    dW = torch.empty(32, 64, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(dW, 64), 32, 64, n * W1, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(dW.cpu(), wr.grad.view(32, 64)) < 1e-2
+
+
+@pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32])
+def test_tapwgrad_conv3(cuda, xdt):
+    """Trunk conv3 weight gradient (1 -> 32 channels, 8x8) through path 3."""
+    g = torch.Generator().manual_seed(22)
+    n, H, W = 2, 20, 600
+    ha, wa = H - 7, W - 7
+    x = torch.randn(n, H, W, generator=g).to(torch.bfloat16).to(xdt)
+    dy = torch.randn(n, ha, wa, 32, generator=g).to(torch.bfloat16)
+    wr = torch.zeros(32, 1, 8, 8, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double().unsqueeze(1), wr).backward(dy.double().permute(0, 3, 1, 2))
+    A = K.dense(dy.contiguous().to(cuda), L.RC, n * ha * wa, 32)
+    Bo = K.conv(x.contiguous().to(cuda), L.RC, n, H, W, 1, ha, wa, 8, 8, row_kind=True)
+    assert L.load().mia_gemm_path(A, Bo, 32, 64, n * ha * wa, L.BF16, 2) == 3
+    dW = torch.empty(32, 64, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(dW, 64), 32, 64, n * ha * wa, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(dW.cpu(), wr.grad.view(32, 64)) < 1e-2
