@@ -417,12 +417,13 @@ __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n,
   st_elem(e.ptr, e.dtype, idx, v);
 }
 
-// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no row map / aux / accumulate,
+// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no aux / accumulate,
 // act none|relu, 16-B aligned destination): bias as float4, 16-B stores.  Otherwise per element.
 __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t n0, int64_t N, const float* v) {
-  const int64_t idx = m * e.ldc + n0;
-  const bool fast = n0 + 16 <= N && !e.rm_inner && !e.accumulate &&
-                    (e.act == MIA_ACT_NONE || e.act == MIA_ACT_RELU) &&
+  int64_t prow = m;
+  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+  const int64_t idx = prow * e.ldc + n0;
+  const bool fast = n0 + 16 <= N && !e.accumulate && (e.act == MIA_ACT_NONE || e.act == MIA_ACT_RELU) &&
                     ((idx * (e.dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
                     ((reinterpret_cast<uintptr_t>(e.ptr)) & 15) == 0;
   if (!fast) {
@@ -823,7 +824,7 @@ struct RowWArgs {
   float* ws;
 };
 
-template <typename T, int NOUT, int S, int C, int KWMAX, bool PRE>
+template <typename T, int NOUT, int S, int C, int KWMAX, int KYB, bool PRE>
 __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
   constexpr int BP = 128;
   constexpr int CG = C / 8;
@@ -839,12 +840,12 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
   constexpr int MT = NOUT / 32;
   constexpr int TPW = MT * (KWMAX * C / 32) / 4;    // accumulator tiles per wave (upper bound)
   constexpr int ES = sizeof(T);
-  __shared__ __attribute__((aligned(16))) char smem[WBYTES + DBYTES];
+  __shared__ __attribute__((aligned(16))) char smem[KYB * WBYTES + DBYTES];
   char* win = smem;
-  char* dyt = smem + WBYTES;
+  char* dyt = smem + KYB * WBYTES;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int ky = blockIdx.x, z = blockIdx.y;
+  const int ky0 = blockIdx.x * KYB, z = blockIdx.y;
   const int NC = g.kw * C;                 // columns of this ky
   const int NCT = NC / 32;
   const int ntiles = MT * NCT;
@@ -858,7 +859,7 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
     for (int i = 0; i < 8; ++i) { sc[i] = g.ps[cg * 8 + i]; sh[i] = g.pt[cg * 8 + i]; }
   }
 
-  u32x4 wreg[WCH];
+  u32x4 wreg[KYB][WCH];
   u32x4 dreg[DCH];
 
   auto pack8 = [&](const float* f) __attribute__((always_inline)) {
@@ -902,10 +903,12 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
       }
       dreg[s] = v;
     }
-    const int iy = oy + ky - g.ph;
-    const bool rowok = iy >= 0 && iy < g.h;
     const int px0 = x0 * S - g.pw;
     const T* xs = reinterpret_cast<const T*>(g.x);
+#pragma unroll
+    for (int kyi = 0; kyi < KYB; ++kyi) {
+    const int iy = oy + ky0 + kyi - g.ph;
+    const bool rowok = iy >= 0 && iy < g.h;
 #pragma unroll
     for (int s = 0; s < WCH; ++s) {
       const int q = t + NT * s;
@@ -929,7 +932,8 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
           v = pack8(f);
         }
       }
-      wreg[s] = v;
+      wreg[kyi][s] = v;
+    }
     }
   };
   auto store_chunk = [&]() __attribute__((always_inline)) {
@@ -940,16 +944,18 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
       *reinterpret_cast<u32x4*>(dyt + p * DSB + cc * 16) = dreg[s];
     }
 #pragma unroll
+    for (int kyi = 0; kyi < KYB; ++kyi)
+#pragma unroll
     for (int s = 0; s < WCH; ++s) {
       const int q = t + NT * s;
       const int p = q / CG;
-      if (p < WPX) *reinterpret_cast<u32x4*>(win + win_slot<S, HALF>(p) * PSB + cg * 16) = wreg[s];
+      if (p < WPX) *reinterpret_cast<u32x4*>(win + kyi * WBYTES + win_slot<S, HALF>(p) * PSB + cg * 16) = wreg[kyi][s];
     }
   };
 
-  f32x16 acc[TPW];
+  f32x16 acc[KYB * TPW];
 #pragma unroll
-  for (int q = 0; q < TPW; ++q)
+  for (int q = 0; q < KYB * TPW; ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
 
@@ -979,6 +985,8 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
         fa[mt] = __builtin_bit_cast(bf16x8, cc);
       }
 #pragma unroll
+      for (int kyi = 0; kyi < KYB; ++kyi)
+#pragma unroll
       for (int q = 0; q < TPW; ++q) {
         const int tile = wave + 4 * q;
         if (tile < ntiles) {
@@ -988,7 +996,7 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
           int slot;
           if constexpr (S == 1) slot = kr + kx;
           else slot = (kx & 1) * HALF + kr + (kx >> 1);
-          const char* p0 = win + slot * PSB + ci * 2;
+          const char* p0 = win + kyi * WBYTES + slot * PSB + ci * 2;
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
           const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * PSB));
           typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -996,7 +1004,7 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
           const bf16x8 fb = __builtin_bit_cast(bf16x8, cc);
           bf16x8 a = fa[0];
           if constexpr (MT > 1) if (mt == 1) a = fa[1];
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, fb, acc[q], 0, 0, 0);
+          acc[kyi * TPW + q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, fb, acc[kyi * TPW + q], 0, 0, 0);
         }
       }
     }
@@ -1008,7 +1016,9 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
   }
 
   // partial slab: ws[z][m][ky*NC + n]
-  float* dst = g.ws + (int64_t)z * NOUT * g.Ntot + (int64_t)ky * NC;
+#pragma unroll
+  for (int kyi = 0; kyi < KYB; ++kyi) {
+  float* dst = g.ws + (int64_t)z * NOUT * g.Ntot + (int64_t)(ky0 + kyi) * NC;
 #pragma unroll
   for (int q = 0; q < TPW; ++q) {
     const int tile = wave + 4 * q;
@@ -1018,9 +1028,10 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        dst[(int64_t)m * g.Ntot + n] = acc[q][r];
+        dst[(int64_t)m * g.Ntot + n] = acc[kyi * TPW + q][r];
       }
     }
+  }
   }
 }
 
@@ -1041,11 +1052,11 @@ bool rowwgrad_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N,
   return true;
 }
 
-template <typename T, int NOUT, int S, int C, int KWMAX>
+template <typename T, int NOUT, int S, int C, int KWMAX, int KYB = 1>
 hipError_t rowwgrad_launch2(const RowWArgs& r, bool pre, hipStream_t s) {
-  dim3 grid((unsigned)r.kh, (unsigned)r.Z);
-  if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, true><<<grid, NT, 0, s>>>(r);
-  else rowwgrad_kernel<T, NOUT, S, C, KWMAX, false><<<grid, NT, 0, s>>>(r);
+  dim3 grid((unsigned)(r.kh / KYB), (unsigned)r.Z);
+  if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, true><<<grid, NT, 0, s>>>(r);
+  else rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, false><<<grid, NT, 0, s>>>(r);
   return hipGetLastError();
 }
 
@@ -1060,6 +1071,7 @@ hipError_t rowwgrad_launch1(const RowWArgs& r, int NOUT, int S, int C, bool pre,
     return rowwgrad_launch2<T, 32, 1, 64, 8>(r, pre, s);
   }
   if (NOUT == 64) return rowwgrad_launch2<T, 64, 1, 32, 8>(r, pre, s);
+  if (r.kh % 4 == 0) return rowwgrad_launch2<T, 32, 1, 32, 8, 4>(r, pre, s);  // conv4: dY chunk shared by 4 ky
   return rowwgrad_launch2<T, 32, 1, 32, 8>(r, pre, s);
 }
 

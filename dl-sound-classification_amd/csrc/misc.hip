@@ -42,16 +42,17 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, void* dst, int
 
 // ------------------------------------------------------------------ soft-label CE
 // One block; wave w handles rows w, w+4, ...
-__global__ __launch_bounds__(NT) void soft_ce_kernel(const float* __restrict__ logits, const float* __restrict__ y,
-                                                     int B, int C, int input_sigmoid, float* loss_out,
-                                                     float* __restrict__ dlogits, int* correct_out) {
-  __shared__ double wl[4];
-  __shared__ int wc[4];
+constexpr int CE_NT = 1024;
+__global__ __launch_bounds__(CE_NT) void soft_ce_kernel(const float* __restrict__ logits, const float* __restrict__ y,
+                                                        int B, int C, int input_sigmoid, float* loss_out,
+                                                        float* __restrict__ dlogits, int* correct_out) {
+  __shared__ double wl[CE_NT / 64];
+  __shared__ int wc[CE_NT / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double lsum = 0.0;
   int hits = 0;
   const float invB = 1.f / (float)B;
-  for (int b = wave; b < B; b += 4) {
+  for (int b = wave; b < B; b += CE_NT / 64) {
     const float* zr = logits + (int64_t)b * C;
     const float* yr = y + (int64_t)b * C;
     // pass 1: max of z (z = sigmoid(logit) if requested), argmax of logits and of y
@@ -103,13 +104,17 @@ __global__ __launch_bounds__(NT) void soft_ce_kernel(const float* __restrict__ l
   if (lane == 0) { wl[wave] = lsum; wc[wave] = hits; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    loss_out[0] = (float)((wl[0] + wl[1] + wl[2] + wl[3]) / (double)B);
-    if (correct_out) correct_out[0] = wc[0] + wc[1] + wc[2] + wc[3];
+    double tl = 0.0;
+    int tc = 0;
+    for (int w = 0; w < CE_NT / 64; ++w) { tl += wl[w]; tc += wc[w]; }
+    loss_out[0] = (float)(tl / (double)B);
+    if (correct_out) correct_out[0] = tc;
   }
 }
 
 // ------------------------------------------------------------------ clip + Adam
-constexpr int ADAM_PARTS = 4096;
+constexpr int ADAM_PARTS = 1024;
+constexpr int NF_NT = 1024;
 
 // Squared L2 norm partials of every gradient tensor: 16-B loads (tensor storage is 16-B aligned
 // torch allocations; a misaligned one takes the scalar path), f32 accumulation flushed to double.
@@ -147,26 +152,29 @@ __global__ __launch_bounds__(NT) void sqnorm_kernel(void* const* __restrict__ gr
 }
 
 // ws layout (doubles): [ntensors][ADAM_PARTS] partials, then [0] = coef (float in double slot)
-__global__ __launch_bounds__(NT) void norm_final_kernel(double* ws, int ntensors, int nparts, float clip, float* total_out,
-                                                        float* coef_out) {
+__global__ __launch_bounds__(NF_NT) void norm_final_kernel(double* ws, int ntensors, int nparts, float clip,
+                                                           float* total_out, float* coef_out) {
   double s = 0.0;
-  for (int i = threadIdx.x; i < ntensors * nparts; i += NT) {  // fixed order: deterministic
+  const int total = ntensors * nparts;
+  for (int i = threadIdx.x; i < total; i += NF_NT) {  // fixed order: deterministic
     const int tsr = i / nparts, p = i % nparts;
     s += ws[(int64_t)tsr * ADAM_PARTS + p];
   }
   s = wave_sum_d(s);
-  __shared__ double red[4];
+  __shared__ double red[NF_NT / 64];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double tot = sqrt(red[0] + red[1] + red[2] + red[3]);
-    const float total = (float)tot;
+    double acc = 0.0;
+    for (int w = 0; w < NF_NT / 64; ++w) acc += red[w];
+    const double tot = sqrt(acc);
+    const float totalf = (float)tot;
     float coef = 1.f;
     if (clip > 0.f) {
-      coef = clip / (total + 1e-6f);
+      coef = clip / (totalf + 1e-6f);
       if (coef > 1.f) coef = 1.f;
     }
-    if (total_out) total_out[0] = total;
+    if (total_out) total_out[0] = totalf;
     coef_out[0] = coef;
   }
 }
@@ -396,7 +404,7 @@ extern "C" int mia_pack_weight(const float* src, void* dst, int32_t dtype, int32
 extern "C" int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32_t input_sigmoid, float* loss,
                            float* dlogits, int32_t* correct, mia_stream_t stream) {
   MIA_CHECK_ARG(logits && y && loss && dlogits && B > 0 && C > 0, "soft_ce: args");
-  soft_ce_kernel<<<1, NT, 0, as_stream(stream)>>>(logits, y, B, C, input_sigmoid, loss, dlogits, correct);
+  soft_ce_kernel<<<1, CE_NT, 0, as_stream(stream)>>>(logits, y, B, C, input_sigmoid, loss, dlogits, correct);
   MIA_LAUNCH_CHECK("soft_ce");
   return 0;
 }
@@ -414,10 +422,10 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   hipStream_t s = as_stream(stream);
   double* ws = reinterpret_cast<double*>(sqnorm_ws);
   float* coef = reinterpret_cast<float*>(ws + (int64_t)ntensors * ADAM_PARTS);
-  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 64)));
+  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 256)));
   sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, reinterpret_cast<float*>(ws));
   MIA_LAUNCH_CHECK("sqnorm");
-  norm_final_kernel<<<1, NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);
+  norm_final_kernel<<<1, NF_NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);
   MIA_LAUNCH_CHECK("norm_final");
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);

@@ -146,9 +146,9 @@ def gemm(A: L.MiaOperand, B: L.MiaOperand, E: L.MiaEpilogue, M: int, N: int, K: 
     lib = L.load()
     if split_k is None:
         path = lib.mia_gemm_path(A, B, M, N, K, compute, 2) if compute == L.BF16 else 0
-        if path == 2:  # row-window wgrad: KH x split blocks, >= ~32 chunks of 128 px per block
+        if path == 2:  # row-window wgrad: (KH / ky-per-block) x split blocks, >= ~32 chunks of 128 px each
             chunks = B.n * B.oh * -(-B.ow // 128)
-            split_k = max(2, min(2048 // max(1, B.kh), chunks // 32))
+            split_k = max(2, min(512, chunks // 32))
         elif path == 3:  # single-channel tap wgrad: split blocks over chunks of 256 px
             chunks = B.n * B.oh * -(-B.ow // 256)
             split_k = max(2, min(1024, chunks // 16))
