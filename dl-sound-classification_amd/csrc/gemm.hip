@@ -1292,6 +1292,119 @@ hipError_t tapwgrad_launch(const TapWArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
+// -------------------------------------------------------------------------- single-channel tap conv (fwd)
+// y[b,oy,ox,n] = sum_{ky,kx} W[n][ky][kx] * X[b, oy+ky, S*ox+kx]  (+ epilogue) for conv1 (1x64,
+// stride 2 over the f32 waveform) and conv3 (8x8 over the 1-channel trunk image): K = 64 taps,
+// N = 32.  A block owns BP output pixels of one row; it stages the KH input row segments it reads
+// and 8 copies of each shifted by 0..7 samples, so that every MFMA A fragment (8 consecutive taps
+// = 8 consecutive samples at any offset) is one aligned ds_read_b128.  Weight fragments are read
+// once per wave straight from global memory (4 KB, L2-resident).  Output is HBM-write-bound.
+struct TapArgs {
+  const char* x;
+  int n, h, wx, oh, ow;
+  const bf16* wt;
+  EpiDev e;
+};
+
+template <typename TX, int S, int KH, int KW>
+__global__ __launch_bounds__(NT) void tapconv_kernel(TapArgs g) {
+  constexpr int BP = 256;
+  constexpr int RAWL = S * (BP - 1) + KW;
+  constexpr int LP = (RAWL + 7) / 8 * 8;     // copy length
+  constexpr int LR = LP + 8;                 // raw length
+  constexpr int CPB = LP * 2 + 16;           // bytes per copy (8-dword bank offset per copy)
+  constexpr int RAWB = KH * LR * 2;
+  constexpr int CPYB = KH * 8 * CPB;
+  constexpr int MAINB = RAWB + CPYB;
+  constexpr int STB = 4 * 32 * 33 * 4;
+  static_assert(KH * KW == 64, "64 taps");
+  __shared__ __attribute__((aligned(16))) char smem[MAINB > STB ? MAINB : STB];
+  bf16* raw = reinterpret_cast<bf16*>(smem);
+  char* cpy = smem + RAWB;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g2 = lane >> 5;
+  const int CPR = (g.ow + BP - 1) / BP;
+  const int64_t row = blockIdx.x / CPR;
+  const int x0 = (int)(blockIdx.x - row * CPR) * BP;
+  const int b = (int)(row / g.oh), oy = (int)(row - (int64_t)b * g.oh);
+  const TX* xs = reinterpret_cast<const TX*>(g.x);
+
+  for (int e = t; e < KH * LR; e += NT) {
+    const int ky = e / LR, i = e - ky * LR;
+    const int iy = oy + ky, ix = S * x0 + i;
+    float v = 0.f;
+    if (i < RAWL && iy < g.h && ix < g.wx) v = (float)xs[((int64_t)b * g.h + iy) * g.wx + ix];
+    raw[e] = (bf16)v;
+  }
+  // weight fragments: k-step ks covers taps ks*16 .. +15, lane holds 8 of them for column lane&31
+  bf16x8 fb[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    fb[ks] = *reinterpret_cast<const bf16x8*>(g.wt + (lane & 31) * 64 + ks * 16 + 8 * g2);
+  __syncthreads();
+  for (int pc = t; pc < KH * 8 * (LP / 8); pc += NT) {
+    const int ky = pc / (8 * (LP / 8));
+    const int rem = pc - ky * 8 * (LP / 8);
+    const int sh = rem / (LP / 8), blk = rem - sh * (LP / 8);
+    const unsigned short* r = reinterpret_cast<const unsigned short*>(raw) + ky * LR + blk * 8 + sh;
+    uint32_t w4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w4[i] = (uint32_t)r[2 * i] | ((uint32_t)r[2 * i + 1] << 16);
+    *reinterpret_cast<u32x4*>(cpy + (ky * 8 + sh) * CPB + blk * 16) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+  }
+  __syncthreads();
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    const int rel = wave * 64 + i * 32 + (lane & 31);   // pixel within the chunk
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k0 = ks * 16 + 8 * g2;
+      const int ky = k0 / KW, kx0 = k0 - ky * KW;
+      const int q = S * rel + kx0;
+      const int sh = q & 7;
+      const bf16x8 fa = *reinterpret_cast<const bf16x8*>(cpy + (ky * 8 + sh) * CPB + (q - sh) * 2);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb[ks], acc[i], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
+  const int64_t mrow0 = row * g.ow;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      stage[((r & 3) + 8 * (r >> 2) + 4 * g2) * 33 + (lane & 31)] = acc[i][r];
+    __syncthreads();
+    const int prow = lane >> 1, c0 = (lane & 1) * 16;
+    const int ox = x0 + wave * 64 + i * 32 + prow;
+    if (ox < g.ow) {
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = stage[prow * 33 + c0 + c];
+      epi_store16(g.e, mrow0 + ox, c0, 32, v);
+    }
+    __syncthreads();
+  }
+}
+
+bool tapconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
+  if (compute != MIA_BF16 || split > 1 || N != 32 || K != 64) return false;
+  if (A.kind != MIA_OP_CONVROW || A.layout != MIA_LAYOUT_KC || A.pre != MIA_PRE_NONE) return false;
+  if (A.dtype != MIA_BF16 && A.dtype != MIA_F32) return false;
+  if (A.sh != 1 || A.sw != 1 || A.ph != 0 || A.pw != 0) return false;
+  const bool conv1 = A.c == 2 && A.kh == 1 && A.kw == 32 && A.h == 1 && A.dtype == MIA_F32;
+  const bool conv3 = A.c == 1 && A.kh == 8 && A.kw == 8;
+  if (!conv1 && !conv3) return false;
+  if (M != (int64_t)A.n * A.oh * A.ow) return false;
+  if (B.kind != MIA_OP_DENSE || B.layout != MIA_LAYOUT_KC || B.dtype != MIA_BF16) return false;
+  if (B.rows != 32 || B.cols != 64 || B.ld != 64 || (reinterpret_cast<uintptr_t>(B.ptr) & 15)) return false;
+  return true;
+}
+
 // Row-window conv applies when: bf16 compute, no split, A = CONV/KC with stride (1, 1|2),
 // C in {32, 64}, KW*C a multiple of 128, B = the packed [N][KH*KW*C] bf16 weights, N in {32, 64}.
 bool rowconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
@@ -1330,6 +1443,37 @@ hipError_t rowconv_launch1(const RowArgs& r, int S, int C, bool pre, hipStream_t
   }
   if (r.N == 64) return rowconv_launch2<TS, 128, 64, 1, 32, 8>(r, pre, s);
   return rowconv_launch2<TS, 256, 32, 1, 32, 8>(r, pre, s);
+}
+
+// Many-slab reduction (split >= 32): 16 outputs x 16 slab lanes per block, fixed per-lane slab
+// order and a fixed LDS tree -> deterministic; the plain kernel walks all slabs per thread.
+__global__ __launch_bounds__(256) void splitk_reduce_wide_kernel(const float* ws, int split, int64_t M, int64_t N,
+                                                                 EpiDev e) {
+  __shared__ float red[16][17];
+  const int64_t total = M * N;
+  const int o = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int64_t idx = (int64_t)blockIdx.x * 16 + o;
+  float s = 0.f;
+  if (idx < total)
+    for (int z = zl; z < split; z += 16) s += ws[(int64_t)z * total + idx];
+  red[zl][o] = s;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float a = 0.f;
+    for (int k = 0; k < 16; ++k) a += red[k][threadIdx.x];
+    const int64_t id = (int64_t)blockIdx.x * 16 + threadIdx.x;
+    if (id < total) epi_store(e, id / N, id % N, a);
+  }
+}
+
+void launch_splitk_reduce(const float* ws, int split, int64_t M, int64_t N, const EpiDev& e, hipStream_t s) {
+  const int64_t total = M * N;
+  if (split >= 32 && total <= (1ll << 22)) {
+    splitk_reduce_wide_kernel<<<(unsigned)cdiv(total, 16), 256, 0, s>>>(ws, split, M, N, e);
+  } else {
+    int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(ws, split, M, N, e);
+  }
 }
 
 OpDev to_dev(const MiaOperand& o) {
@@ -1426,6 +1570,21 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   if (split_k < 1) split_k = 1;
   if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");
   if (M == 0 || N == 0) return 0;
+  if (tapconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
+    TapArgs r;
+    r.x = reinterpret_cast<const char*>(A->ptr);
+    r.n = A->n; r.h = A->h; r.wx = A->w * A->c; r.oh = A->oh; r.ow = A->ow;
+    r.wt = reinterpret_cast<const bf16*>(B->ptr);
+    r.e = to_dev(*E);
+    const int64_t blocks = (int64_t)A->n * A->oh * cdiv(A->ow, 256);
+    MIA_CHECK_ARG(blocks < (1ll << 31), "tapconv: too many chunks");
+    hipStream_t s = as_stream(stream);
+    if (A->c == 2) tapconv_kernel<float, 2, 1, 64><<<(unsigned)blocks, NT, 0, s>>>(r);
+    else if (A->dtype == MIA_BF16) tapconv_kernel<bf16, 1, 8, 8><<<(unsigned)blocks, NT, 0, s>>>(r);
+    else tapconv_kernel<float, 1, 8, 8><<<(unsigned)blocks, NT, 0, s>>>(r);
+    MIA_LAUNCH_CHECK("tapconv");
+    return 0;
+  }
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
     RowArgs r;
     r.x = reinterpret_cast<const char*>(A->ptr);
@@ -1460,8 +1619,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
                                  : tapwgrad_launch<float, float, 1, 8, 8>(r, s);
     }
     if (err != hipSuccess) return mia::fail(-(int)err, "tapwgrad launch: %s", hipGetErrorString(err));
-    int blocks = (int)std::min<int64_t>(cdiv(M * N, 256), 8192);
-    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(r.ws, split_k, M, N, to_dev(*E));
+    launch_splitk_reduce(r.ws, split_k, M, N, to_dev(*E), s);
     MIA_LAUNCH_CHECK("splitk_reduce");
     return 0;
   }
@@ -1478,9 +1636,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     hipError_t err = A->dtype == MIA_BF16 ? rowwgrad_launch1<bf16>(r, (int)M, B->sw, B->c, pre, s)
                                           : rowwgrad_launch1<float>(r, (int)M, B->sw, B->c, pre, s);
     if (err != hipSuccess) return mia::fail(-(int)err, "rowwgrad launch: %s", hipGetErrorString(err));
-    const int64_t total = M * N;
-    int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
-    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(r.ws, split_k, M, N, to_dev(*E));
+    launch_splitk_reduce(r.ws, split_k, M, N, to_dev(*E), s);
     MIA_LAUNCH_CHECK("splitk_reduce");
     return 0;
   }
@@ -1497,9 +1653,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
                                              : launch_t<float>(g, A->layout, B->layout, s);
   if (err != hipSuccess) return mia::fail(-(int)err, "gemm launch: %s", hipGetErrorString(err));
   if (split_k > 1) {
-    const int64_t total = M * N;
-    int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
-    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g.ws, split_k, M, N, g.e);
+    launch_splitk_reduce(g.ws, split_k, M, N, g.e, s);
     MIA_LAUNCH_CHECK("splitk_reduce");
   }
   return 0;
@@ -1508,6 +1662,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
 extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                              int32_t compute_dtype, int32_t split_k) {
   if (!A || !B) return -1;
+  if (tapconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 4;
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
   if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;
   if (tapwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 3;
@@ -1520,8 +1675,7 @@ extern "C" int mia_splitk_reduce(const float* ws, int32_t split_k, int64_t M, in
   EpiDev e = to_dev(*E);
   const int64_t total = M * N;
   if (total == 0) return 0;
-  int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
-  splitk_reduce_kernel<<<blocks, 256, 0, as_stream(stream)>>>(ws, split_k, M, N, e);
+  launch_splitk_reduce(ws, split_k, M, N, e, as_stream(stream));
   MIA_LAUNCH_CHECK("splitk_reduce");
   return 0;
 }

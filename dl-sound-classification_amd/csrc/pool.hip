@@ -23,14 +23,14 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
                                                       const float* __restrict__ shift, void* out, int layout,
                                                       uint8_t* __restrict__ argmax) {
   const int OH = H / kh, OW = W / kw, G = C / 8;
-  const int64_t total = (int64_t)n * OH * OW * G;
-  for (int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * NT) {
-    const int cg = (int)(idx % G);
-    int64_t p = idx / G;
-    const int ox = (int)(p % OW);
+  const int total = n * OH * OW * G;  // < 2^31 (checked by the launcher): 32-bit index math
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < total; idx += gridDim.x * NT) {
+    const int cg = idx % G;
+    int p = idx / G;
+    const int ox = p % OW;
     p /= OW;
-    const int oy = (int)(p % OH);
-    const int b = (int)(p / OH);
+    const int oy = p % OH;
+    const int b = p / OH;
     float sc[8], sh[8], best[8];
     int arg[8];
 #pragma unroll
@@ -91,13 +91,13 @@ __global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ d
     sc[i] = scale[cg * 8 + i]; sh[i] = shift[cg * 8 + i]; mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i];
   }
   float s1[8] = {0}, s2[8] = {0};
-  const int64_t P = (int64_t)n * H * W;
-  for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
-    const int ix = (int)(r % W);
-    const int64_t q = r / W;
-    const int iy = (int)(q % H);
-    const int b = (int)(q / H);
-    const int64_t off = r * C + cg * 8;
+  const int P = n * H * W;  // < 2^31 (checked by the launcher): 32-bit index math
+  for (int r = blockIdx.x * rslots + rs; r < P; r += gridDim.x * rslots) {
+    const int ix = r % W;
+    const int q = r / W;
+    const int iy = q % H;
+    const int b = q / H;
+    const int64_t off = (int64_t)r * C + cg * 8;
     float g[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) g[i] = 0.f;
@@ -153,12 +153,12 @@ __global__ void partial_final_kernel(const float* __restrict__ partial, int nblk
 // out[b][ih][iw] = sum_ky p[b][ih-ky][iw][ky]
 __global__ void col2im_rows_kernel(const float* __restrict__ p, int n, int ph, int w, int kh, void* out, int dtype) {
   const int H = ph + kh - 1;
-  const int64_t total = (int64_t)n * H * w;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
-    const int iw = (int)(idx % w);
-    const int64_t q = idx / w;
-    const int ih = (int)(q % H);
-    const int b = (int)(q / H);
+  const int total = n * H * w;  // < 2^31 (checked by the launcher)
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int iw = idx % w;
+    const int q = idx / w;
+    const int ih = q % H;
+    const int b = q / H;
     float s = 0.f;
     for (int ky = 0; ky < kh; ++ky) {
       const int r = ih - ky;
@@ -176,6 +176,7 @@ extern "C" int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, 
   MIA_CHECK_ARG(x && out && argmax, "pool_fwd: null pointer");
   MIA_CHECK_ARG(c % 8 == 0 && kh > 0 && kw > 0 && kh * kw <= 256 && h >= kh && w >= kw, "pool_fwd: bad geometry");
   MIA_CHECK_ARG(out_layout >= 0 && out_layout <= 2 && (out_layout != 1 || h / kh == 1), "pool_fwd: bad layout");
+  MIA_CHECK_ARG((int64_t)n * h * w * (c / 8) < (1ll << 31), "pool_fwd: too many elements for 32-bit indexing");
   const int64_t total = (int64_t)n * (h / kh) * (w / kw) * (c / 8);
   const int nb = (int)std::min<int64_t>(cdiv(total, NT), 16384);
   pool_fwd_kernel<<<nb, NT, 0, as_stream(stream)>>>(x, dtype, n, h, w, c, kh, kw, scale, shift, out, out_layout, argmax);
@@ -191,6 +192,7 @@ extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout,
   MIA_CHECK_ARG(dout && argmax && x && scale && shift && mean && invstd && dz && dgamma && dbeta && partial,
                 "pool_bwd: null pointer");
   MIA_CHECK_ARG(c % 8 == 0 && c >= 8 && (NT % (c / 8)) == 0, "pool_bwd: channels");
+  MIA_CHECK_ARG((int64_t)n * h * w < (1ll << 31), "pool_bwd: too many pixels for 32-bit indexing");
   const int rslots = NT / (c / 8);
   const int64_t P = (int64_t)n * h * w;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
@@ -206,6 +208,7 @@ extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout,
 extern "C" int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh, void* out, int32_t dtype,
                                mia_stream_t stream) {
   MIA_CHECK_ARG(p && out && n > 0 && ph > 0 && w > 0 && kh > 0, "col2im_rows: bad arguments");
+  MIA_CHECK_ARG((int64_t)n * (ph + kh - 1) * w < (1ll << 31), "col2im_rows: too many elements");
   const int64_t total = (int64_t)n * (ph + kh - 1) * w;
   const int nb = (int)std::min<int64_t>(cdiv(total, 256), 16384);
   col2im_rows_kernel<<<nb, 256, 0, as_stream(stream)>>>(p, n, ph, w, kh, out, dtype);

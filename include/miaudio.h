@@ -88,7 +88,7 @@ int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int
  * convs, the frontend conv2 and their dgrads), 2 = row-window weight gradient (A = dY as RC,
  * B = the conv input as RC, M = Cout in {32,64}, split_k >= 2 partial slabs: blocks = KH x split),
  * 3 = single-channel tap weight gradient (conv1 pair view / 1-channel 8x8 conv3, M = 32, N = 64,
- * split_k >= 2 blocks). */
+ * split_k >= 2 blocks), 4 = single-channel tap conv forward (the same two convs, N = 32, K = 64). */
 int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                   int32_t compute_dtype, int32_t split_k);
 

@@ -315,3 +315,44 @@ def test_tapwgrad_conv3(cuda, xdt):
     K.gemm(A, Bo, K.epilogue(dW, 64), 32, 64, n * ha * wa, L.BF16)
     torch.cuda.synchronize()
     assert rel(dW.cpu(), wr.grad.view(32, 64)) < 1e-2
+
+
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+def test_tapconv_conv1_fwd(cuda, odt):
+    """Frontend conv1 forward (1x64 taps, stride 2, bias) through path 4."""
+    g = torch.Generator().manual_seed(31)
+    n, T = 3, 2 * 3001 + 64
+    W1 = (T - 64) // 2 + 1
+    x = torch.randn(n, T, generator=g)
+    wt = (torch.randn(32, 1, 1, 64, generator=g) / 8).to(torch.bfloat16).float()
+    bias = torch.randn(32, generator=g)
+    ref = F.conv2d(x.to(torch.bfloat16).double().view(n, 1, 1, T), wt.double(), bias.double(), stride=(1, 2))
+    ref = ref[:, :, 0].permute(0, 2, 1)
+    wp = K.pack_weight(wt.contiguous().to(cuda), L.BF16, 0)
+    A = K.conv(x.to(cuda), L.KC, n, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
+    Bo = K.dense(wp, L.KC, 32, 64)
+    assert L.load().mia_gemm_path(A, Bo, n * W1, 32, 64, L.BF16, 1) == 4
+    out = torch.empty(n * W1, 32, dtype=odt, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out, 32, bias=bias.to(cuda)), n * W1, 32, 64, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(out.float().view(n, W1, 32).cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32])
+def test_tapconv_conv3_fwd(cuda, xdt):
+    """Trunk conv3 forward (1 -> 32 channels, 8x8) through path 4."""
+    g = torch.Generator().manual_seed(32)
+    n, H, W = 2, 20, 700
+    ha, wa = H - 7, W - 7
+    x = torch.randn(n, H, W, generator=g).to(torch.bfloat16).to(xdt)
+    wt = (torch.randn(32, 1, 8, 8, generator=g) / 8).to(torch.bfloat16).float()
+    bias = torch.randn(32, generator=g)
+    ref = F.conv2d(x.double().unsqueeze(1), wt.double(), bias.double()).permute(0, 2, 3, 1)
+    wp = K.pack_weight(wt.contiguous().to(cuda), L.BF16, 0)
+    A = K.conv(x.contiguous().to(cuda), L.KC, n, H, W, 1, ha, wa, 8, 8, row_kind=True)
+    Bo = K.dense(wp, L.KC, 32, 64)
+    assert L.load().mia_gemm_path(A, Bo, n * ha * wa, 32, 64, L.BF16, 1) == 4
+    out = torch.empty(n * ha * wa, 32, dtype=torch.bfloat16, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out, 32, bias=bias.to(cuda)), n * ha * wa, 32, 64, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(out.float().view(n, ha, wa, 32).cpu(), ref) < 1e-2
