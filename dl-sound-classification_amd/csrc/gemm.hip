@@ -408,6 +408,10 @@ __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n,
     }
     case MIA_DACT_GELU: v *= gelu_erf_grad(ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n)); break;
     case MIA_ACT_ADD_AUX: v += ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n); break;
+    case MIA_ACT_GELU_SAVE:
+      st_elem(const_cast<char*>(e.aux), e.aux_dtype, m * e.ldaux + n, v);
+      v = gelu_erf(v);
+      break;
     default: break;
   }
   int64_t prow = m;
@@ -417,15 +421,62 @@ __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n,
   st_elem(e.ptr, e.dtype, idx, v);
 }
 
-// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no aux / accumulate,
-// act none|relu, 16-B aligned destination): bias as float4, 16-B stores.  Otherwise per element.
+__device__ __forceinline__ void ld16(const void* p, int dtype, int64_t idx, float* f) {
+  if (dtype == MIA_BF16) {
+    const uint4* q = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + idx);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4 u = q[h];
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[8 * h + 2 * i] = __uint_as_float(w[i] << 16);
+        f[8 * h + 2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    }
+  } else {
+    const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float4 u = q[h];
+      f[4 * h] = u.x; f[4 * h + 1] = u.y; f[4 * h + 2] = u.z; f[4 * h + 3] = u.w;
+    }
+  }
+}
+
+__device__ __forceinline__ void st16(void* p, int dtype, int64_t idx, const float* o) {
+  if (dtype == MIA_BF16) {
+    uint32_t w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16 lo = (bf16)o[2 * c], hi = (bf16)o[2 * c + 1];
+      w[c] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+}
+
+// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no accumulate, 16-B aligned output
+// and aux rows): bias as float4, aux read/written with 16-B accesses, 16-B stores.  Otherwise per
+// element.
 __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t n0, int64_t N, const float* v) {
   int64_t prow = m;
   if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
   const int64_t idx = prow * e.ldc + n0;
-  const bool fast = n0 + 16 <= N && !e.accumulate && (e.act == MIA_ACT_NONE || e.act == MIA_ACT_RELU) &&
+  const bool uses_aux = e.act == MIA_DACT_NZ || e.act == MIA_DACT_GELU || e.act == MIA_ACT_ADD_AUX ||
+                        e.act == MIA_ACT_GELU_SAVE;
+  const int64_t aidx = m * e.ldaux + n0;
+  const bool fast = n0 + 16 <= N && !e.accumulate &&
                     ((idx * (e.dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
-                    ((reinterpret_cast<uintptr_t>(e.ptr)) & 15) == 0;
+                    ((reinterpret_cast<uintptr_t>(e.ptr)) & 15) == 0 &&
+                    (!uses_aux || (((aidx * (e.aux_dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
+                                   ((reinterpret_cast<uintptr_t>(e.aux)) & 15) == 0));
   if (!fast) {
     for (int c = 0; c < 16; ++c)
       if (n0 + c < N) epi_store(e, m, n0 + c, v[c]);
@@ -448,22 +499,28 @@ __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t 
   if (e.act == MIA_ACT_RELU) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) o[c] = fmaxf(o[c], 0.f);
-  }
-  if (e.dtype == MIA_BF16) {
-    uint32_t w[8];
+  } else if (e.act == MIA_ACT_GELU) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const bf16 lo = (bf16)o[2 * c], hi = (bf16)o[2 * c + 1];
-      w[c] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
+  } else if (e.act == MIA_ACT_GELU_SAVE) {
+    st16(const_cast<char*>(e.aux), e.aux_dtype, aidx, o);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
+  } else if (uses_aux) {
+    float a[16];
+    ld16(e.aux, e.aux_dtype, aidx, a);
+    if (e.act == MIA_DACT_NZ) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) o[c] = a[c] != 0.f ? o[c] * e.act_scale : 0.f;
+    } else if (e.act == MIA_DACT_GELU) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) o[c] *= gelu_erf_grad(a[c]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) o[c] += a[c];
     }
-    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(e.ptr) + idx);
-    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  } else {
-    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(e.ptr) + idx);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   }
+  st16(e.ptr, e.dtype, idx, o);
 }
 
 template <typename T, int BM, int BN, int WM, int LA, int LB>
@@ -1405,6 +1462,203 @@ bool tapconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, 
   return true;
 }
 
+// -------------------------------------------------------------------------- dense bf16 GEMM (LDS-DMA)
+// C = A . B^T for bf16 DENSE operands in any KC/RC layout combination (AST linears fwd/dgrad/wgrad,
+// EnvNet FC layers).  128x128x64 tiles, 4 waves (2x2, 64x64 each, MFMA 32x32x16), both operands
+// staged global -> LDS with global_load_lds_dwordx4 (no register staging, no VALU address work
+// in the loop beyond a pointer bump), double-buffered: the next K-tile's DMA is issued before the
+// current tile's MFMAs, retired with a counted vmcnt + raw s_barrier.  LDS images are XOR-swizzled
+// on the SOURCE address (the DMA destination is lane-linear): KC rows of 128 B permute their 16-B
+// chunks by (row & 7) (conflict-free ds_read_b128 per 8 lanes); RC rows of 256 B permute their
+// 32-B blocks by (k & 3) (conflict-free ds_read_b64_tr_b16 per 16 lanes).  Blocks are remapped so
+// that neighbouring tiles share an XCD (bijective XCD swizzle) and walk M fastest (B-tile reuse).
+struct DArgs {
+  const bf16* a;
+  const bf16* b;
+  int64_t lda, ldb, M, N, K, kper;
+  int split, nbm, nbn;
+  float* ws;
+  EpiDev e;
+};
+
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef const __attribute__((address_space(1))) void* glb_vp;
+
+template <int L>
+struct DLoader {
+  // per-lane source pointers for this wave's 4 DMA instructions of a tile, advanced per K-tile
+  const bf16* src[4];
+  int64_t step;
+  __device__ __forceinline__ void init(const bf16* base, int64_t ld, int64_t rows_or_cols, int64_t r0, int64_t kbeg,
+                                       int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;
+      if constexpr (L == MIA_LAYOUT_KC) {
+        const int r = 8 * j + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        int64_t row = r0 + r;
+        if (row >= rows_or_cols) row = rows_or_cols - 1;
+        src[i] = base + row * ld + kbeg + c * 8;
+      } else {
+        const int kr = 4 * j + (lane >> 4);
+        const int p = lane & 15;
+        const int c = 2 * ((p >> 1) ^ (kr & 3)) + (p & 1);
+        int64_t col = r0 + c * 8;
+        if (col + 8 > rows_or_cols) col = rows_or_cols - 8;
+        src[i] = base + (kbeg + kr) * ld + col;
+      }
+    }
+    step = L == MIA_LAYOUT_KC ? 64 : 64 * ld;
+  }
+  __device__ __forceinline__ void issue(char* tile, int wave) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((glb_vp)src[i], (lds_vp)(tile + (wave * 4 + i) * 1024), 16, 0, 0);
+      src[i] += step;
+    }
+  }
+};
+
+template <int L>
+__device__ __forceinline__ bf16x8 dfrag(const char* tile, int rbase, int ks, int lane) {
+  if constexpr (L == MIA_LAYOUT_KC) {
+    const int rr = rbase + (lane & 31);
+    const int c = 2 * ks + (lane >> 5);
+    return *reinterpret_cast<const bf16x8*>(tile + rr * 128 + ((c ^ (rr & 7)) * 16));
+  } else {
+    const int i16 = lane & 15, gq = lane >> 4;
+    const int col = rbase + 16 * (gq & 1) + 4 * (i16 & 3);
+    const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
+    const char* p0 = tile + kr * 256 + (((col >> 4) ^ (kr & 3)) * 32) + (col & 15) * 2;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * 256));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, cc);
+  }
+}
+
+template <int LA, int LB>
+__global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
+  constexpr int TILE = 128 * 64 * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = g.nbm * g.nbn;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int bm = wgid % g.nbm, bn = wgid / g.nbm;
+  const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
+  const int z = blockIdx.y;
+  const int64_t kbeg = (int64_t)z * g.kper;
+  int64_t kend = kbeg + g.kper;
+  if (kend > g.K) kend = g.K;
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
+
+  DLoader<LA> la;
+  DLoader<LB> lb;
+  la.init(g.a, g.lda, LA == MIA_LAYOUT_KC ? g.M : g.M, m0, kbeg, wave, lane);
+  lb.init(g.b, g.ldb, g.N, n0, kbeg, wave, lane);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    la.issue(smem, wave);
+    lb.issue(smem + TILE, wave);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * 2 * TILE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * 2 * TILE;
+      la.issue(nxt, wave);
+      lb.issue(nxt + TILE, wave);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* As = cur;
+    const char* Bs = cur + TILE;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = dfrag<LA>(As, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = dfrag<LB>(Bs, wn * 64 + j * 32, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = acc[i][j][r];
+      __syncthreads();
+      const int row = lane >> 1, c0 = (lane & 1) * 16;
+      const int64_t m = m0 + wm * 64 + i * 32 + row;
+      const int64_t nb = n0 + wn * 64 + j * 32 + c0;
+      if (m < g.M && nb < g.N) {
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = stage[row * 33 + c0 + c];
+        if (g.split > 1) {
+          float* dst = g.ws + ((int64_t)z * g.M + m) * g.N + nb;
+          if (nb + 16 <= g.N && (g.N & 3) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              reinterpret_cast<float4*>(dst)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+          } else {
+            for (int c = 0; c < 16; ++c)
+              if (nb + c < g.N) dst[c] = v[c];
+          }
+        } else {
+          epi_store16(g.e, m, nb, g.N, v);
+        }
+      }
+      __syncthreads();
+    }
+}
+
+bool dgemm_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute) {
+  if (compute != MIA_BF16 || K < 64 || K % 64 != 0 || M < 64 || N < 64) return false;
+  if (A.kind != MIA_OP_DENSE || B.kind != MIA_OP_DENSE) return false;
+  if (A.dtype != MIA_BF16 || B.dtype != MIA_BF16 || A.pre != MIA_PRE_NONE || B.pre != MIA_PRE_NONE) return false;
+  if (A.ld % 8 || B.ld % 8 || (reinterpret_cast<uintptr_t>(A.ptr) & 15) || (reinterpret_cast<uintptr_t>(B.ptr) & 15))
+    return false;
+  if (A.layout == MIA_LAYOUT_KC) { if (A.rows != M || A.cols < K) return false; }
+  else { if (A.rows < K || A.cols != M || M % 8) return false; }
+  if (B.layout == MIA_LAYOUT_KC) { if (B.rows != N || B.cols < K) return false; }
+  else { if (B.rows < K || B.cols != N || N % 8) return false; }
+  if (cdiv(M, 128) * cdiv(N, 128) >= (1ll << 31)) return false;
+  return true;
+}
+
+template <int LA, int LB>
+hipError_t dgemm_launch2(const DArgs& d, hipStream_t s) {
+  dim3 grid((unsigned)(d.nbm * d.nbn), (unsigned)d.split);
+  dgemm_kernel<LA, LB><<<grid, NT, 0, s>>>(d);
+  return hipGetLastError();
+}
+
 // Row-window conv applies when: bf16 compute, no split, A = CONV/KC with stride (1, 1|2),
 // C in {32, 64}, KW*C a multiple of 128, B = the packed [N][KH*KW*C] bf16 weights, N in {32, 64}.
 bool rowconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute, int split) {
@@ -1565,11 +1819,31 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   if (int r = check_operand(*B, "B")) return r;
   MIA_CHECK_ARG(E->ptr != nullptr, "gemm: output is null");
   MIA_CHECK_ARG(compute_dtype == MIA_F32 || compute_dtype == MIA_BF16, "gemm: compute dtype");
-  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU || E->act == MIA_ACT_ADD_AUX)
+  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU || E->act == MIA_ACT_ADD_AUX || E->act == MIA_ACT_GELU_SAVE)
     MIA_CHECK_ARG(E->aux != nullptr, "gemm: this epilogue needs aux");
   if (split_k < 1) split_k = 1;
   if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");
   if (M == 0 || N == 0) return 0;
+  if (dgemm_ok(*A, *B, M, N, K, compute_dtype) && (split_k <= 1 || workspace)) {
+    DArgs d;
+    d.a = reinterpret_cast<const bf16*>(A->ptr); d.b = reinterpret_cast<const bf16*>(B->ptr);
+    d.lda = A->ld; d.ldb = B->ld; d.M = M; d.N = N; d.K = K;
+    d.split = split_k < 1 ? 1 : split_k;
+    d.kper = cdiv(cdiv(K, d.split), 64) * 64;
+    d.nbm = (int)cdiv(M, 128); d.nbn = (int)cdiv(N, 128);
+    d.ws = reinterpret_cast<float*>(workspace);
+    d.e = to_dev(*E);
+    hipStream_t s = as_stream(stream);
+    hipError_t err;
+    const int la = A->layout, lb = B->layout;
+    if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
+    else if (la == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_RC>(d, s);
+    else if (lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_KC>(d, s);
+    else err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC>(d, s);
+    if (err != hipSuccess) return mia::fail(-(int)err, "dgemm launch: %s", hipGetErrorString(err));
+    if (d.split > 1) launch_splitk_reduce(d.ws, d.split, M, N, d.e, s);
+    return 0;
+  }
   if (tapconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
     TapArgs r;
     r.x = reinterpret_cast<const char*>(A->ptr);
@@ -1662,6 +1936,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
 extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                              int32_t compute_dtype, int32_t split_k) {
   if (!A || !B) return -1;
+  if (dgemm_ok(*A, *B, M, N, K, compute_dtype)) return 5;
   if (tapconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 4;
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
   if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;

@@ -19,7 +19,7 @@ F32, BF16, U8 = 0, 1, 2
 OP_DENSE, OP_CONV, OP_CONVROW = 0, 1, 2
 KC, RC = 0, 1
 PRE_NONE, PRE_AFFINE, PRE_AFFINE_RELU, PRE_GELU = 0, 1, 2, 3
-ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU, ACT_ADD_AUX = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU, ACT_ADD_AUX, ACT_GELU_SAVE = 0, 1, 2, 3, 4, 5, 6
 
 vp = C.c_void_p
 i32 = C.c_int32

@@ -4,9 +4,11 @@ Reference op sequence: src/models/ast.py:50-63 + timm 1.0.16 Block (pre-LN, qkv 
 SDPA, proj, LN, fc1, exact-erf GELU, fc2), LN eps 1e-6, sigmoid head on the CLS token.
 HBM layout per block (T = B*1645 tokens, D = 768): residual stream x (T, 768) f32; LN outputs,
 qkv (T, 3, 12, 64), attention output (T, 12, 64) and fc1 pre-activation (T, 3072) in the compute
-dtype.  GELU is never materialised: fc2 applies it while staging its operand (MIA_PRE_GELU) and the
-fc1 backward applies gelu' in the epilogue of the dgrad GEMM (MIA_DACT_GELU); residual adds are GEMM
-epilogues (MIA_ACT_ADD_AUX / accumulate).
+dtype.  fc1's epilogue writes both gelu(u) (fc2's operand) and the pre-activation u
+(MIA_ACT_GELU_SAVE); the fc1 backward applies gelu'(u) in the epilogue of the fc2 dgrad GEMM
+(MIA_DACT_GELU); residual adds are GEMM epilogues (MIA_ACT_ADD_AUX / accumulate).  In bf16 mode the
+linear weights are cast to bf16 once per step and every GEMM operand is bf16, so the projections run
+on the LDS-DMA dense kernel (mia_gemm path 5).
 """
 from __future__ import annotations
 
@@ -50,6 +52,8 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
 def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag=""):
     """dW = dy^T x (f32), db = colsum(dy), dx = dy @ W (optionally with an activation backward)."""
     Nf, Kf = W.shape
+    if cd == L.BF16 and dy.dtype == torch.float32:
+        dy = K.cast(dy, torch.bfloat16)  # bf16 GEMM operands (f32 accumulation inside)
     dW = torch.empty(Nf, Kf, dtype=torch.float32, device=dy.device)
     K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf), Nf, Kf, M, cd,
            tag=tag + ".wgrad")
@@ -91,8 +95,12 @@ class ASTFunction(torch.autograd.Function):
         saved_blocks = []
         nb = len(model.transformer)
         scale = (D // Hh) ** -0.5
+        wcast = []
         for i in range(nb):
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = params[4 + 12 * i: 16 + 12 * i]
+            if cd == L.BF16:
+                wqkv, wproj, w1, w2 = (K.cast(w, torch.bfloat16) for w in (wqkv, wproj, w1, w2))
+            wcast.append((wqkv, wproj, w1, w2))
             h, m1, r1 = _ln(x, g1, b1, tdt, Tt, D)
             qkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
             _linear(h, wqkv, bqkv, qkv, Tt, cd, tag="qkv.fwd")
@@ -104,11 +112,13 @@ class ASTFunction(torch.autograd.Function):
             xm = torch.empty(Tt, D, dtype=torch.float32, device=dev)
             _linear(a, wproj, bproj, xm, Tt, cd, act=L.ACT_ADD_AUX, aux=x, tag="proj.fwd")
             h2, m2, r2 = _ln(xm, g2, b2, tdt, Tt, D)
-            u = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
-            _linear(h2, w1, bb1, u, Tt, cd, tag="fc1.fwd")
+            u = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)   # fc1 pre-activation
+            gu = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)  # gelu(u)
+            _linear(h2, w1, bb1, gu, Tt, cd, act=L.ACT_GELU_SAVE, aux=u, tag="fc1.fwd")
             xo = torch.empty(Tt, D, dtype=torch.float32, device=dev)
-            _linear(u, w2, bb2, xo, Tt, cd, act=L.ACT_ADD_AUX, aux=xm, pre=L.PRE_GELU, tag="fc2.fwd")
-            saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u))
+            _linear(gu, w2, bb2, xo, Tt, cd, act=L.ACT_ADD_AUX, aux=xm, tag="fc2.fwd")
+            saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u,
+                                     gu=gu))
             x = xo
         # final norm only matters for the CLS rows (ast.py:62-63 takes x[:, 0])
         gn, bn_, wh, bh = params[4 + 12 * nb: 8 + 12 * nb]
@@ -117,7 +127,7 @@ class ASTFunction(torch.autograd.Function):
         z = torch.empty(B, wh.shape[0], dtype=torch.float32, device=dev)
         _linear(hc, wh, bh, z, B, cd, tag="head.fwd")
         probs = torch.sigmoid(z)
-        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec, gh=gh, gw=gw, blocks=saved_blocks, xc=xc,
+        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec, gh=gh, gw=gw, blocks=saved_blocks, xc=xc, wcast=wcast,
                      mc=mc, rc=rc, hc=hc, probs=probs, scale=scale)
         ctx.model = model
         ctx.params = params
@@ -155,10 +165,11 @@ class ASTFunction(torch.autograd.Function):
         for i in reversed(range(nb)):
             sb = s["blocks"][i]
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = p[4 + 12 * i: 16 + 12 * i]
+            wqkv, wproj, w1, w2 = s["wcast"][i]
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
-            dW2, db2_ = _linear_bwd(dx, sb["u"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
-                                    x_pre=L.PRE_GELU, tag="fc2")
+            dW2, db2_ = _linear_bwd(dx, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
+                                    tag="fc2")
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
             dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1")
             dg2, dbt2 = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True)  # dx now = d(xm)

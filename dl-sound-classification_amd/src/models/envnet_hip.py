@@ -159,14 +159,19 @@ class EnvNetFunction(torch.autograd.Function):
         saved["trunk"] = trunk_saved
         saved["flat"] = flat
 
-        # ---- classifier (FC weights streamed as f32 and converted while staging)
+        # ---- classifier (bf16 mode: FC1/FC2 weights cast to bf16 once per step -> LDS-DMA dense GEMM;
+        # f32 mode: weights streamed as f32)
         drop_p = model.classifier[3].p if training else 0.0
         h = flat
         hs = []
+        wfc = []
         for li, idx in enumerate((1, 4, 7)):
             Wt, bias = p[40 + 2 * li], p[41 + 2 * li]
             fout, fin = Wt.shape
             last = li == 2
+            if cd == L.BF16 and not last:
+                Wt = K.cast(Wt, torch.bfloat16)
+            wfc.append(Wt)
             out = torch.empty(B, fout, dtype=torch.float32 if last else tdt, device=dev)
             K.gemm(K.dense(h, L.KC, B, fin), K.dense(Wt, L.KC, fout, fin),
                    K.epilogue(out, fout, act=L.ACT_NONE if last else L.ACT_RELU, bias=bias), B, fout, fin, cd,
@@ -176,6 +181,7 @@ class EnvNetFunction(torch.autograd.Function):
             hs.append(out)
             h = out
         saved["h1"], saved["h2"] = hs[0], hs[1]
+        saved["wfc"] = wfc
         saved["drop_p"] = drop_p
         if getattr(model, "_debug_capture", False):
             model._debug = saved
@@ -211,7 +217,7 @@ class EnvNetFunction(torch.autograd.Function):
         acts = [s["flat"], s["h1"], s["h2"]]
         dcur = glogits
         for li in (2, 1, 0):
-            Wt = p[40 + 2 * li]
+            Wt = s["wfc"][li]
             fout, fin = Wt.shape
             hin = acts[li]
             dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)

@@ -33,7 +33,7 @@ enum { MIA_OP_DENSE = 0, MIA_OP_CONV = 1, MIA_OP_CONVROW = 2 };
 enum { MIA_LAYOUT_KC = 0, MIA_LAYOUT_RC = 1 };
 enum { MIA_PRE_NONE = 0, MIA_PRE_AFFINE = 1, MIA_PRE_AFFINE_RELU = 2, MIA_PRE_GELU = 3 };
 enum { MIA_ACT_NONE = 0, MIA_ACT_RELU = 1, MIA_ACT_GELU = 2, MIA_DACT_NZ = 3, MIA_DACT_GELU = 4,
-       MIA_ACT_ADD_AUX = 5 };
+       MIA_ACT_ADD_AUX = 5, MIA_ACT_GELU_SAVE = 6 };
 
 /* A GEMM operand = a logical 2-D source S[i][j] whose j axis is contiguous in memory.
  *  DENSE   : S[i][j] = ptr[i*ld + j], i < rows, j < cols (zero outside).
@@ -62,7 +62,8 @@ typedef struct MiaOperand {
  *   (m / rm_inner)*rm_outer + (m % rm_inner)*rm_istride + rm_offset.
  *   DACT_NZ  : v *= (aux[m][n] != 0) * act_scale   (ReLU+dropout backward from saved output)
  *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation)
- *   ADD_AUX  : v += aux[m][n]                       (residual connection into a new tensor) */
+ *   ADD_AUX  : v += aux[m][n]                       (residual connection into a new tensor)
+ *   GELU_SAVE: aux[m][n] = v; v = gelu(v)          (MLP fc1: keeps the pre-activation for the backward) */
 typedef struct MiaEpilogue {
   void* ptr;
   int32_t dtype, act, accumulate, aux_dtype;
@@ -88,7 +89,8 @@ int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int
  * convs, the frontend conv2 and their dgrads), 2 = row-window weight gradient (A = dY as RC,
  * B = the conv input as RC, M = Cout in {32,64}, split_k >= 2 partial slabs: blocks = KH x split),
  * 3 = single-channel tap weight gradient (conv1 pair view / 1-channel 8x8 conv3, M = 32, N = 64,
- * split_k >= 2 blocks), 4 = single-channel tap conv forward (the same two convs, N = 32, K = 64). */
+ * split_k >= 2 blocks), 4 = single-channel tap conv forward (the same two convs, N = 32, K = 64),
+ * 5 = dense bf16 GEMM with LDS-DMA staging (bf16 DENSE operands, K % 64 == 0, M, N >= 64). */
 int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                   int32_t compute_dtype, int32_t split_k);
 

@@ -356,3 +356,48 @@ def test_tapconv_conv3_fwd(cuda, xdt):
     K.gemm(A, Bo, K.epilogue(out, 32, bias=bias.to(cuda)), n * ha * wa, 32, 64, L.BF16)
     torch.cuda.synchronize()
     assert rel(out.float().view(n, ha, wa, 32).cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
+@pytest.mark.parametrize("M,N,Kd,split", [(256, 256, 128, 1), (296, 200, 192, 1), (128, 1000, 512, 1),
+                                          (256, 384, 4096, 4), (64, 72, 64, 1)])
+def test_dgemm_path(cuda, la, lb, M, N, Kd, split):
+    """The LDS-DMA dense bf16 GEMM (mia_gemm_path == 5) against float64, every layout pair."""
+    g = torch.Generator().manual_seed(M + N + Kd)
+    a, A, ta = _mat(la, M, Kd, torch.bfloat16, cuda, g)
+    b, Bo, tb = _mat(lb, N, Kd, torch.bfloat16, cuda, g)
+    assert L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, split) == 5
+    bias = torch.randn(N, generator=g)
+    out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out, N, bias=bias.to(cuda)), M, N, Kd, L.BF16, split_k=split)
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double().t() + bias.double()
+    assert rel(out.cpu(), ref) < 1e-3
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu_save", "dact_gelu", "add_aux"])
+def test_dgemm_epilogues(cuda, act):
+    g = torch.Generator().manual_seed(5)
+    M, N, Kd = 320, 256, 256
+    a = torch.randn(M, Kd, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, Kd, generator=g).to(torch.bfloat16)
+    aux = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    A, Bo = K.dense(a.to(cuda), L.KC, M, Kd), K.dense(w.to(cuda), L.KC, N, Kd)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    z = a.double() @ w.double().t()
+    taux = aux.to(cuda).clone()
+    code = {"relu": L.ACT_RELU, "gelu_save": L.ACT_GELU_SAVE, "dact_gelu": L.DACT_GELU, "add_aux": L.ACT_ADD_AUX}[act]
+    K.gemm(A, Bo, K.epilogue(out, N, act=code, aux=None if act == "relu" else taux, ldaux=N), M, N, Kd, L.BF16)
+    torch.cuda.synchronize()
+    if act == "relu":
+        ref = torch.relu(z)
+    elif act == "gelu_save":
+        ref = F.gelu(z)
+        assert rel(taux.float().cpu(), z) < 1e-2  # pre-activation saved into aux
+    elif act == "dact_gelu":
+        x = aux.double().requires_grad_(True)
+        F.gelu(x).backward(torch.ones_like(x))
+        ref = z * x.grad
+    else:
+        ref = z + aux.double()
+    assert rel(out.float().cpu(), ref) < 1e-2
