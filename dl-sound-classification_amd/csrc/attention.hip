@@ -44,6 +44,27 @@ __device__ __forceinline__ void stage64(bf16* lds, const bf16* g, int64_t ld, in
   }
 }
 
+// Register-staged tile copy, split so the global loads of tile t+1 fly under tile t's MFMAs
+// (issue early / write late): 64 rows x 64 bf16 = 2 x 16 B per thread.
+struct Stage64 {
+  uint4 v[2];
+  __device__ __forceinline__ void load(const bf16* g, int64_t ld, int nvalid, int t) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = t + 256 * s;
+      const int row = c >> 3, c16 = c & 7;
+      v[s] = row < nvalid ? *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(bf16* lds, int t) const {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = t + 256 * s;
+      *reinterpret_cast<uint4*>(lds + (c >> 3) * LROW + (c & 7) * 8) = v[s];
+    }
+  }
+};
+
 // Row fragment: tile[row][16ks + 8h + j], j = 0..7 (A operand rows / B operand columns).
 __device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int ks, int lane) {
   return *reinterpret_cast<const bf16x8*>(lds + row * LROW + ks * 16 + 8 * (lane >> 5));
@@ -87,8 +108,8 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 // ------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                        float* __restrict__ lse, int N, int H, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D;
@@ -99,46 +120,65 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) qf[ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qvalid);
   f32x16 o0 = zero16(), o1 = zero16();
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // m: running max of the log2-scaled scores
   const int ntiles = (N + 63) / 64;
+  Stage64 kreg, vreg;
+  kreg.load(base + H * D, ldt, N, t);
+  vreg.load(base + 2 * H * D, ldt, N, t);
+  kreg.store(Ks[0], t);
+  vreg.store(Vs[0], t);
+  __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * 64;
-    __syncthreads();
-    stage64(Ks, base + (int64_t)k0 * ldt + H * D, ldt, N - k0, t);
-    stage64(Vs, base + (int64_t)k0 * ldt + 2 * H * D, ldt, N - k0, t);
-    __syncthreads();
+    const bool more = kt + 1 < ntiles;
+    if (more) {
+      kreg.load(base + (int64_t)(k0 + 64) * ldt + H * D, ldt, N - k0 - 64, t);
+      vreg.load(base + (int64_t)(k0 + 64) * ldt + 2 * H * D, ldt, N - k0 - 64, t);
+    }
+    const bf16* K_ = Ks[kt & 1];
+    const bf16* V_ = Vs[kt & 1];
+    const bool tail = k0 + 64 > N;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       f32x16 s = zero16();
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s = mfma(frag_row(Ks, st * 32 + (lane & 31), ks, lane), qf[ks], s);
+      for (int ks = 0; ks < 4; ++ks) s = mfma(frag_row(K_, st * 32 + (lane & 31), ks, lane), qf[ks], s);
+      if (tail) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + st * 32 + acc_row(r, lane) >= N) s[r] = -INFINITY;
+      }
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + st * 32 + acc_row(r, lane);
-        s[r] = key < N ? s[r] * scale_log2 : -INFINITY;
-        mx = fmaxf(mx, s[r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
       const float mn = fmaxf(m, mx);
-      const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
-      float ls = 0.f;
+      // rescale O only when some lane's running max moved (wave-uniform branch)
+      if (__any(mn > m)) {
+        const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
+        l *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+      m = mn;
+      const float nm = mn == -INFINITY ? 0.f : -mn;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s[r] = mn == -INFINITY ? 0.f : exp2f(s[r] - mn);
-        ls += s[r];
+        s[r] = exp2f(fmaf(s[r], scale_log2, nm));
+        l += s[r];
       }
-      l = l * alpha + ls;
-      m = mn;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 pf = acc_frag(s, sk);
-        o0 = mfma(frag_tr(Vs, st * 32 + 16 * sk, 0, lane), pf, o0);
-        o1 = mfma(frag_tr(Vs, st * 32 + 16 * sk, 32, lane), pf, o1);
+        o0 = mfma(frag_tr(V_, st * 32 + 16 * sk, 0, lane), pf, o0);
+        o1 = mfma(frag_tr(V_, st * 32 + 16 * sk, 32, lane), pf, o1);
       }
     }
+    if (more) {
+      kreg.store(Ks[(kt + 1) & 1], t);
+      vreg.store(Vs[(kt + 1) & 1], t);
+    }
+    __syncthreads();
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   if (qvalid) {
@@ -161,14 +201,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 // delta[b,h,q] = sum_d dO[q][d] * O[q][d]
 __global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout, float* __restrict__ delta,
                                   int B, int N, int H) {
-  const int64_t total = (int64_t)B * N * H;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int hd = (int)(i % H);
-    const int64_t bq = i / H;
-    const int q = (int)(bq % N);
-    const int b = (int)(bq / N);
-    const bf16* o = out + i * D;
-    const bf16* g = dout + i * D;
+  const int total = B * N * H;  // < 2^31 (checked by the launcher)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int hd = i % H;
+    const int bq = i / H;
+    const int q = bq % N;
+    const int b = bq / N;
+    const bf16* o = out + (int64_t)i * D;
+    const bf16* g = dout + (int64_t)i * D;
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < D / 8; ++c) {
@@ -186,10 +226,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                             int N, int H, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Qs[64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Gs[64 * LROW];
-  __shared__ __attribute__((aligned(16))) float Ls[64];
-  __shared__ __attribute__((aligned(16))) float Ds[64];
+  __shared__ __attribute__((aligned(16))) bf16 Qs[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Gs[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) float Ls[2][64];
+  __shared__ __attribute__((aligned(16))) float Ds[2][64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
@@ -205,43 +245,60 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   }
   f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
   const int ntiles = (N + 63) / 64;
-  for (int qt = 0; qt < ntiles; ++qt) {
-    const int q0 = qt * 64;
-    __syncthreads();
-    stage64(Qs, base + (int64_t)q0 * ldt, ldt, N - q0, t);
-    stage64(Gs, gbase + (int64_t)q0 * ldo, ldo, N - q0, t);
+  Stage64 qreg, greg;
+  float lreg = 0.f, dreg = 0.f;
+  auto load_rows = [&](int q0) __attribute__((always_inline)) {
+    qreg.load(base + (int64_t)q0 * ldt, ldt, N - q0, t);
+    greg.load(gbase + (int64_t)q0 * ldo, ldo, N - q0, t);
     if (t < 64) {
       const int q = q0 + t;
-      Ls[t] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;  // q >= N -> p = 0
-      Ds[t] = q < N ? delta[(int64_t)bh * N + q] : 0.f;
+      lreg = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;  // q >= N -> p = 0
+      dreg = q < N ? delta[(int64_t)bh * N + q] : 0.f;
     }
-    __syncthreads();
+  };
+  auto store_rows = [&](int buf) __attribute__((always_inline)) {
+    qreg.store(Qs[buf], t);
+    greg.store(Gs[buf], t);
+    if (t < 64) { Ls[buf][t] = lreg; Ds[buf][t] = dreg; }
+  };
+  load_rows(0);
+  store_rows(0);
+  __syncthreads();
+  for (int qt = 0; qt < ntiles; ++qt) {
+    const bool more = qt + 1 < ntiles;
+    if (more) load_rows((qt + 1) * 64);
+    const bf16* Q_ = Qs[qt & 1];
+    const bf16* G_ = Gs[qt & 1];
+    const float* L_ = Ls[qt & 1];
+    const float* D_ = Ds[qt & 1];
 #pragma unroll
     for (int sq = 0; sq < 2; ++sq) {
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma(frag_row(Qs, sq * 32 + (lane & 31), ks, lane), kf[ks], s);
-        dp = mfma(frag_row(Gs, sq * 32 + (lane & 31), ks, lane), vf[ks], dp);
+        s = mfma(frag_row(Q_, sq * 32 + (lane & 31), ks, lane), kf[ks], s);
+        dp = mfma(frag_row(G_, sq * 32 + (lane & 31), ks, lane), vf[ks], dp);
       }
       // rows of the accumulators are queries sq*32 + acc_row(r)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = sq * 32 + acc_row(r, lane);
-        const float p = exp2f(s[r] * scale_log2 - Ls[qi]);
+        const float p = exp2f(fmaf(s[r], scale_log2, -L_[qi]));
         s[r] = p;
-        dp[r] = p * (dp[r] - Ds[qi]);
+        dp[r] = p * (dp[r] - D_[qi]);
       }
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 pf = acc_frag(s, sk);
         const bf16x8 df = acc_frag(dp, sk);
-        dv0 = mfma(frag_tr(Gs, sq * 32 + 16 * sk, 0, lane), pf, dv0);
-        dv1 = mfma(frag_tr(Gs, sq * 32 + 16 * sk, 32, lane), pf, dv1);
-        dk0 = mfma(frag_tr(Qs, sq * 32 + 16 * sk, 0, lane), df, dk0);
-        dk1 = mfma(frag_tr(Qs, sq * 32 + 16 * sk, 32, lane), df, dk1);
+        dv0 = mfma(frag_tr(G_, sq * 32 + 16 * sk, 0, lane), pf, dv0);
+        dv1 = mfma(frag_tr(G_, sq * 32 + 16 * sk, 32, lane), pf, dv1);
+        dk0 = mfma(frag_tr(Q_, sq * 32 + 16 * sk, 0, lane), df, dk0);
+        dk1 = mfma(frag_tr(Q_, sq * 32 + 16 * sk, 32, lane), df, dk1);
       }
     }
+    if (more) store_rows((qt + 1) & 1);
+    __syncthreads();
   }
   if (kvalid) {
     bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
@@ -270,8 +327,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           bf16* __restrict__ dqkv, int N, int H, float scale,
                                                           float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
@@ -288,33 +345,47 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const float dq_delta = qvalid ? delta[(int64_t)bh * N + q] : 0.f;
   f32x16 a0 = zero16(), a1 = zero16();
   const int ntiles = (N + 63) / 64;
+  Stage64 kreg, vreg;
+  kreg.load(base + H * D, ldt, N, t);
+  vreg.load(base + 2 * H * D, ldt, N, t);
+  kreg.store(Ks[0], t);
+  vreg.store(Vs[0], t);
+  __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * 64;
-    __syncthreads();
-    stage64(Ks, base + (int64_t)k0 * ldt + H * D, ldt, N - k0, t);
-    stage64(Vs, base + (int64_t)k0 * ldt + 2 * H * D, ldt, N - k0, t);
-    __syncthreads();
+    const bool more = kt + 1 < ntiles;
+    if (more) {
+      kreg.load(base + (int64_t)(k0 + 64) * ldt + H * D, ldt, N - k0 - 64, t);
+      vreg.load(base + (int64_t)(k0 + 64) * ldt + 2 * H * D, ldt, N - k0 - 64, t);
+    }
+    const bf16* K_ = Ks[kt & 1];
+    const bf16* V_ = Vs[kt & 1];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma(frag_row(Ks, st * 32 + (lane & 31), ks, lane), qf[ks], s);
-        dp = mfma(frag_row(Vs, st * 32 + (lane & 31), ks, lane), gf[ks], dp);
+        s = mfma(frag_row(K_, st * 32 + (lane & 31), ks, lane), qf[ks], s);
+        dp = mfma(frag_row(V_, st * 32 + (lane & 31), ks, lane), gf[ks], dp);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + st * 32 + acc_row(r, lane);
-        const float p = key < N ? exp2f(s[r] * scale_log2 - lq) : 0.f;
+        const float p = key < N ? exp2f(fmaf(s[r], scale_log2, -lq)) : 0.f;
         dp[r] = p * (dp[r] - dq_delta);
       }
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 df = acc_frag(dp, sk);
-        a0 = mfma(frag_tr(Ks, st * 32 + 16 * sk, 0, lane), df, a0);
-        a1 = mfma(frag_tr(Ks, st * 32 + 16 * sk, 32, lane), df, a1);
+        a0 = mfma(frag_tr(K_, st * 32 + 16 * sk, 0, lane), df, a0);
+        a1 = mfma(frag_tr(K_, st * 32 + 16 * sk, 32, lane), df, a1);
       }
     }
+    if (more) {
+      kreg.store(Ks[(kt + 1) & 1], t);
+      vreg.store(Vs[(kt + 1) & 1], t);
+    }
+    __syncthreads();
   }
   if (qvalid) {
     bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
@@ -502,6 +573,7 @@ extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, 
     return 0;
   }
   MIA_CHECK_ARG(dtype == MIA_BF16, "attn_bwd: dtype");
+  MIA_CHECK_ARG(rows < (1ll << 31), "attn_bwd: B*N*H too large");
   attn_delta_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
       (const bf16*)out, (const bf16*)dout, delta, B, N, H);
   MIA_LAUNCH_CHECK("attn_delta");

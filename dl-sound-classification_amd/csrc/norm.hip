@@ -182,6 +182,34 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const void* __restrict__ x, 
   for (int64_t r = blockIdx.x; r < P; r += gridDim.x) s += ld_elem(x, dtype, r * ld + c);
   partial[(int64_t)blockIdx.x * C + c] = s;
 }
+// vectorised column sum (C % 8 == 0, 16-B aligned rows): thread = 8 columns x a row slot
+__global__ __launch_bounds__(NT) void colsum8_kernel(const void* __restrict__ x, int dtype, int64_t P, int C, int64_t ld,
+                                                     float* __restrict__ partial) {
+  __shared__ float red[NT * 8];
+  const int t = threadIdx.x;
+  const int G = C / 8, Gb = G < NT ? G : NT, rslots = NT / Gb;
+  const int cg = blockIdx.y * NT + t % Gb, rs = t / Gb;
+  float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rs < rslots && cg < G) {
+    for (int64_t r = (int64_t)blockIdx.x * rslots + rs; r < P; r += (int64_t)gridDim.x * rslots) {
+      float f[8];
+      load8(x, dtype, r * ld + cg * 8, f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s8[i] += f[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[t * 8 + i] = s8[i];
+  __syncthreads();
+  for (int e = t; e < Gb * 8; e += NT) {
+    const int g = e / 8, i = e % 8;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < rslots; ++r2) acc += red[(r2 * Gb + g) * 8 + i];
+    const int c = (blockIdx.y * NT + g) * 8 + i;
+    if (c < C) partial[(int64_t)blockIdx.x * C + c] = acc;
+  }
+}
+
 __global__ void colsum_final_kernel(const float* __restrict__ partial, int nblk, int C, float* out) {
   const int c = blockIdx.x;  // one block per column
   const double s = block_sum_strided(partial + c, nblk, C);
@@ -295,6 +323,97 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy,
   for (int i = threadIdx.x; i < 2 * D; i += NT) partial[(int64_t)blockIdx.x * 2 * D + i] = pg[i / D][i % D];
 }
 
+// Vectorised LayerNorm backward for D = 64*PER (PER % 4 == 0): lane owns PER contiguous features
+// (16-B / 8-B accesses), one wave per row, LN_VEC_ROWS rows per block; dgamma/dbeta partials are
+// summed per lane in registers, then across the 4 waves through LDS (fixed order, no atomics).
+constexpr int LN_VEC_ROWS = 64;
+
+template <int PER>
+__device__ __forceinline__ void ldv(const void* p, int dt, int64_t off, float* f) {
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) {
+    if (dt == MIA_BF16) {
+      const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(p) + off + 4 * q);
+      f[4 * q] = __uint_as_float(u.x << 16); f[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
+      f[4 * q + 2] = __uint_as_float(u.y << 16); f[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+      const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + off + 4 * q);
+      f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+    }
+  }
+}
+template <int PER>
+__device__ __forceinline__ void stv(void* p, int dt, int64_t off, const float* f) {
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) {
+    if (dt == MIA_BF16) {
+      const bf16 a = (bf16)f[4 * q], b = (bf16)f[4 * q + 1], c = (bf16)f[4 * q + 2], d = (bf16)f[4 * q + 3];
+      uint2 u;
+      u.x = (uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16);
+      u.y = (uint32_t)__builtin_bit_cast(unsigned short, c) | ((uint32_t)__builtin_bit_cast(unsigned short, d) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(p) + off + 4 * q) = u;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + off + 4 * q) =
+          make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+    }
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__ dy, int dydt, const void* __restrict__ x,
+                                                        int xdt, const float* __restrict__ g,
+                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                        void* dx, int dxdt, int accumulate, void* dx2, int dx2dt,
+                                                        float* __restrict__ partial, int64_t rows) {
+  constexpr int D = 64 * PER;
+  __shared__ float red[4][2][D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d0 = lane * PER;
+  float gg[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) gg[i] = g[d0 + i];
+  float ag[PER], ab[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * LN_VEC_ROWS;
+  for (int64_t row = r0 + wave; row < r0 + LN_VEC_ROWS && row < rows; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float dv[PER], xh[PER];
+    ldv<PER>(dy, dydt, row * D + d0, dv);
+    ldv<PER>(x, xdt, row * D + d0, xh);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      xh[i] = (xh[i] - mu) * rs;
+      ag[i] = fmaf(dv[i], xh[i], ag[i]);
+      ab[i] += dv[i];
+      dv[i] *= gg[i];
+      s1 += dv[i];
+      s2 = fmaf(dv[i], xh[i], s2);
+    }
+    s1 = wave_sum(s1) * (1.f / (float)D);
+    s2 = wave_sum(s2) * (1.f / (float)D);
+    float o[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) o[i] = rs * (dv[i] - s1 - xh[i] * s2);
+    if (accumulate) {
+      float old[PER];
+      ldv<PER>(dx, dxdt, row * D + d0, old);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) o[i] += old[i];
+    }
+    stv<PER>(dx, dxdt, row * D + d0, o);
+    if (dx2) stv<PER>(dx2, dx2dt, row * D + d0, o);
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { red[wave][0][d0 + i] = ag[i]; red[wave][1][d0 + i] = ab[i]; }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += NT) {
+    const int q = i / D, d = i % D;
+    partial[(int64_t)blockIdx.x * 2 * D + i] = ((red[0][q][d] + red[1][q][d]) + red[2][q][d]) + red[3][q][d];
+  }
+}
+
 __global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, float* dgamma, float* dbeta) {
   const int d = blockIdx.x;  // one block per feature
   const double a = block_sum_strided(partial + d, nblk, 2 * (int64_t)D);
@@ -377,7 +496,12 @@ extern "C" int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, in
   MIA_CHECK_ARG(x && out && partial && C > 0 && P > 0 && ld >= C, "colsum: bad arguments");
   int nb = (int)std::min<int64_t>(P, 256);
   hipStream_t s = as_stream(stream);
-  colsum_kernel<<<dim3(nb, (unsigned)cdiv(C, NT)), NT, 0, s>>>(x, dtype, P, C, ld, (float*)partial);
+  const int es = dtype == MIA_BF16 ? 2 : 4;
+  if (C % 8 == 0 && ld % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (int64_t)es * 8 >= 16) {
+    colsum8_kernel<<<dim3(nb, (unsigned)cdiv(C / 8, NT)), NT, 0, s>>>(x, dtype, P, C, ld, (float*)partial);
+  } else {
+    colsum_kernel<<<dim3(nb, (unsigned)cdiv(C, NT)), NT, 0, s>>>(x, dtype, P, C, ld, (float*)partial);
+  }
   MIA_LAUNCH_CHECK("colsum");
   colsum_final_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, out);
   MIA_LAUNCH_CHECK("colsum_final");
@@ -398,23 +522,32 @@ extern "C" int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gam
 }
 
 extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
-  return cdiv(rows, LN_ROWS_PER_BLOCK) * 2 * D * 4;
+  return cdiv(rows, LN_VEC_ROWS) * 2 * D * 4;
 }
 
 extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
                                  const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
-                                 float* dgamma, float* dbeta, void* partial, int64_t rows, int32_t D,
-                                 mia_stream_t stream) {
+                                 void* dx2, int32_t dx2dtype, float* dgamma, float* dbeta, void* partial, int64_t rows,
+                                 int32_t D, mia_stream_t stream) {
   MIA_CHECK_ARG(dy && x && gamma && mean && rstd && dx && partial, "layernorm_bwd: null pointer");
   MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_bwd: D must be <= 1024");
-  const unsigned nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
   hipStream_t s = as_stream(stream);
-  if (D <= 768)
-    ln_bwd_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
-                                        (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
-  else
-    ln_bwd_kernel<16><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
-                                        (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
+  unsigned nb;
+  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0;
+  if (D == 768 && al) {
+    nb = (unsigned)cdiv(rows, LN_VEC_ROWS);
+    ln_bwd_vec_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                            dx2, dx2dtype, (float*)partial, rows);
+  } else {
+    MIA_CHECK_ARG(dx2 == nullptr, "layernorm_bwd: the bf16 copy needs D == 768 and aligned rows");
+    nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
+    if (D <= 768)
+      ln_bwd_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                          (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
+    else
+      ln_bwd_kernel<16><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                          (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
+  }
   MIA_LAUNCH_CHECK("layernorm_bwd");
   ln_partial_final_kernel<<<(unsigned)D, 256, 0, s>>>((const float*)partial, (int)nb, D, dgamma, dbeta);
   MIA_LAUNCH_CHECK("layernorm_partial_final");

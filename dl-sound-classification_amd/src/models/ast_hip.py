@@ -30,14 +30,17 @@ def _ln(x, g, b, out_dtype, rows, D):
     return y, mean, rstd
 
 
-def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool):
+def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool, dx2=None):
+    """LayerNorm backward into dx (optionally accumulating); dx2 receives a second copy of the result
+    (the bf16 operand of the next linear backward)."""
     dg = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty(D, dtype=torch.float32, device=x.device)
     lib = L.load()
     ws = K.workspace(lib.mia_layernorm_partial_bytes(rows, D), x.device, "ln")
     L.check(lib.mia_layernorm_bwd(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x), g.data_ptr(),
                                   mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), L.dtype_code(dx), int(accumulate),
-                                  dg.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, D, L.stream_ptr()),
+                                  L.ptr(dx2), L.dtype_code(dx2) if dx2 is not None else 0, dg.data_ptr(),
+                                  db.data_ptr(), ws.data_ptr(), rows, D, L.stream_ptr()),
             "mia_layernorm_bwd")
     return dg, db
 
@@ -162,19 +165,26 @@ class ASTFunction(torch.autograd.Function):
         emit(4 + 12 * nb, 8 + 12 * nb)
         dx = torch.zeros(Tt, D, dtype=torch.float32, device=dev)
         dx.view(B, N, D)[:, 0] = dxc
+        # bf16 mode: a bf16 copy of the residual gradient feeds the next linear backward's GEMMs
+        dxb = K.cast(dx, torch.bfloat16) if cd == L.BF16 else dx
+        dxb2 = torch.empty_like(dxb) if cd == L.BF16 else None
         for i in reversed(range(nb)):
             sb = s["blocks"][i]
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = p[4 + 12 * i: 16 + 12 * i]
             wqkv, wproj, w1, w2 = s["wcast"][i]
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
-            dW2, db2_ = _linear_bwd(dx, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
+            dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
                                     tag="fc2")
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
             dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1")
-            dg2, dbt2 = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True)  # dx now = d(xm)
+            dg2, dbt2 = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2)  # dx = d(xm)
+            if dxb2 is not None:
+                dxb, dxb2 = dxb2, dxb
+            else:
+                dxb = dx
             da = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dWp, dbp = _linear_bwd(dx, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj")
+            dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj")
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
             delta = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
             with K.probe("attn.bwd", 10.0 * B * Hh * N * N * (D // Hh),
@@ -184,7 +194,11 @@ class ASTFunction(torch.autograd.Function):
                                               s["scale"], L.stream_ptr()), "mia_attn_bwd")
             dh = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")
-            dg1, dbt1 = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True)  # dx now = d(block input)
+            dg1, dbt1 = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2)  # d(block input)
+            if dxb2 is not None:
+                dxb, dxb2 = dxb2, dxb
+            else:
+                dxb = dx
             grads[4 + 12 * i: 16 + 12 * i] = [dg1, dbt1, dWq, dbq, dWp, dbp, dg2, dbt2, dW1, db1_, dW2, db2_]
             emit(4 + 12 * i, 16 + 12 * i)
             s["blocks"][i] = None

@@ -206,10 +206,12 @@ int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gamma, const f
                       int32_t D, float eps, mia_stream_t stream);
 /* dx (+= if accumulate) and partial sums for dgamma/dbeta (f32 [nblk][2][D] in partial,
  * reduced into dgamma/dbeta). */
+/* dx2 (optional, may be null): a second copy of the final dx in dx2dtype (the bf16 GEMM operand of
+ * the next linear's backward, saving a separate cast pass). */
 int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
                       const float* gamma, const float* mean, const float* rstd, void* dx,
-                      int32_t dxdtype, int32_t accumulate, float* dgamma, float* dbeta,
-                      void* partial, int64_t rows, int32_t D, mia_stream_t stream);
+                      int32_t dxdtype, int32_t accumulate, void* dx2, int32_t dx2dtype, float* dgamma,
+                      float* dbeta, void* partial, int64_t rows, int32_t D, mia_stream_t stream);
 int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
 
 /* Fused multi-head attention (timm Attention with F.scaled_dot_product_attention,
