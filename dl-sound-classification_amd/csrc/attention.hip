@@ -222,7 +222,7 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __re
 }
 
 // key on the lane: each wave owns 32 keys (128 per block); sweeps query tiles of 64.
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                             int N, int H, float scale, float scale_log2) {

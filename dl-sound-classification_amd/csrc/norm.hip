@@ -494,7 +494,7 @@ extern "C" int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t
 extern "C" int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, int64_t ld, float* out, void* partial,
                           mia_stream_t stream) {
   MIA_CHECK_ARG(x && out && partial && C > 0 && P > 0 && ld >= C, "colsum: bad arguments");
-  int nb = (int)std::min<int64_t>(P, 256);
+  int nb = (int)std::min<int64_t>(cdiv(P, 64), MIA_COLSUM_MAXBLK);  // workspace: MIA_COLSUM_MAXBLK * C floats
   hipStream_t s = as_stream(stream);
   const int es = dtype == MIA_BF16 ? 2 : 4;
   if (C % 8 == 0 && ld % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (int64_t)es * 8 >= 16) {

@@ -231,7 +231,7 @@ def pool_bwd_bn_relu_reduce(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn:
 
 def colsum(x, P, C, ld=None):
     out = torch.empty(C, dtype=torch.float32, device=x.device)
-    ws = workspace(256 * C * 4, x.device, "colsum")
+    ws = workspace(1024 * C * 4, x.device, "colsum")  # MIA_COLSUM_MAXBLK * C floats
     L.check(L.load().mia_colsum(x.data_ptr(), L.dtype_code(x), P, C, C if ld is None else ld, out.data_ptr(),
                                 ws.data_ptr(), _s()), "mia_colsum")
     return out

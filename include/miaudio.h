@@ -151,7 +151,9 @@ int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint
                                 void* dz, float* dgamma, float* dbeta, void* partial,
                                 mia_stream_t stream);
 
-/* Column sums over rows of a (P, C) matrix: bias gradients. out f32[C] (overwritten). */
+/* Column sums over rows of a (P, C) matrix: bias gradients. out f32[C] (overwritten).
+ * partial: MIA_COLSUM_MAXBLK * C floats of workspace. */
+#define MIA_COLSUM_MAXBLK 1024
 int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, int64_t ld, float* out,
                void* partial, mia_stream_t stream);
 
