@@ -92,7 +92,40 @@ def envnet_step_fn(model, opt, wav, labels, g, world, ddp):
     return step
 
 
-def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 3):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(model: str, ks: dict):
+    """HBM bytes per launch of the probed kernel from the committed rocprofv3 PMC summary of the same
+    bench command (profiles/<round>_pmc_<model>.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes).  The probed launch is matched to a kernel symbol by launches per
+    step and by its rocprof average duration (must agree with the live HIP-event time within 10 %)."""
+    files = sorted((REPO / "profiles").glob(f"r*_pmc_{model}.json"))
+    if not files:
+        return None, None
+    table = json.loads(files[-1].read_text())["kernels"]
+    best = None
+    for name, e in table.items():
+        if "hbm_bytes" not in e or e["launches_per_step"] != round(ks["launches_per_step"]):
+            continue
+        rel = abs(e["avg_ms"] - ks["ms"]) / ks["ms"]
+        if rel < 0.10 and (best is None or rel < best[0]):
+            best = (rel, name, e)
+    if best is None:
+        return None, {"file": files[-1].name, "match": None}
+    rel, name, e = best
+    return e["hbm_bytes"], {"file": files[-1].name, "kernel": name, "rocprof_avg_ms": e["avg_ms"],
+                            "live_vs_rocprof": round(rel, 4)}
+
+
+def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 10):
     """Oracle (CPU restatement of the reference path) timed on this host: fwd+loss+bwd+clip+Adam."""
     sys.path.insert(0, str(REPO))
     from oracle import envnet as oenv
@@ -125,7 +158,8 @@ def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 3):
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
             "sample": f"oracle EnvNet-v2 f32 train step (fwd+loss+bwd+clip+Adam), batch {batch}, "
-                      f"{steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work"}
+                      f"{steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work on {threads} threads "
+                      f"of {cpu_model()}"}
 
 
 def main():
@@ -194,8 +228,12 @@ def main():
         ks = kstats[dom]
         kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel"}.get(
             dom, "igemm_kernel")
+        traffic, tsrc = pmc_traffic(args.model, ks)
+        if tsrc and tsrc.get("kernel"):
+            kname = tsrc["kernel"].replace("_ZN12_GLOBAL__N_1", "").replace("(anonymous namespace)::", "").split("(")[0]
         roof = {"bound": "mfma", "kernel": f"{kname} [{dom}]", "achieved": round(ks["tflops"], 2),
-                "peak": peak_tf, "unit": "TFLOP/s", "frac": round(ks["tflops"] / peak_tf, 4), "traffic": None,
+                "peak": peak_tf, "unit": "TFLOP/s", "frac": round(ks["tflops"] / peak_tf, 4), "traffic": traffic,
+                "traffic_source": tsrc,
                 "algorithmic_per_launch": {"flop": ks["flop"], "bytes": ks["bytes"]},
                 "ms_per_launch": round(ks["ms"], 4)}
     step_tf = flop_per_clip * B / (ms * 1e-3) / 1e12

@@ -652,6 +652,49 @@ __global__ void splitk_reduce_kernel(const float* ws, int split, int64_t M, int6
 // owning BM/4 output pixels x all N channels.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// Loads are issued unconditionally (out-of-range chunks read the tensor base instead) and kept raw in
+// registers; zero padding, the producer's BN affine + ReLU and the bf16 pack are applied when the
+// chunk is written to LDS.  A per-load branch or a conversion right after the load would make hipcc
+// wait vmcnt(0) at the load and serialise the HBM latency with the MFMA work.
+struct RawChunk {
+  u32x4 a, b;  // 8 elements: bf16 in a; f32 in a (0..3) and b (4..7)
+};
+template <typename TS>
+__device__ __forceinline__ RawChunk load_raw(const TS* p) {
+  RawChunk r;
+  r.a = *reinterpret_cast<const u32x4*>(p);
+  if constexpr (sizeof(TS) == 4) r.b = *reinterpret_cast<const u32x4*>(p + 4);
+  else r.b = u32x4{0u, 0u, 0u, 0u};
+  return r;
+}
+template <typename TS, bool PRE>
+__device__ __forceinline__ u32x4 cook_raw(const RawChunk& r, bool ok, const float* sc, const float* sh, bool relu) {
+  if (!ok) return u32x4{0u, 0u, 0u, 0u};
+  if constexpr (sizeof(TS) == 2 && !PRE) return r.a;
+  float f[8];
+  if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(r.a[i] << 16); f[2 * i + 1] = __uint_as_float(r.a[i] & 0xffff0000u); }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[i] = __uint_as_float(r.a[i]); f[4 + i] = __uint_as_float(r.b[i]); }
+  }
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f[i] = fmaf(f[i], sc[i], sh[i]);
+      if (relu) f[i] = fmaxf(f[i], 0.f);
+    }
+  }
+  uint32_t w4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
+    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+  }
+  return u32x4{w4[0], w4[1], w4[2], w4[3]};
+}
+
 struct RowArgs {
   const char* x;
   int xdt, pre;
@@ -705,58 +748,25 @@ __global__ __launch_bounds__(NT) void rowconv_kernel(RowArgs g) {
     for (int i = 0; i < 8; ++i) { sc[i] = g.ps[cg * 8 + i]; sh[i] = g.pt[cg * 8 + i]; }
   }
 
-  u32x4 wreg[Cfg::WCH];
+  RawChunk wraw[Cfg::WCH];
+  uint32_t wok = 0;
   u32x4 breg[Cfg::BCH];
+  const bool relu = g.pre == MIA_PRE_AFFINE_RELU;
 
   auto load_window = [&](int ky) __attribute__((always_inline)) {
     const int iy = oy + ky - g.ph;
     const bool rowok = iy >= 0 && iy < g.h;
     const TS* xs = reinterpret_cast<const TS*>(g.x);
+    wok = 0;
 #pragma unroll
     for (int s = 0; s < Cfg::WCH; ++s) {
       const int q = t + NT * s;
       const int p = q / Cfg::CG;
       const int ix = px0 + p;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (p < Cfg::WPX && rowok && ix >= 0 && ix < g.w) {
-        const int64_t off = ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8;
-        float f[8];
-        if constexpr (sizeof(TS) == 2) {
-          const u32x4 u = *reinterpret_cast<const u32x4*>(xs + off);
-          if constexpr (!PRE) {
-            v = u;
-          } else {
-            const uint32_t w4[4] = {u[0], u[1], u[2], u[3]};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              f[2 * i] = __uint_as_float(w4[i] << 16);
-              f[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
-            }
-          }
-        } else {
-          const float4 a = reinterpret_cast<const float4*>(xs + off)[0];
-          const float4 c = reinterpret_cast<const float4*>(xs + off)[1];
-          f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
-        }
-        if constexpr (PRE || sizeof(TS) == 4) {
-          if constexpr (PRE) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              f[i] = fmaf(f[i], sc[i], sh[i]);
-              if (g.pre == MIA_PRE_AFFINE_RELU) f[i] = fmaxf(f[i], 0.f);
-            }
-          }
-          uint32_t w4[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
-                    ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
-          }
-          v = u32x4{w4[0], w4[1], w4[2], w4[3]};
-        }
-      }
-      wreg[s] = v;
+      const bool ok = p < Cfg::WPX && rowok && ix >= 0 && ix < g.w;
+      const int64_t off = ok ? ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8 : 0;
+      wraw[s] = load_raw<TS>(xs + off);
+      wok |= (uint32_t)ok << s;
     }
   };
   auto store_window = [&]() __attribute__((always_inline)) {
@@ -765,7 +775,8 @@ __global__ __launch_bounds__(NT) void rowconv_kernel(RowArgs g) {
       const int q = t + NT * s;
       const int p = q / Cfg::CG;
       if (p < Cfg::WPX)
-        *reinterpret_cast<u32x4*>(win + win_slot<S, Cfg::HALF>(p) * Cfg::PSB + cg * 16) = wreg[s];
+        *reinterpret_cast<u32x4*>(win + win_slot<S, Cfg::HALF>(p) * Cfg::PSB + cg * 16) =
+            cook_raw<TS, PRE>(wraw[s], (wok >> s) & 1u, sc, sh, relu);
     }
   };
   auto load_b = [&](int kt) __attribute__((always_inline)) {
@@ -881,7 +892,7 @@ struct RowWArgs {
   float* ws;
 };
 
-template <typename T, int NOUT, int S, int C, int KWMAX, int KYB, bool PRE>
+template <typename T, int NOUT, int S, int C, int KWMAX, int KYB, bool PRE, bool FULL = false>
 __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
   constexpr int BP = 128;
   constexpr int CG = C / 8;
@@ -903,7 +914,7 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ky0 = blockIdx.x * KYB, z = blockIdx.y;
-  const int NC = g.kw * C;                 // columns of this ky
+  const int NC = (FULL ? KWMAX : g.kw) * C;  // columns of this ky (FULL: kw == KWMAX, tile loop static)
   const int NCT = NC / 32;
   const int ntiles = MT * NCT;
   const int CPR = (g.ow + BP - 1) / BP;
@@ -916,81 +927,42 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
     for (int i = 0; i < 8; ++i) { sc[i] = g.ps[cg * 8 + i]; sh[i] = g.pt[cg * 8 + i]; }
   }
 
-  u32x4 wreg[KYB][WCH];
-  u32x4 dreg[DCH];
+  RawChunk wraw[KYB][WCH];
+  RawChunk draw[DCH];
+  uint32_t wok = 0, dok = 0;
+  const bool relu = g.pre == MIA_PRE_AFFINE_RELU;
 
-  auto pack8 = [&](const float* f) __attribute__((always_inline)) {
-    uint32_t w4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-      w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
-    }
-    return u32x4{w4[0], w4[1], w4[2], w4[3]};
-  };
-  auto load8f = [&](const T* p, float* f) __attribute__((always_inline)) {
-    if constexpr (ES == 2) {
-      const u32x4 u = *reinterpret_cast<const u32x4*>(p);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(u[i] << 16); f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u); }
-    } else {
-      const float4 a = reinterpret_cast<const float4*>(p)[0];
-      const float4 c = reinterpret_cast<const float4*>(p)[1];
-      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
-    }
-  };
   auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
     const int64_t row = c / CPR;
     const int x0 = (int)(c - row * CPR) * BP;
     const int b = (int)(row / g.oh), oy = (int)(row - (int64_t)b * g.oh);
-    const T* dys = reinterpret_cast<const T*>(g.dy) + ((int64_t)row * g.ow + x0) * NOUT;
+    const T* dys = reinterpret_cast<const T*>(g.dy);
+    const int64_t dbase = ((int64_t)row * g.ow + x0) * NOUT;
+    dok = 0;
 #pragma unroll
     for (int s = 0; s < DCH; ++s) {
       const int q = t + NT * s;
       const int p = q / (NOUT / 8), cc = q % (NOUT / 8);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (x0 + p < g.ow) {
-        if constexpr (ES == 2) {
-          v = *reinterpret_cast<const u32x4*>(dys + p * NOUT + cc * 8);
-        } else {
-          float f[8];
-          load8f(dys + p * NOUT + cc * 8, f);
-          v = pack8(f);
-        }
-      }
-      dreg[s] = v;
+      const bool ok = x0 + p < g.ow;
+      draw[s] = load_raw<T>(dys + (ok ? dbase + p * NOUT + cc * 8 : 0));
+      dok |= (uint32_t)ok << s;
     }
     const int px0 = x0 * S - g.pw;
     const T* xs = reinterpret_cast<const T*>(g.x);
+    wok = 0;
 #pragma unroll
     for (int kyi = 0; kyi < KYB; ++kyi) {
-    const int iy = oy + ky0 + kyi - g.ph;
-    const bool rowok = iy >= 0 && iy < g.h;
+      const int iy = oy + ky0 + kyi - g.ph;
+      const bool rowok = iy >= 0 && iy < g.h;
 #pragma unroll
-    for (int s = 0; s < WCH; ++s) {
-      const int q = t + NT * s;
-      const int p = q / CG;
-      const int ix = px0 + p;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (p < WPX && rowok && ix >= 0 && ix < g.w) {
-        const T* src = xs + ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8;
-        if constexpr (ES == 2 && !PRE) {
-          v = *reinterpret_cast<const u32x4*>(src);
-        } else {
-          float f[8];
-          load8f(src, f);
-          if constexpr (PRE) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              f[i] = fmaf(f[i], sc[i], sh[i]);
-              if (g.pre == MIA_PRE_AFFINE_RELU) f[i] = fmaxf(f[i], 0.f);
-            }
-          }
-          v = pack8(f);
-        }
+      for (int s = 0; s < WCH; ++s) {
+        const int q = t + NT * s;
+        const int p = q / CG;
+        const int ix = px0 + p;
+        const bool ok = p < WPX && rowok && ix >= 0 && ix < g.w;
+        wraw[kyi][s] = load_raw<T>(xs + (ok ? ((int64_t)(b * g.h + iy) * g.w + ix) * C + cg * 8 : 0));
+        wok |= (uint32_t)ok << (kyi * WCH + s);
       }
-      wreg[kyi][s] = v;
-    }
     }
   };
   auto store_chunk = [&]() __attribute__((always_inline)) {
@@ -998,7 +970,7 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
     for (int s = 0; s < DCH; ++s) {
       const int q = t + NT * s;
       const int p = q / (NOUT / 8), cc = q % (NOUT / 8);
-      *reinterpret_cast<u32x4*>(dyt + p * DSB + cc * 16) = dreg[s];
+      *reinterpret_cast<u32x4*>(dyt + p * DSB + cc * 16) = cook_raw<T, false>(draw[s], (dok >> s) & 1u, sc, sh, false);
     }
 #pragma unroll
     for (int kyi = 0; kyi < KYB; ++kyi)
@@ -1006,7 +978,9 @@ __global__ __launch_bounds__(NT) void rowwgrad_kernel(RowWArgs g) {
     for (int s = 0; s < WCH; ++s) {
       const int q = t + NT * s;
       const int p = q / CG;
-      if (p < WPX) *reinterpret_cast<u32x4*>(win + kyi * WBYTES + win_slot<S, HALF>(p) * PSB + cg * 16) = wreg[kyi][s];
+      if (p < WPX)
+        *reinterpret_cast<u32x4*>(win + kyi * WBYTES + win_slot<S, HALF>(p) * PSB + cg * 16) =
+            cook_raw<T, PRE>(wraw[kyi][s], (wok >> (kyi * WCH + s)) & 1u, sc, sh, relu);
     }
   };
 
@@ -1112,8 +1086,13 @@ bool rowwgrad_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N,
 template <typename T, int NOUT, int S, int C, int KWMAX, int KYB = 1>
 hipError_t rowwgrad_launch2(const RowWArgs& r, bool pre, hipStream_t s) {
   dim3 grid((unsigned)(r.kh / KYB), (unsigned)r.Z);
-  if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, true><<<grid, NT, 0, s>>>(r);
-  else rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, false><<<grid, NT, 0, s>>>(r);
+  if (r.kw == KWMAX) {
+    if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, true, true><<<grid, NT, 0, s>>>(r);
+    else rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, false, true><<<grid, NT, 0, s>>>(r);
+  } else {
+    if (pre) rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, true><<<grid, NT, 0, s>>>(r);
+    else rowwgrad_kernel<T, NOUT, S, C, KWMAX, KYB, false><<<grid, NT, 0, s>>>(r);
+  }
   return hipGetLastError();
 }
 

@@ -242,6 +242,18 @@ def col2im_rows(p, n, ph, w, kh, out):
             "mia_col2im_rows")
 
 
+def conv1ch_dgrad(dy: torch.Tensor, w: torch.Tensor, n: int, oh: int, ow: int, out: torch.Tensor,
+                  tag: str | None = None):
+    """dX of the 1-input-channel 8x8 conv (bf16): dy (n*oh*ow, 32) NHWC, w f32 (32, 1, 8, 8) -> out (n, oh+7, ow+7)."""
+    assert dy.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and w.dtype == torch.float32
+    assert dy.numel() == n * oh * ow * 32 and out.numel() == n * (oh + 7) * (ow + 7) and w.numel() == 32 * 64
+    assert dy.is_contiguous() and out.is_contiguous() and w.is_contiguous()
+    flop = 2.0 * n * oh * ow * 32 * 64
+    with probe(tag or "", flop, dy.numel() * 2 + out.numel() * 2):
+        L.check(L.load().mia_conv1ch_dgrad(dy.data_ptr(), w.data_ptr(), out.data_ptr(), n, oh, ow, _s()),
+                "mia_conv1ch_dgrad")
+
+
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:
     cout, cin, kh, kw = src.shape
     out = torch.empty(src.numel(), dtype=L.torch_dtype(dtype), device=src.device)

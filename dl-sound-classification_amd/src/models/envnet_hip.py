@@ -290,7 +290,11 @@ class EnvNetFunction(torch.autograd.Function):
             K.unpack_ohwi_grad(dWa, p[pa].shape, gwa)
             grads[pa] = gwa
             # dgrad a -> gradient of the block input (pooled map of the previous stage)
-            if cin == 1:
+            if cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32:
+                # 1-channel 8x8 conv: one sweep over dY rows, kernel row ky on the MFMA N side
+                dinp = torch.empty(B, H, W, dtype=tdt, device=dev)
+                K.conv1ch_dgrad(dya, p[pa], B, ha, wa, dinp, tag=f"t{blk}a.dgrad")
+            elif cin == 1:
                 # 1-channel 8x8 conv: P[b][r][iw][ky] = sum_{j,co} dya[b][r][iw+j-7][co] W[co][0][ky][7-j]
                 wr = K.pack_weight(p[pa], cd, 3)
                 Pm = torch.empty(B * ha * W, kh, dtype=torch.float32, device=dev)

@@ -162,6 +162,14 @@ int mia_colsum(const void* x, int32_t dtype, int64_t P, int32_t C, int64_t ld, f
 int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh, void* out,
                     int32_t dtype, mia_stream_t stream);
 
+/* Backward-data of the single-input-channel 8x8 conv, EnvNet-v2 trunk conv3
+ * (reference src/models/envnet_v2.py:31 Conv2d(1, 32, (8, 8)); replaces cuDNN conv2d backward-data):
+ *   dx[b][y][x] = sum_{ky,kx,co} dy[b][y-ky][x-kx][co] * w[co][0][ky][kx]
+ * dy bf16 NHWC (n, oh, ow, 32), w f32 OIHW (32, 1, 8, 8), dx bf16 (n, oh+7, ow+7);
+ * oh+7 <= 64, (ow+7) % 4 == 0, dy/dx 16-byte aligned.  Deterministic. */
+int mia_conv1ch_dgrad(const void* dy, const float* w, void* dx, int32_t n, int32_t oh, int32_t ow,
+                      mia_stream_t stream);
+
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
  * mode 0: OHWI (cout, kh, kw, cin)            — forward operand
  * mode 1: flipped dgrad operand (cin, kh, kw, cout) with ky->kh-1-ky, kx->kw-1-kx

@@ -30,11 +30,15 @@ def test_library_exports_every_declared_symbol():
     assert set(declared()) <= set(L.SIGNATURES), "ctypes signatures out of sync with the header"
 
 
-def test_library_is_gfx950():
+def test_library_is_gfx950(tmp_path):
+    import shutil
     import subprocess
     from src.miaudio import lib as L
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(L.LIB_PATH)],
-                         capture_output=True, text=True, cwd="/tmp").stdout
+    # --offloading extracts the device images next to its input: run it on a copy
+    lib = tmp_path / L.LIB_PATH.name
+    shutil.copy(L.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=str(tmp_path)).stdout
     if not out:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out

@@ -401,3 +401,18 @@ def test_dgemm_epilogues(cuda, act):
     else:
         ref = z + aux.double()
     assert rel(out.float().cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("n,oh,ow", [(2, 57, 853), (3, 10, 121), (1, 57, 129)])
+def test_conv1ch_dgrad_bf16(cuda, n, oh, ow):
+    """Single-input-channel 8x8 conv backward-data (EnvNet trunk conv3) vs float64 conv_transpose2d
+    of the same bf16-rounded operands."""
+    g = torch.Generator().manual_seed(oh * 1000 + ow)
+    dy = torch.randn(n, oh, ow, 32, generator=g).to(torch.bfloat16)
+    w = torch.randn(32, 1, 8, 8, generator=g) * 0.1
+    out = torch.empty(n, oh + 7, ow + 7, dtype=torch.bfloat16, device=cuda)
+    K.conv1ch_dgrad(dy.to(cuda).reshape(-1, 32), w.to(cuda), n, oh, ow, out)
+    torch.cuda.synchronize()
+    wb = w.to(torch.bfloat16).double()
+    ref = F.conv_transpose2d(dy.double().permute(0, 3, 1, 2), wb)[:, 0]
+    assert rel(out.float().cpu(), ref) < 1e-2

@@ -121,8 +121,10 @@ def _ddp_worker(rank, world, port, q):
     first = next(model.parameters())
     model._grad_ready([(first, first.grad.clone())])
     red.finish()
-    q.put((rank, {n: p.detach().clone() for n, p in model.named_parameters()},
-           {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}, x))
+    # numpy payloads: torch tensors would travel as shared-memory handles that vanish when the
+    # worker exits before the parent has read them
+    q.put((rank, {n: p.detach().numpy().copy() for n, p in model.named_parameters()},
+           {n: p.grad.numpy().copy() for n, p in model.named_parameters() if p.grad is not None}, x.numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -133,7 +135,11 @@ def test_grad_allreducer_gloo():
     procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (params, grads, x)) for r, params, grads, x in (q.get(timeout=60) for _ in range(world)))
+    res = {}
+    for _ in range(world):
+        r, params, grads, x = q.get(timeout=60)
+        res[r] = ({n: torch.from_numpy(v) for n, v in params.items()},
+                  {n: torch.from_numpy(v) for n, v in grads.items()}, torch.from_numpy(x))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
