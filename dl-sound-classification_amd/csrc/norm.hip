@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NT) void bn_relu_bwd_reduce_kernel(const void* __re
       s1[i] += g[i];
       s2[i] = fmaf(g[i], (xv[i] - mu[i]) * is[i], s2[i]);
     }
-    store8(dz, dtype, off, g);
+    if (dz) store8(dz, dtype, off, g);
   }
   block_channel_reduce(s1, s2, C, partial);
 }
@@ -136,6 +136,9 @@ __global__ void channel_partial_sum_kernel(const float* __restrict__ partial, in
   if (out_q1) out_q1[c] = (float)b;
 }
 
+// MASK: dz is the gradient of relu(bn(x)) and the ReLU mask is recomputed from x (scale/shift),
+// so the reduce pass never has to write the masked gradient out.
+template <bool MASK>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const void* __restrict__ dz, const void* __restrict__ x,
                                                           void* dx, int dtype, int64_t P, int C,
                                                           const float* __restrict__ gamma,
@@ -143,10 +146,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const void* __restrict
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ dgamma,
                                                           const float* __restrict__ dbeta,
-                                                          float* __restrict__ partial) {
+                                                          float* __restrict__ partial,
+                                                          const float* __restrict__ scale = nullptr,
+                                                          const float* __restrict__ shift = nullptr) {
   const int t = threadIdx.x;
   const int G = C / 8, cg = t % G, rs = t / G, rslots = NT / G;
-  float a[8], mu[8], is[8], mb[8], mg[8];
+  float a[8], mu[8], is[8], mb[8], mg[8], sc[8], sh[8];
+  if constexpr (MASK) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = scale[cg * 8 + i]; sh[i] = shift[cg * 8 + i]; }
+  }
   float s1[8] = {0}, s2[8] = {0};
   const float invP = 1.f / (float)P;
 #pragma unroll
@@ -165,6 +174,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const void* __restrict
     load8(x, dtype, off, xv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if constexpr (MASK) g[i] = fmaf(xv[i], sc[i], sh[i]) > 0.f ? g[i] : 0.f;
       g[i] = a[i] * (g[i] - mb[i] - (xv[i] - mu[i]) * is[i] * mg[i]);
       s1[i] += g[i];
     }
@@ -462,7 +472,7 @@ extern "C" int mia_bn_relu_bwd_reduce(const void* dact, void* dz, const void* x,
                                       const float* invstd, float* dgamma, float* dbeta, void* partial,
                                       mia_stream_t stream) {
   if (int r = check_bn(x, dtype, P, C)) return r;
-  MIA_CHECK_ARG(dact && dz && scale && shift && mean && invstd && dgamma && dbeta && partial,
+  MIA_CHECK_ARG(dact && scale && shift && mean && invstd && dgamma && dbeta && partial,
                 "bn_relu_bwd_reduce: null pointer");
   hipStream_t s = as_stream(stream);
   const int nb = nblocks_for(P, C);
@@ -481,9 +491,28 @@ extern "C" int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t
   MIA_CHECK_ARG(!dbias || partial, "bn_bwd_apply: dbias needs the partial workspace");
   const int nb = nblocks_for(P, C);
   hipStream_t s = as_stream(stream);
-  bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(dz, x, dx, dtype, P, C, gamma, mean, invstd, dgamma, dbeta,
-                                        dbias ? (float*)partial : nullptr);
+  bn_bwd_apply_kernel<false><<<nb, NT, 0, s>>>(dz, x, dx, dtype, P, C, gamma, mean, invstd, dgamma, dbeta,
+                                               dbias ? (float*)partial : nullptr);
   MIA_LAUNCH_CHECK("bn_bwd_apply");
+  if (dbias) {
+    channel_partial_sum_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, nullptr, dbias);
+    MIA_LAUNCH_CHECK("channel_partial_sum");
+  }
+  return 0;
+}
+
+extern "C" int mia_bn_relu_bwd_apply(const void* dact, const void* x, void* dx, int32_t dtype, int64_t P, int32_t C,
+                                     const float* gamma, const float* scale, const float* shift, const float* mean,
+                                     const float* invstd, const float* dgamma, const float* dbeta, float* dbias,
+                                     void* partial, mia_stream_t stream) {
+  if (int r = check_bn(x, dtype, P, C)) return r;
+  MIA_CHECK_ARG(dact && dx && scale && shift && mean && invstd && dgamma && dbeta, "bn_relu_bwd_apply: null pointer");
+  MIA_CHECK_ARG(!dbias || partial, "bn_relu_bwd_apply: dbias needs the partial workspace");
+  const int nb = nblocks_for(P, C);
+  hipStream_t s = as_stream(stream);
+  bn_bwd_apply_kernel<true><<<nb, NT, 0, s>>>(dact, x, dx, dtype, P, C, gamma, mean, invstd, dgamma, dbeta,
+                                              dbias ? (float*)partial : nullptr, scale, shift);
+  MIA_LAUNCH_CHECK("bn_relu_bwd_apply");
   if (dbias) {
     channel_partial_sum_kernel<<<(unsigned)C, 256, 0, s>>>((const float*)partial, nb, C, nullptr, dbias);
     MIA_LAUNCH_CHECK("channel_partial_sum");

@@ -141,13 +141,156 @@ __global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ d
   }
 }
 
+// Sparse BN reductions of the pooled backward: only the argmax position of each pooled cell carries
+// a gradient, so dbeta = sum g and dgamma = sum g * xhat are gathered per pooled cell (one thread =
+// one (pooled cell, 8-channel group)) without touching the other kh*kw - 1 pixels of the window.
+// gm[cell][c] (f32, NHWC cells) keeps the ReLU-masked gradient at the argmax for the dense pass.
+__global__ __launch_bounds__(NT) void pool_bwd_sparse_kernel(const void* __restrict__ dout, int layout,
+                                                             const uint8_t* __restrict__ argmax,
+                                                             const void* __restrict__ x, int dtype, int n, int H,
+                                                             int W, int C, int kh, int kw,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             float* __restrict__ gm,
+                                                             float* __restrict__ partial) {
+  const int OH = H / kh, OW = W / kw, G = C / 8;
+  const int t = threadIdx.x;
+  const int cg = t % G, rs = t / G, rslots = NT / G;
+  float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[cg * 8 + i]; sh[i] = shift[cg * 8 + i]; mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i];
+  }
+  float s1[8] = {0}, s2[8] = {0};
+  const int cells = n * OH * OW;
+  for (int cell = blockIdx.x * rslots + rs; cell < cells; cell += gridDim.x * rslots) {
+    const int ox = cell % OW;
+    const int q = cell / OW;
+    const int oy = q % OH;
+    const int b = q / OH;
+    const uint2 am = *reinterpret_cast<const uint2*>(argmax + (int64_t)cell * C + cg * 8);
+    float xv[8], dv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // all loads first, unconditionally
+      const uint32_t word = i < 4 ? am.x : am.y;
+      const int a = (int)((word >> (8 * (i & 3))) & 0xffu);
+      const int iy = oy * kh + a / kw, ix = ox * kw + a % kw;
+      xv[i] = ld_elem(x, dtype, (((int64_t)b * H + iy) * W + ix) * C + cg * 8 + i);
+      dv[i] = ld_elem(dout, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C));
+    }
+    float gv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float g = fmaf(xv[i], sc[i], sh[i]) > 0.f ? dv[i] : 0.f;
+      gv[i] = g;
+      s1[i] += g;
+      s2[i] = fmaf(g, (xv[i] - mu[i]) * is[i], s2[i]);
+    }
+    float4* gq = reinterpret_cast<float4*>(gm + (int64_t)cell * C + cg * 8);
+    gq[0] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    gq[1] = make_float4(gv[4], gv[5], gv[6], gv[7]);
+  }
+  __shared__ float red[NT * 16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[t * 16 + i] = s1[i]; red[t * 16 + 8 + i] = s2[i]; }
+  __syncthreads();
+  for (int e = t; e < 2 * C; e += NT) {
+    const int qq = e / C, c = e % C, g2 = c / 8, ci = c % 8;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < rslots; ++r2) acc += red[(r2 * G + g2) * 16 + qq * 8 + ci];
+    partial[((int64_t)blockIdx.x * C + c) * 2 + qq] = acc;
+  }
+}
+
+// Dense BN backward of a pooled layer in one pass: dx = gamma*invstd*(g - dbeta/P - xhat*dgamma/P)
+// with g = gm[cell] at the argmax position of the pixel's pooled cell, 0 elsewhere (gm already
+// carries the ReLU mask).  Reads x once, writes dx once; the masked dense gradient is never
+// materialised.  s1 partials = dbias.  All loads are unconditional (a conditional load makes hipcc
+// wait vmcnt(0) in the loop); four pixels per thread-iteration.
+constexpr int PB_UNROLL = 4;
+__global__ __launch_bounds__(NT) void pool_bn_bwd_apply_kernel(const float* __restrict__ gm,
+                                                               const uint8_t* __restrict__ argmax,
+                                                               const void* __restrict__ x, int dtype, int n, int H,
+                                                               int W, int C, int kh, int kw,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ dgamma,
+                                                               const float* __restrict__ dbeta, void* dx,
+                                                               float* __restrict__ partial) {
+  const int OH = H / kh, OW = W / kw, G = C / 8;
+  const int t = threadIdx.x;
+  const int cg = t % G, rs = t / G, rslots = NT / G;
+  const int P = n * H * W;
+  float mu[8], is[8], a[8], mb[8], mg[8];
+  const float invP = 1.f / (float)P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = cg * 8 + i;
+    mu[i] = mean[c]; is[i] = invstd[c];
+    a[i] = (gamma ? gamma[c] : 1.f) * is[i];
+    mb[i] = dbeta[c] * invP;
+    mg[i] = dgamma[c] * invP;
+  }
+  float s1[8] = {0};
+  const int stride = gridDim.x * rslots;
+  for (int r0 = blockIdx.x * rslots + rs; r0 < P; r0 += PB_UNROLL * stride) {
+    float xv[PB_UNROLL][8];
+    uint2 am[PB_UNROLL];
+    float4 g0[PB_UNROLL], g1[PB_UNROLL];
+#pragma unroll
+    for (int u = 0; u < PB_UNROLL; ++u) {
+      const int r = min(r0 + u * stride, P - 1);
+      load8(x, dtype, (int64_t)r * C + cg * 8, xv[u]);
+      const int ix = r % W, q = r / W, iy = q % H, b = q / H;
+      const int oy = min(iy / kh, OH - 1), ox = min(ix / kw, OW - 1);
+      const int64_t coff = (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8;
+      am[u] = *reinterpret_cast<const uint2*>(argmax + coff);
+      g0[u] = reinterpret_cast<const float4*>(gm + coff)[0];
+      g1[u] = reinterpret_cast<const float4*>(gm + coff)[1];
+    }
+#pragma unroll
+    for (int u = 0; u < PB_UNROLL; ++u) {
+      const int r = r0 + u * stride;
+      if (r >= P) break;
+      const int ix = r % W, q = r / W, iy = q % H;
+      const int oy = iy / kh, ox = ix / kw;
+      const int pos = oy < OH && ox < OW ? (iy - oy * kh) * kw + (ix - ox * kw) : -1;
+      const float gv[8] = {g0[u].x, g0[u].y, g0[u].z, g0[u].w, g1[u].x, g1[u].y, g1[u].z, g1[u].w};
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t word = i < 4 ? am[u].x : am[u].y;
+        const int av = (int)((word >> (8 * (i & 3))) & 0xffu);
+        const float gi = av == pos ? gv[i] : 0.f;
+        g[i] = a[i] * (gi - mb[i] - (xv[u][i] - mu[i]) * is[i] * mg[i]);
+        s1[i] += g[i];
+      }
+      store8(dx, dtype, (int64_t)r * C + cg * 8, g);
+    }
+  }
+  if (!partial) return;
+  __shared__ float red[NT * 8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[t * 8 + i] = s1[i];
+  __syncthreads();
+  for (int c = t; c < C; c += NT) {
+    const int g2 = c / 8, ci = c % 8;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < rslots; ++r2) acc += red[(r2 * G + g2) * 8 + ci];
+    partial[((int64_t)blockIdx.x * C + c) * 2] = acc;
+  }
+}
+
 __global__ void partial_final_kernel(const float* __restrict__ partial, int nblk, int C, float* dgamma, float* dbeta) {
   const int c = blockIdx.x;  // one block per channel
   const double a = block_sum_strided(partial + (int64_t)c * 2, nblk, (int64_t)C * 2);
   const double b = block_sum_strided(partial + (int64_t)c * 2 + 1, nblk, (int64_t)C * 2);
   if (threadIdx.x != 0) return;
-  dbeta[c] = (float)a;
-  dgamma[c] = (float)b;
+  if (dbeta) dbeta[c] = (float)a;
+  if (dgamma) dgamma[c] = (float)b;
 }
 
 // out[b][ih][iw] = sum_ky p[b][ih-ky][iw][ky]
@@ -195,13 +338,59 @@ extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout,
   MIA_CHECK_ARG((int64_t)n * h * w < (1ll << 31), "pool_bwd: too many pixels for 32-bit indexing");
   const int rslots = NT / (c / 8);
   const int64_t P = (int64_t)n * h * w;
-  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
   hipStream_t s = as_stream(stream);
-  pool_bwd_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean, invstd,
-                                    dz, (float*)partial);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
+  pool_bwd_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean,
+                                    invstd, dz, (float*)partial);
   MIA_LAUNCH_CHECK("pool_bwd");
   partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);
   MIA_LAUNCH_CHECK("pool_bwd_final");
+  return 0;
+}
+
+extern "C" int mia_pool_bwd_gather(const void* dout, int32_t out_layout, const uint8_t* argmax, const void* x,
+                                   int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                                   const float* scale, const float* shift, const float* mean, const float* invstd,
+                                   float* gm, float* dgamma, float* dbeta, void* partial, mia_stream_t stream) {
+  MIA_CHECK_ARG(dout && argmax && x && scale && shift && mean && invstd && gm && dgamma && dbeta && partial,
+                "pool_bwd_gather: null pointer");
+  MIA_CHECK_ARG(c % 8 == 0 && c >= 8 && (NT % (c / 8)) == 0, "pool_bwd_gather: channels");
+  MIA_CHECK_ARG((int64_t)n * h * w < (1ll << 31), "pool_bwd_gather: too many pixels for 32-bit indexing");
+  MIA_CHECK_ARG(h >= kh && w >= kw && kh * kw <= 256 && (reinterpret_cast<uintptr_t>(gm) & 15) == 0,
+                "pool_bwd_gather: bad geometry / alignment");
+  const int rslots = NT / (c / 8);
+  const int64_t cells = (int64_t)n * (h / kh) * (w / kw);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(cells, (int64_t)rslots * 2), 1024));
+  hipStream_t s = as_stream(stream);
+  pool_bwd_sparse_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean,
+                                           invstd, gm, (float*)partial);
+  MIA_LAUNCH_CHECK("pool_bwd_gather");
+  partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);
+  MIA_LAUNCH_CHECK("pool_bwd_gather_final");
+  return 0;
+}
+
+extern "C" int mia_pool_bn_relu_bwd_apply(const float* gm, const uint8_t* argmax, const void* x, int32_t dtype,
+                                          int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                                          const float* gamma, const float* mean, const float* invstd,
+                                          const float* dgamma, const float* dbeta, void* dx, float* dbias,
+                                          void* partial, mia_stream_t stream) {
+  MIA_CHECK_ARG(gm && argmax && x && mean && invstd && dgamma && dbeta && dx, "pool_bn_bwd_apply: null pointer");
+  MIA_CHECK_ARG(!dbias || partial, "pool_bn_bwd_apply: dbias needs the partial workspace");
+  MIA_CHECK_ARG(c % 8 == 0 && c >= 8 && (NT % (c / 8)) == 0, "pool_bn_bwd_apply: channels");
+  MIA_CHECK_ARG((int64_t)n * h * w < (1ll << 31), "pool_bn_bwd_apply: too many pixels for 32-bit indexing");
+  MIA_CHECK_ARG(h >= kh && w >= kw && kh * kw <= 256, "pool_bn_bwd_apply: bad geometry");
+  const int rslots = NT / (c / 8);
+  const int64_t P = (int64_t)n * h * w;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
+  hipStream_t s = as_stream(stream);
+  pool_bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(gm, argmax, x, dtype, n, h, w, c, kh, kw, gamma, mean, invstd, dgamma,
+                                             dbeta, dx, dbias ? (float*)partial : nullptr);
+  MIA_LAUNCH_CHECK("pool_bn_bwd_apply");
+  if (dbias) {
+    partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, nullptr, dbias);
+    MIA_LAUNCH_CHECK("pool_bn_bwd_apply_final");
+  }
   return 0;
 }
 

@@ -192,11 +192,13 @@ def bn_fwd_stats(x: torch.Tensor, P: int, C: int, gamma, beta, running_mean, run
 
 
 def bn_relu_bwd_reduce(dact, dz, x, P, C, bn: BNState):
+    """ReLU+BN backward reductions (dgamma, dbeta); dz=None: the masked gradient is not written
+    (bn_relu_bwd_apply recomputes the mask)."""
     dev = x.device
     g = torch.empty(2, C, dtype=torch.float32, device=dev)
     lib = L.load()
     ws = workspace(lib.mia_bn_partial_bytes(P, C), dev, "bn")
-    L.check(lib.mia_bn_relu_bwd_reduce(dact.data_ptr(), dz.data_ptr(), x.data_ptr(), L.dtype_code(x), P, C,
+    L.check(lib.mia_bn_relu_bwd_reduce(dact.data_ptr(), L.ptr(dz), x.data_ptr(), L.dtype_code(x), P, C,
                                        bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
                                        bn.invstd.data_ptr(), g[0].data_ptr(), g[1].data_ptr(), ws.data_ptr(),
                                        _s()), "mia_bn_relu_bwd_reduce")
@@ -209,6 +211,41 @@ def bn_bwd_apply(dz, x, dx, P, C, gamma, bn: BNState, dgamma, dbeta, dbias=None)
     L.check(lib.mia_bn_bwd_apply(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), L.dtype_code(x), P, C,
                                  L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(), dgamma.data_ptr(),
                                  dbeta.data_ptr(), L.ptr(dbias), ws.data_ptr(), _s()), "mia_bn_bwd_apply")
+
+
+def bn_relu_bwd_apply(dact, x, dx, P, C, gamma, bn: BNState, dgamma, dbeta, dbias=None):
+    """dx = BN backward of relu(bn(x)) with the ReLU mask recomputed from x (one pass)."""
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(P, C), x.device, "bn")
+    L.check(lib.mia_bn_relu_bwd_apply(dact.data_ptr(), x.data_ptr(), dx.data_ptr(), L.dtype_code(x), P, C,
+                                      L.ptr(gamma), bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
+                                      bn.invstd.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), L.ptr(dbias),
+                                      ws.data_ptr(), _s()), "mia_bn_relu_bwd_apply")
+
+
+def pool_bwd_gather(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn: BNState):
+    """Sparse half of the pooled backward: (gm, dgamma, dbeta); gm = ReLU-masked gradient at each
+    pooled cell's argmax, f32 (n, h//kh, w//kw, c)."""
+    dev = x.device
+    g = torch.empty(2, c, dtype=torch.float32, device=dev)
+    gm = torch.empty(n * (h // kh) * (w // kw), c, dtype=torch.float32, device=dev)
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(n * h * w, c), dev, "bn")
+    L.check(lib.mia_pool_bwd_gather(dout.data_ptr(), out_layout, argmax.data_ptr(), x.data_ptr(), L.dtype_code(x),
+                                    n, h, w, c, kh, kw, bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
+                                    bn.invstd.data_ptr(), gm.data_ptr(), g[0].data_ptr(), g[1].data_ptr(),
+                                    ws.data_ptr(), _s()), "mia_pool_bwd_gather")
+    return gm, g[0], g[1]
+
+
+def pool_bn_relu_bwd_apply(gm, argmax, x, n, h, w, c, kh, kw, gamma, bn: BNState, dgamma, dbeta, dx, dbias=None):
+    """Dense half: BN backward of the pooled layer, g taken from gm at the argmax (one pass x -> dx)."""
+    lib = L.load()
+    ws = workspace(lib.mia_bn_partial_bytes(n * h * w, c), x.device, "bn")
+    L.check(lib.mia_pool_bn_relu_bwd_apply(gm.data_ptr(), argmax.data_ptr(), x.data_ptr(), L.dtype_code(x), n, h, w,
+                                           c, kh, kw, L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                           dgamma.data_ptr(), dbeta.data_ptr(), dx.data_ptr(), L.ptr(dbias),
+                                           ws.data_ptr(), _s()), "mia_pool_bn_relu_bwd_apply")
 
 
 def pool_fwd(x, n, h, w, c, kh, kw, bn: BNState, out, out_layout, argmax):

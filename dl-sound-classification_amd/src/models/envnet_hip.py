@@ -247,13 +247,14 @@ class EnvNetFunction(torch.autograd.Function):
             pa = 8 + 8 * blk
             ph, pw = TRUNK_POOL[blk]
             Pb = B * hb * wb
-            dzb = torch.empty(Pb, cout2, dtype=tdt, device=dev)
-            dgb, dbb = K.pool_bwd_bn_relu_reduce(dpool, 2 if blk == 3 else 0, ts["am"], ts["yb"], B, hb, wb, cout2,
-                                                 ph, pw, ts["bnb"], dzb)
+            lay = 2 if blk == 3 else 0
+            # reductions gathered at the argmax positions, then one dense pass x -> dy
+            gm, dgb, dbb = K.pool_bwd_gather(dpool, lay, ts["am"], ts["yb"], B, hb, wb, cout2, ph, pw, ts["bnb"])
             grads[pa + 6], grads[pa + 7] = dgb, dbb
-            dyb = dzb  # in place: dy overwrites dz
+            dyb = torch.empty(Pb, cout2, dtype=tdt, device=dev)
             dbias_b = torch.empty(cout2, dtype=torch.float32, device=dev)
-            K.bn_bwd_apply(dzb, ts["yb"], dyb, Pb, cout2, bns[3 + 2 * blk].weight, ts["bnb"], dgb, dbb, dbias_b)
+            K.pool_bn_relu_bwd_apply(gm, ts["am"], ts["yb"], B, hb, wb, cout2, ph, pw, bns[3 + 2 * blk].weight,
+                                     ts["bnb"], dgb, dbb, dyb, dbias_b)
             grads[pa + 5] = dbias_b
             # wgrad b: dW[co][(ky,kx,ci)] = sum_pix dyb[pix][co] * relu(bn_a(ya))[pix + tap][ci]
             Kb = kh2 * kw2 * cin2
@@ -272,10 +273,10 @@ class EnvNetFunction(torch.autograd.Function):
             Kdb = kh2 * kw2 * cout2
             K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
                    K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd, tag=f"t{blk}b.dgrad")
-            dga, dba = K.bn_relu_bwd_reduce(da, da, ts["ya"], Pa, cout, ts["bna"])
+            dga, dba = K.bn_relu_bwd_reduce(da, None, ts["ya"], Pa, cout, ts["bna"])
             grads[pa + 2], grads[pa + 3] = dga, dba
             dbias_a = torch.empty(cout, dtype=torch.float32, device=dev)
-            K.bn_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba, dbias_a)
+            K.bn_relu_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba, dbias_a)
             grads[pa + 1] = dbias_a
             dya = da
             # wgrad a
@@ -316,13 +317,13 @@ class EnvNetFunction(torch.autograd.Function):
         # ---- frontend backward
         W1, W2, Wp = g["W1"], g["W2"], g["Wp"]
         P2, P1 = B * W2, B * W1
-        dz2 = torch.empty(P2, 64, dtype=tdt, device=dev)
-        dg2, db2 = K.pool_bwd_bn_relu_reduce(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"], dz2)
+        gm, dg2, db2 = K.pool_bwd_gather(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"])
         grads[6], grads[7] = dg2, db2
+        dy2 = torch.empty(P2, 64, dtype=tdt, device=dev)
         dbias2 = torch.empty(64, dtype=torch.float32, device=dev)
-        K.bn_bwd_apply(dz2, s["y2"], dz2, P2, 64, bns[1].weight, s["bn2"], dg2, db2, dbias2)
+        K.pool_bn_relu_bwd_apply(gm, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, bns[1].weight, s["bn2"], dg2, db2, dy2,
+                                 dbias2)
         grads[5] = dbias2
-        dy2 = dz2
         dW2 = torch.empty(64, 512, dtype=torch.float32, device=dev)
         K.gemm(K.dense(dy2, L.RC, P2, 64),
                K.conv(s["y1"], L.RC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU,
@@ -339,10 +340,10 @@ class EnvNetFunction(torch.autograd.Function):
             K.gemm(K.conv(dy2, L.KC, B, 1, W2, 64, 1, Tp, 1, 8, pw=7),
                    K.dense(wpar[par], L.KC, 32, 512),
                    K.epilogue(da1, 32, rowmap=(Tp, W1, 2, par)), B * Tp, 32, 512, cd, tag="conv2.dgrad")
-        dg1, db1 = K.bn_relu_bwd_reduce(da1, da1, s["y1"], P1, 32, s["bn1"])
+        dg1, db1 = K.bn_relu_bwd_reduce(da1, None, s["y1"], P1, 32, s["bn1"])
         grads[2], grads[3] = dg1, db1
         dbias1 = torch.empty(32, dtype=torch.float32, device=dev)
-        K.bn_bwd_apply(da1, s["y1"], da1, P1, 32, bns[0].weight, s["bn1"], dg1, db1, dbias1)
+        K.bn_relu_bwd_apply(da1, s["y1"], da1, P1, 32, bns[0].weight, s["bn1"], dg1, db1, dbias1)
         grads[1] = dbias1
         dW1 = torch.empty(32, 64, dtype=torch.float32, device=dev)
         T = g["T"]

@@ -122,8 +122,9 @@ int mia_bn_fwd_stats(const void* x, int32_t dtype, int64_t P, int32_t C, const f
                      const float* beta, float* running_mean, float* running_var, float momentum,
                      float eps, int32_t training, float* mean, float* invstd, float* scale,
                      float* shift, void* partial, mia_stream_t stream);
-/* ReLU + BN backward reductions: dz = dact * (scale*x+shift > 0) (in place allowed),
- * dgamma = sum dz*xhat, dbeta = sum dz (written, not accumulated). */
+/* ReLU + BN backward reductions: dz = dact * (scale*x+shift > 0) (in place allowed; dz may be
+ * NULL when mia_bn_relu_bwd_apply recomputes the mask), dgamma = sum dz*xhat, dbeta = sum dz
+ * (written, not accumulated).  Replaces autograd of nn.ReLU + nn.BatchNorm2d (envnet_v2.py:16-17). */
 int mia_bn_relu_bwd_reduce(const void* dact, void* dz, const void* x, int32_t dtype, int64_t P,
                            int32_t C, const float* scale, const float* shift, const float* mean,
                            const float* invstd, float* dgamma, float* dbeta, void* partial,
@@ -134,6 +135,12 @@ int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t dtype, int
                      const float* gamma, const float* mean, const float* invstd,
                      const float* dgamma, const float* dbeta, float* dbias, void* partial,
                      mia_stream_t stream);
+/* mia_bn_bwd_apply with the ReLU mask recomputed from x: dz = dact * (scale*x+shift > 0) is never
+ * materialised (dact = gradient of relu(bn(x))). */
+int mia_bn_relu_bwd_apply(const void* dact, const void* x, void* dx, int32_t dtype, int64_t P, int32_t C,
+                          const float* gamma, const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* dgamma, const float* dbeta, float* dbias,
+                          void* partial, mia_stream_t stream);
 
 /* Max-pool of relu(scale*x+shift) — nn.MaxPool2d (envnet_v2.py:23,37) fused with the
  * preceding BN+ReLU.  x: (n, h, w, c) NHWC; window (kh,kw) == stride, floor mode.
@@ -143,13 +150,30 @@ int mia_bn_bwd_apply(const void* dz, const void* x, void* dx, int32_t dtype, int
 int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c,
                  int32_t kh, int32_t kw, const float* scale, const float* shift, void* out,
                  int32_t out_layout, uint8_t* argmax, mia_stream_t stream);
-/* Backward of pool(relu(bn(x))) up to dz (the BN output grad) + BN reductions. */
+/* Backward of pool(relu(bn(x))) up to dz (the BN output grad) + BN reductions
+ * (nn.MaxPool2d after BN+ReLU, envnet_v2.py:16-23,32-37). */
 int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint8_t* argmax,
                                 const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w,
                                 int32_t c, int32_t kh, int32_t kw, const float* scale,
                                 const float* shift, const float* mean, const float* invstd,
                                 void* dz, float* dgamma, float* dbeta, void* partial,
                                 mia_stream_t stream);
+/* Pooled backward, sparse half: at the argmax position of every pooled cell,
+ * gm[cell][c] = dout[cell][c] * (scale*x+shift > 0) (f32, NHWC cells (n, h/kh, w/kw, c)), and the BN
+ * reductions dgamma = sum gm*xhat, dbeta = sum gm (the other kh*kw-1 window pixels carry no
+ * gradient and are never read).  Replaces autograd of nn.MaxPool2d + nn.ReLU (envnet_v2.py:16-23). */
+int mia_pool_bwd_gather(const void* dout, int32_t out_layout, const uint8_t* argmax, const void* x,
+                        int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                        const float* scale, const float* shift, const float* mean, const float* invstd,
+                        float* gm, float* dgamma, float* dbeta, void* partial, mia_stream_t stream);
+/* Pooled backward, dense half (one read of x, one write of dx): BN backward
+ * dx = gamma*invstd*(g - dbeta/P - xhat*dgamma/P), g = gm[cell] at the argmax position, else 0;
+ * optional dbias[c] = sum_rows dx (nn.BatchNorm2d backward, envnet_v2.py:16,33). */
+int mia_pool_bn_relu_bwd_apply(const float* gm, const uint8_t* argmax, const void* x, int32_t dtype,
+                               int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                               const float* gamma, const float* mean, const float* invstd,
+                               const float* dgamma, const float* dbeta, void* dx, float* dbias,
+                               void* partial, mia_stream_t stream);
 
 /* Column sums over rows of a (P, C) matrix: bias gradients. out f32[C] (overwritten).
  * partial: MIA_COLSUM_MAXBLK * C floats of workspace. */

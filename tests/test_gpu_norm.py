@@ -79,3 +79,40 @@ def test_pool_fwd_bwd(cuda, geom):
     gz = (a.grad * zmask).permute(0, 2, 3, 1)
     assert rel(dz, gz) < 1e-6
     assert rel(db, gz.sum(dim=(0, 1, 2))) < 1e-5
+    # sparse reductions (dz=None) agree with the dense pass; the fused apply equals the two-pass one
+    gm, dg2, db2 = K.pool_bwd_gather(dout.to(cuda), layout, am, ty, n, h, w, c, kh, kw, st)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(cuda)
+    dx_ref = torch.empty_like(ty)
+    K.bn_bwd_apply(dz, ty, dx_ref, n * h * w, c, gamma, st, dg, db)
+    dx = torch.empty_like(ty)
+    dbias = torch.empty(c, device=cuda)
+    K.pool_bn_relu_bwd_apply(gm, am, ty, n, h, w, c, kh, kw, gamma, st, dg2, db2, dx, dbias)
+    torch.cuda.synchronize()
+    assert rel(dg2, dg) < 1e-5 and rel(db2, db) < 1e-5
+    assert rel(dx, dx_ref) < 1e-5
+    assert rel(dbias, dx_ref.double().sum(dim=(0, 1, 2))) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_relu_bwd_masked_apply(cuda, dt):
+    """bn_relu_bwd_apply (mask recomputed from x) == reduce-with-dz + bn_bwd_apply."""
+    g = torch.Generator().manual_seed(3)
+    P, C = 5000, 64
+    y = torch.randn(P, C, generator=g).to(dt).to(cuda)
+    dact = torch.randn(P, C, generator=g).to(dt).to(cuda)
+    st = K.BNState(torch.randn(C, generator=g).to(cuda) * 0.1, (torch.rand(C, generator=g) + 0.5).to(cuda),
+                   (torch.rand(C, generator=g) + 0.5).to(cuda), (torch.randn(C, generator=g) * 0.3).to(cuda))
+    gamma = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    dz = torch.empty_like(dact)
+    dg, db = K.bn_relu_bwd_reduce(dact, dz, y, P, C, st)
+    dg2, db2 = K.bn_relu_bwd_reduce(dact, None, y, P, C, st)
+    dx_ref = torch.empty_like(dact)
+    K.bn_bwd_apply(dz, y, dx_ref, P, C, gamma, st, dg, db)
+    dx = torch.empty_like(dact)
+    dbias = torch.empty(C, device=cuda)
+    K.bn_relu_bwd_apply(dact, y, dx, P, C, gamma, st, dg2, db2, dbias)
+    torch.cuda.synchronize()
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    assert torch.equal(dx, dx_ref)
+    # dbias sums the f32 values before the store rounds them (bf16: compare against the rounded sum loosely)
+    assert rel(dbias, dx_ref.double().sum(0)) < (1e-4 if dt == torch.float32 else 2e-2)
