@@ -16,9 +16,11 @@
 //  * 256 threads = 4 waves, each owning (BM/WM) x (BN/WN) of 32x32 accumulator tiles;
 //    register-staged double-buffered K loop (BK = 32), one barrier per K tile.
 //  * split-K writes f32 partial slabs; a reduce kernel applies the epilogue.
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
+
+using namespace mgemm;
 
 constexpr int BK = 32;
 constexpr int NT = 256;
@@ -33,15 +35,7 @@ struct OpDev {
   const float* pt;
 };
 
-struct EpiDev {
-  char* ptr;
-  int dtype, act, accumulate, aux_dtype;
-  int64_t ldc, rm_inner, rm_outer, rm_istride, rm_offset;
-  const float* bias;
-  const char* aux;
-  int64_t ldaux;
-  float alpha, act_scale;
-};
+
 
 struct GemmArgs {
   OpDev a, b;
@@ -392,135 +386,6 @@ __device__ __forceinline__ void mma(f32x16& acc, const Frag<bf16>& a, const Frag
 __device__ __forceinline__ void mma(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x[t], b.x[t], acc, 0, 0, 0);
-}
-
-// -------------------------------------------------------------------------- epilogue
-__device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int64_t n, float acc) {
-  float v = acc * e.alpha;
-  if (e.bias) v += e.bias[n];
-  switch (e.act) {
-    case MIA_ACT_RELU: v = fmaxf(v, 0.f); break;
-    case MIA_ACT_GELU: v = gelu_erf(v); break;
-    case MIA_DACT_NZ: {
-      const float a = ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n);
-      v = a != 0.f ? v * e.act_scale : 0.f;
-      break;
-    }
-    case MIA_DACT_GELU: v *= gelu_erf_grad(ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n)); break;
-    case MIA_ACT_ADD_AUX: v += ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n); break;
-    case MIA_ACT_GELU_SAVE:
-      st_elem(const_cast<char*>(e.aux), e.aux_dtype, m * e.ldaux + n, v);
-      v = gelu_erf(v);
-      break;
-    default: break;
-  }
-  int64_t prow = m;
-  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
-  const int64_t idx = prow * e.ldc + n;
-  if (e.accumulate) v += ld_elem(e.ptr, e.dtype, idx);
-  st_elem(e.ptr, e.dtype, idx, v);
-}
-
-__device__ __forceinline__ void ld16(const void* p, int dtype, int64_t idx, float* f) {
-  if (dtype == MIA_BF16) {
-    const uint4* q = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + idx);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint4 u = q[h];
-      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f[8 * h + 2 * i] = __uint_as_float(w[i] << 16);
-        f[8 * h + 2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-      }
-    }
-  } else {
-    const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const float4 u = q[h];
-      f[4 * h] = u.x; f[4 * h + 1] = u.y; f[4 * h + 2] = u.z; f[4 * h + 3] = u.w;
-    }
-  }
-}
-
-__device__ __forceinline__ void st16(void* p, int dtype, int64_t idx, const float* o) {
-  if (dtype == MIA_BF16) {
-    uint32_t w[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const bf16 lo = (bf16)o[2 * c], hi = (bf16)o[2 * c + 1];
-      w[c] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
-    }
-    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx);
-    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  } else {
-    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-  }
-}
-
-// 16 contiguous outputs (m, n0..n0+15) of one row.  Fast path (no accumulate, 16-B aligned output
-// and aux rows): bias as float4, aux read/written with 16-B accesses, 16-B stores.  Otherwise per
-// element.
-__device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t n0, int64_t N, const float* v) {
-  int64_t prow = m;
-  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
-  const int64_t idx = prow * e.ldc + n0;
-  const bool uses_aux = e.act == MIA_DACT_NZ || e.act == MIA_DACT_GELU || e.act == MIA_ACT_ADD_AUX ||
-                        e.act == MIA_ACT_GELU_SAVE;
-  const int64_t aidx = m * e.ldaux + n0;
-  const bool fast = n0 + 16 <= N && !e.accumulate &&
-                    ((idx * (e.dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
-                    ((reinterpret_cast<uintptr_t>(e.ptr)) & 15) == 0 &&
-                    (!uses_aux || (((aidx * (e.aux_dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
-                                   ((reinterpret_cast<uintptr_t>(e.aux)) & 15) == 0));
-  if (!fast) {
-    for (int c = 0; c < 16; ++c)
-      if (n0 + c < N) epi_store(e, m, n0 + c, v[c]);
-    return;
-  }
-  float o[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) o[c] = v[c] * e.alpha;
-  if (e.bias) {
-    const float4* b4 = reinterpret_cast<const float4*>(e.bias + n0);
-    const bool ba = ((reinterpret_cast<uintptr_t>(e.bias + n0)) & 15) == 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 bb;
-      if (ba) bb = b4[q];
-      else bb = make_float4(e.bias[n0 + 4 * q], e.bias[n0 + 4 * q + 1], e.bias[n0 + 4 * q + 2], e.bias[n0 + 4 * q + 3]);
-      o[4 * q] += bb.x; o[4 * q + 1] += bb.y; o[4 * q + 2] += bb.z; o[4 * q + 3] += bb.w;
-    }
-  }
-  if (e.act == MIA_ACT_RELU) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) o[c] = fmaxf(o[c], 0.f);
-  } else if (e.act == MIA_ACT_GELU) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
-  } else if (e.act == MIA_ACT_GELU_SAVE) {
-    st16(const_cast<char*>(e.aux), e.aux_dtype, aidx, o);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
-  } else if (uses_aux) {
-    float a[16];
-    ld16(e.aux, e.aux_dtype, aidx, a);
-    if (e.act == MIA_DACT_NZ) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) o[c] = a[c] != 0.f ? o[c] * e.act_scale : 0.f;
-    } else if (e.act == MIA_DACT_GELU) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) o[c] *= gelu_erf_grad(a[c]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) o[c] += a[c];
-    }
-  }
-  st16(e.ptr, e.dtype, idx, o);
 }
 
 template <typename T, int BM, int BN, int WM, int LA, int LB>
@@ -1451,14 +1316,7 @@ bool tapconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, 
 // chunks by (row & 7) (conflict-free ds_read_b128 per 8 lanes); RC rows of 256 B permute their
 // 32-B blocks by (k & 3) (conflict-free ds_read_b64_tr_b16 per 16 lanes).  Blocks are remapped so
 // that neighbouring tiles share an XCD (bijective XCD swizzle) and walk M fastest (B-tile reuse).
-struct DArgs {
-  const bf16* a;
-  const bf16* b;
-  int64_t lda, ldb, M, N, K, kper;
-  int split, nbm, nbn;
-  float* ws;
-  EpiDev e;
-};
+
 
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
@@ -1815,7 +1673,8 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     hipStream_t s = as_stream(stream);
     hipError_t err;
     const int la = A->layout, lb = B->layout;
-    if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
+    if (dgemm256_pays(M, N, d.split)) err = dgemm256_launch(d, la, lb, s);
+    else if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
     else if (la == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_RC>(d, s);
     else if (lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_KC>(d, s);
     else err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC>(d, s);

@@ -181,6 +181,7 @@ __global__ __launch_bounds__(NF_NT) void norm_final_kernel(double* ws, int ntens
 
 __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ params, void* const* __restrict__ grads,
                                                   void* const* __restrict__ m1, void* const* __restrict__ m2,
+                                                  void* const* __restrict__ shadow,
                                                   const int64_t* __restrict__ sizes, const float* __restrict__ coef_p,
                                                   float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps,
                                                   float wd) {
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
   const float* g = reinterpret_cast<const float*>(grads[tsr]);
   float* m = reinterpret_cast<float*>(m1[tsr]);
   float* v = reinterpret_cast<float*>(m2[tsr]);
+  bf16* sw = shadow ? reinterpret_cast<bf16*>(shadow[tsr]) : nullptr;  // bf16 operand copy of p (or none)
   const int64_t n = sizes[tsr];
   const float coef = coef_p[0];
   auto upd = [&](float pv, float gv, float& mv, float& vv) {
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
   };
   const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nthr = (int64_t)gridDim.x * NT;
   const bool al = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
-                    reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+                    reinterpret_cast<uintptr_t>(v)) & 15) == 0 && (reinterpret_cast<uintptr_t>(sw) & 7) == 0;
   int64_t done = 0;
   if (al) {
     const int64_t n4 = n >> 2;
@@ -216,6 +218,10 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
       reinterpret_cast<float4*>(p)[i] = pv;
       reinterpret_cast<float4*>(m)[i] = mv;
       reinterpret_cast<float4*>(v)[i] = vv;
+      if (sw) {
+        const bf16x4 b4 = {(bf16)pv.x, (bf16)pv.y, (bf16)pv.z, (bf16)pv.w};
+        reinterpret_cast<bf16x4*>(sw)[i] = b4;
+      }
     }
     done = n4 << 2;
   }
@@ -224,6 +230,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
     p[i] = upd(p[i], g[i], mv, vv);
     m[i] = mv;
     v[i] = vv;
+    if (sw) sw[i] = (bf16)p[i];
   }
 }
 
@@ -414,7 +421,7 @@ extern "C" int64_t mia_adam_workspace_bytes(int32_t ntensors) {
 }
 
 extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg, void* const* exp_avg_sq,
-                             const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
+                             void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
                              float beta2, float eps, float weight_decay, int32_t step, float clip,
                              float* total_norm_out, void* sqnorm_ws, mia_stream_t stream) {
   MIA_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && sizes && sqnorm_ws, "clip_adam: null table");
@@ -430,7 +437,7 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
   const int ablocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(max_numel, 256 * 16)));
-  adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, sizes, coef,
+  adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, shadow_bf16, sizes, coef,
                                                      (float)(lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
                                                      weight_decay);
   MIA_LAUNCH_CHECK("adam");

@@ -320,6 +320,21 @@ def soft_ce(logits: torch.Tensor, y: torch.Tensor, input_sigmoid: bool):
     return loss[0], dlogits, correct[0]
 
 
+def bf16_shadow(p: torch.Tensor) -> torch.Tensor:
+    """bf16 GEMM-operand copy of an f32 parameter, kept on the parameter and refreshed by FusedAdam in
+    its update pass (no per-step cast).  Recast when anything else changed the parameter in place
+    (``_version`` moved: load_state_dict, DDP broadcast, a non-fused optimizer)."""
+    sh = getattr(p, "_mia_bf16", None)
+    if sh is not None and getattr(p, "_mia_bf16_ver", None) == p._version and sh.shape == p.shape:
+        return sh
+    if sh is None or sh.shape != p.shape or sh.device != p.device:
+        sh = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+    L.check(L.load().mia_cast(p.data_ptr(), L.F32, sh.data_ptr(), L.BF16, p.numel(), _s()), "mia_cast")
+    p._mia_bf16 = sh
+    p._mia_bf16_ver = p._version
+    return sh
+
+
 def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     out = torch.empty(src.shape, dtype=dtype, device=src.device)
     L.check(L.load().mia_cast(src.data_ptr(), L.dtype_code(src), out.data_ptr(), L.dtype_code(out), src.numel(),

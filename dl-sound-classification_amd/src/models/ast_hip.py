@@ -102,7 +102,7 @@ class ASTFunction(torch.autograd.Function):
         for i in range(nb):
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = params[4 + 12 * i: 16 + 12 * i]
             if cd == L.BF16:
-                wqkv, wproj, w1, w2 = (K.cast(w, torch.bfloat16) for w in (wqkv, wproj, w1, w2))
+                wqkv, wproj, w1, w2 = (K.bf16_shadow(w) for w in (wqkv, wproj, w1, w2))
             wcast.append((wqkv, wproj, w1, w2))
             h, m1, r1 = _ln(x, g1, b1, tdt, Tt, D)
             qkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)

@@ -170,7 +170,7 @@ class EnvNetFunction(torch.autograd.Function):
             fout, fin = Wt.shape
             last = li == 2
             if cd == L.BF16 and not last:
-                Wt = K.cast(Wt, torch.bfloat16)
+                Wt = K.bf16_shadow(Wt)
             wfc.append(Wt)
             out = torch.empty(B, fout, dtype=torch.float32 if last else tdt, device=dev)
             K.gemm(K.dense(h, L.KC, B, fin), K.dense(Wt, L.KC, fout, fin),

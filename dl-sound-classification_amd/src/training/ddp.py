@@ -34,6 +34,7 @@ class GradAllReducer:
         with torch.no_grad():
             for p in self.params:
                 dist.broadcast(p.data, 0)
+                p._mia_bf16_ver = None  # a collective writes behind autograd's version counter: recast
             for b in model.buffers():
                 dist.broadcast(b.data, 0)
         model._grad_ready = self.grad_ready

@@ -48,9 +48,13 @@ class FusedAdam(torch.optim.Optimizer):
             st["step"] += 1
         step = int(self.state[ps[0]]["step"].item())
         gs = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
+        # parameters with a live bf16 operand copy (K.bf16_shadow) get it rewritten in the update pass
+        shadows = [getattr(p, "_mia_bf16", None) if getattr(p, "_mia_bf16_ver", None) == p._version else None
+                   for p in ps]
         table = torch.tensor([[p.data_ptr() for p in ps], [g.data_ptr() for g in gs],
                               [self.state[p]["exp_avg"].data_ptr() for p in ps],
                               [self.state[p]["exp_avg_sq"].data_ptr() for p in ps],
+                              [0 if sh is None else sh.data_ptr() for sh in shadows],
                               [p.numel() for p in ps]], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         n = len(ps)
         lib = L.load()
@@ -58,10 +62,14 @@ class FusedAdam(torch.optim.Optimizer):
         tot = torch.empty(1, dtype=torch.float32, device=dev)
         b1, b2 = grp["betas"]
         L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
-                                  table[3].data_ptr(), table[4].data_ptr(), n, max(p.numel() for p in ps),
+                                  table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
+                                  max(p.numel() for p in ps),
                                   float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
                                   float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
                                   L.stream_ptr()), "mia_clip_adam")
         self.last_total_norm = tot
+        for p, sh in zip(ps, shadows):
+            if sh is not None:
+                p._mia_bf16_ver = p._version  # the copy now matches the updated parameter
         self._keep = (table, gs)  # keep the pointer table alive until the next step
         return loss

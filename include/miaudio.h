@@ -224,11 +224,13 @@ int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32
 /* Gradient clipping + Adam over a device-side table of tensors (Lightning
  * gradient_clip_val=1.0 + torch.optim.Adam(lr, weight_decay), base_training.yaml:51,56-59).
  * tables: f32* params[n], grads[n], m[n], v[n]; int64 sizes[n] (all device arrays).
+ * shadow_bf16: optional table of bf16* (entries may be NULL): the bf16 GEMM-operand copy of each
+ * updated parameter is written in the same pass (replaces a separate cast of the weights).
  * sqnorm_ws: f32 workspace of mia_adam_workspace_bytes(ntensors) bytes.
  * clip <= 0 disables clipping. step is 1-based. */
 int64_t mia_adam_workspace_bytes(int32_t ntensors);
 int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
-                  void* const* exp_avg_sq, const int64_t* sizes, int32_t ntensors,
+                  void* const* exp_avg_sq, void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors,
                   int64_t max_numel, float lr, float beta1, float beta2, float eps,
                   float weight_decay, int32_t step, float clip, float* total_norm_out,
                   void* sqnorm_ws, mia_stream_t stream);

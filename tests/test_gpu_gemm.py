@@ -416,3 +416,24 @@ def test_conv1ch_dgrad_bf16(cuda, n, oh, ow):
     wb = w.to(torch.bfloat16).double()
     ref = F.conv_transpose2d(dy.double().permute(0, 3, 1, 2), wb)[:, 0]
     assert rel(out.float().cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
+@pytest.mark.parametrize("M,N,Kd,split", [(4096, 3072, 256, 1), (4000, 3000, 192, 1), (3840, 3584, 1024, 3)])
+def test_dense256_layouts(cuda, monkeypatch, la, lb, M, N, Kd, split):
+    """The 256x256-tile LDS-DMA GEMM (opt-in: MIA_DGEMM256=1) vs a PyTorch fp32 matmul of the same
+    bf16 operands: every layout pair, ragged M/N edges, split-K slabs."""
+    monkeypatch.setenv("MIA_DGEMM256", "1")
+    g = torch.Generator(device=cuda).manual_seed(M + N + Kd)
+    a = torch.randn(M, Kd, generator=g, device=cuda).to(torch.bfloat16)
+    b = torch.randn(N, Kd, generator=g, device=cuda).to(torch.bfloat16)
+    ta = a.contiguous() if la == L.KC else a.t().contiguous()
+    tb = b.contiguous() if lb == L.KC else b.t().contiguous()
+    A = K.dense(ta, L.KC, M, Kd) if la == L.KC else K.dense(ta, L.RC, Kd, M)
+    Bo = K.dense(tb, L.KC, N, Kd) if lb == L.KC else K.dense(tb, L.RC, Kd, N)
+    bias = torch.randn(N, generator=g, device=cuda)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_RELU, bias=bias), M, N, Kd, L.BF16, split_k=split)
+    ref = torch.relu(a.float() @ b.float().t() + bias)
+    torch.cuda.synchronize()
+    assert rel(out.float(), ref) < 1e-2
