@@ -48,12 +48,14 @@ __device__ __forceinline__ void stage64(bf16* lds, const bf16* g, int64_t ld, in
 // (issue early / write late): 64 rows x 64 bf16 = 2 x 16 B per thread.
 struct Stage64 {
   uint4 v[2];
+  // rows >= nvalid re-read the last valid row (finite data; the scores of such keys are masked to
+  // -inf so their V rows meet p = 0): an unconditional load keeps hipcc from branching around it
   __device__ __forceinline__ void load(const bf16* g, int64_t ld, int nvalid, int t) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = t + 256 * s;
-      const int row = c >> 3, c16 = c & 7;
-      v[s] = row < nvalid ? *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8) : make_uint4(0, 0, 0, 0);
+      const int row = min(c >> 3, nvalid - 1), c16 = c & 7;
+      v[s] = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
     }
   }
   __device__ __forceinline__ void store(bf16* lds, int t) const {
@@ -102,11 +104,31 @@ __device__ __forceinline__ bf16x8 load_frag_global(const bf16* row, int ks, int 
   return *reinterpret_cast<const bf16x8*>(row + ks * 16 + 8 * (lane >> 5));
 }
 
+// v_max3_f32 as one instruction: fmaxf on MFMA results otherwise gets a canonicalising v_max per
+// operand (IEEE mode) and no max3 fusion
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// max(x[lane], x[lane ^ 32]) without an LDS round trip (v_permlane32_swap exchanges the halves)
+__device__ __forceinline__ float half_exchange_max(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float half_exchange_sum(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
 // row index of accumulator register r for this lane half
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 // ------------------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                        float* __restrict__ lse, int N, int H, float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
@@ -138,41 +160,55 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     const bf16* K_ = Ks[kt & 1];
     const bf16* V_ = Vs[kt & 1];
     const bool tail = k0 + 64 > N;
+    // both 32-key halves of the tile first (8 MFMAs), then ONE max / rescale decision per 64 keys
+    f32x16 s0 = zero16(), s1 = zero16();
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      f32x16 s = zero16();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s = mfma(frag_row(K_, st * 32 + (lane & 31), ks, lane), qf[ks], s);
-      if (tail) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (k0 + st * 32 + acc_row(r, lane) >= N) s[r] = -INFINITY;
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
-      const float mn = fmaxf(m, mx);
-      // rescale O only when some lane's running max moved (wave-uniform branch)
-      if (__any(mn > m)) {
-        const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
-        l *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-      }
-      m = mn;
-      const float nm = mn == -INFINITY ? 0.f : -mn;
+    for (int ks = 0; ks < 4; ++ks) {
+      s0 = mfma(frag_row(K_, lane & 31, ks, lane), qf[ks], s0);
+      s1 = mfma(frag_row(K_, 32 + (lane & 31), ks, lane), qf[ks], s1);
+    }
+    if (tail) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s[r] = exp2f(fmaf(s[r], scale_log2, nm));
-        l += s[r];
+        if (k0 + acc_row(r, lane) >= N) s0[r] = -INFINITY;
+        if (k0 + 32 + acc_row(r, lane) >= N) s1[r] = -INFINITY;
       }
+    }
+    float mx = max3(s0[0], s1[0], s0[1]);
 #pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        const bf16x8 pf = acc_frag(s, sk);
-        o0 = mfma(frag_tr(V_, st * 32 + 16 * sk, 0, lane), pf, o0);
-        o1 = mfma(frag_tr(V_, st * 32 + 16 * sk, 32, lane), pf, o1);
-      }
+    for (int r = 1; r < 15; ++r) mx = max3(mx, s1[r], s0[r + 1]);
+    mx = max3(mx, s1[15], s1[15]);
+    mx = half_exchange_max(mx) * scale_log2;
+    const float mn = fmaxf(m, mx);
+    // rescale O only when some lane's running max moved (wave-uniform branch)
+    if (__any(mn > m)) {
+      const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+      l *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    m = mn;
+    const float nm = mn == -INFINITY ? 0.f : -mn;
+    float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, nm));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, nm));
+      l0 += s0[r];
+      l1 += s1[r];
+    }
+    l += l0 + l1;
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 pf = acc_frag(s0, sk);
+      o0 = mfma(frag_tr(V_, 16 * sk, 0, lane), pf, o0);
+      o1 = mfma(frag_tr(V_, 16 * sk, 32, lane), pf, o1);
+    }
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 pf = acc_frag(s1, sk);
+      o0 = mfma(frag_tr(V_, 32 + 16 * sk, 0, lane), pf, o0);
+      o1 = mfma(frag_tr(V_, 32 + 16 * sk, 32, lane), pf, o1);
     }
     if (more) {
       kreg.store(Ks[(kt + 1) & 1], t);
@@ -180,7 +216,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     }
     __syncthreads();
   }
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = half_exchange_sum(l);
   if (qvalid) {
     const float inv = 1.f / lt;
     bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
@@ -222,7 +258,7 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __re
 }
 
 // key on the lane: each wave owns 32 keys (128 per block); sweeps query tiles of 64.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                             int N, int H, float scale, float scale_log2) {
@@ -283,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = sq * 32 + acc_row(r, lane);
-        const float p = exp2f(fmaf(s[r], scale_log2, -L_[qi]));
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -L_[qi]));
         s[r] = p;
         dp[r] = p * (dp[r] - D_[qi]);
       }
@@ -323,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 }
 
 // query on the lane: each wave owns 32 queries (128 per block); sweeps key tiles of 64.
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           bf16* __restrict__ dqkv, int N, int H, float scale,
                                                           float scale_log2) {
@@ -371,7 +407,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + st * 32 + acc_row(r, lane);
-        const float p = key < N ? exp2f(fmaf(s[r], scale_log2, -lq)) : 0.f;
+        const float p = key < N ? __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -lq)) : 0.f;
         dp[r] = p * (dp[r] - dq_delta);
       }
 #pragma unroll
