@@ -92,6 +92,20 @@ def envnet_step_fn(model, opt, wav, labels, g, world, ddp):
     return step
 
 
+def frontend_summary(regions: dict, B: int):
+    """The EnvNet-v2 1-D conv frontend (conv1 -> BN/ReLU -> conv2 -> BN/ReLU -> pool, fwd + bwd) as
+    one HBM-bound path: its algorithmic bytes (SURVEY.md §8(d), 86.6 MB/clip in bf16) over the live
+    HIP-event time of all its kernels, against the 8 TB/s HBM peak."""
+    f, b = regions.get("frontend.fwd"), regions.get("frontend.bwd")
+    if not f or not b:
+        return None
+    byts = f["bytes"] + b["bytes"]
+    ms = f["ms"] + b["ms"]
+    return {"bytes_per_clip": byts // B, "ms_fwd": round(f["ms"], 4), "ms_bwd": round(b["ms"], 4),
+            "achieved_gbs": round(byts / (ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+            "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -178,6 +192,7 @@ def main():
         step = envnet_step_fn(model, opt, wav, labels, g, world, ddp)
         flop_per_clip = ENVNET_FLOP_PER_CLIP
         probe_tags = (args.probe.split(",") if args.probe else ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv2.fwd"])
+        probe_tags += ["frontend.fwd", "frontend.bwd"]
         workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
     else:
         sys.path.insert(0, str(REPO))
@@ -221,6 +236,8 @@ def main():
         flops, byts = recs[0][2], recs[0][3]
         kstats[tag] = {"ms": dur, "tflops": flops / (dur * 1e-3) / 1e12, "gbs": byts / (dur * 1e-3) / 1e9,
                        "launches_per_step": len(recs) / args.steps, "flop": flops, "bytes": byts}
+    regions = {k: v for k, v in kstats.items() if k.startswith("frontend.")}
+    kstats = {k: v for k, v in kstats.items() if k not in regions}
     dom = max(kstats, key=lambda k: kstats[k]["ms"] * kstats[k]["launches_per_step"]) if kstats else None
     peak_tf = BF16_MFMA_PEAK_TF if args.dtype == "bf16" else F32_PEAK_TF
     roof = None
@@ -250,6 +267,7 @@ def main():
         "step_tflops": round(step_tf, 2),
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in kstats.items()},
+        "frontend_path": frontend_summary(regions, B),
         "loss": float(loss),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "envnet":

@@ -1525,7 +1525,7 @@ hipError_t rowconv_launch2(const RowArgs& r, bool pre, hipStream_t s) {
 template <typename TS>
 hipError_t rowconv_launch1(const RowArgs& r, int S, int C, bool pre, hipStream_t s) {
   if (S == 2) {
-    if (r.N == 64) return rowconv_launch2<TS, 128, 64, 2, 32, 16>(r, pre, s);
+    if (r.N == 64) return rowconv_launch2<TS, 256, 64, 2, 32, 16>(r, pre, s);  // conv2: 64 KB of weights per 256 px
     return rowconv_launch2<TS, 128, 32, 2, 32, 16>(r, pre, s);
   }
   if (C == 64) {
@@ -1732,6 +1732,25 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     }
     if (err != hipSuccess) return mia::fail(-(int)err, "tapwgrad launch: %s", hipGetErrorString(err));
     launch_splitk_reduce(r.ws, split_k, M, N, to_dev(*E), s);
+    MIA_LAUNCH_CHECK("splitk_reduce");
+    return 0;
+  }
+  if (workspace && rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k) && A->dtype == MIA_BF16 && M == 32 &&
+      B->c == 32 && B->kh == 8 && B->kw == 8 && B->sw == 1 && B->ph == 0 && B->pw == 0 &&
+      B->pre == MIA_PRE_AFFINE_RELU && B->h == B->oh + 7 && B->w == B->ow + 7) {
+    // trunk conv4 wgrad: rolling 8-row window per (clip, column chunk), one slab per block
+    W8Args w8;
+    w8.x = reinterpret_cast<const bf16*>(B->ptr);
+    w8.dy = reinterpret_cast<const bf16*>(A->ptr);
+    w8.ps = B->pre_scale; w8.pt = B->pre_shift;
+    w8.n = B->n; w8.h = B->h; w8.w = B->w; w8.oh = B->oh; w8.ow = B->ow;
+    const int64_t items = (int64_t)B->n * cdiv(B->ow, 128);
+    w8.nblk = (int)std::min<int64_t>(std::min<int64_t>(split_k, 256), items);
+    w8.ws = reinterpret_cast<float*>(workspace);
+    hipStream_t s = as_stream(stream);
+    hipError_t err = wgrad8_launch(w8, s);
+    if (err != hipSuccess) return mia::fail(-(int)err, "wgrad8 launch: %s", hipGetErrorString(err));
+    launch_splitk_reduce(w8.ws, w8.nblk, M, N, to_dev(*E), s);
     MIA_LAUNCH_CHECK("splitk_reduce");
     return 0;
   }

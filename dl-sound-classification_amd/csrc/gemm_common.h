@@ -154,6 +154,20 @@ static __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, i
 }
 
 
+// Rolling-window weight gradient of the 8x8, 32 -> 32 channel valid conv with a BN+ReLU pre-op
+// (wgrad8.hip): bf16 NHWC x (n, oh+7, ow+7, 32) raw, dy (n, oh, ow, 32); writes nblk f32 slabs
+// ws[nblk][32][2048] (OHWI columns) for the split-K reducer.
+struct W8Args {
+  const bf16* x;
+  const bf16* dy;
+  const float* ps;
+  const float* pt;
+  int n, h, w, oh, ow;
+  int nblk;
+  float* ws;
+};
+hipError_t wgrad8_launch(const W8Args& a, hipStream_t s);
+
 // 256x256-tile dense bf16 GEMM (dgemm256.hip); la/lb = MIA_LAYOUT_KC / MIA_LAYOUT_RC.
 hipError_t dgemm256_launch(const DArgs& d, int la, int lb, hipStream_t s);
 bool dgemm256_pays(int64_t M, int64_t N, int split);

@@ -11,6 +11,18 @@ namespace {
 
 constexpr int NT = 256;
 
+// n / d for 0 <= n < 2^31 without an integer division (Granlund-Montgomery: one mul_hi, add, shift)
+struct FastDiv {
+  uint32_t d, m, l;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1u << l) < d) ++l;
+  const uint32_t m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  return FastDiv{d, m, l};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.l; }
+
 __device__ __forceinline__ int64_t out_index(int layout, int b, int oy, int ox, int c, int OH, int OW, int C) {
   if (layout == 0) return (((int64_t)b * OH + oy) * OW + ox) * C + c;
   if (layout == 1) return ((int64_t)b * C + c) * OW + ox;                 // (n, c, ow), OH == 1
@@ -213,7 +225,8 @@ constexpr int PB_UNROLL = 4;
 __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_kernel(const float* __restrict__ gm,
                                                                const uint8_t* __restrict__ argmax,
                                                                const void* __restrict__ x, int dtype, int n, int H,
-                                                               int W, int C, int kh, int kw,
+                                                               int W, int C, int kh, int kw, FastDiv dW, FastDiv dH,
+                                                               FastDiv dkw, FastDiv dkh,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd,
@@ -244,8 +257,9 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_kernel(const float* __re
     for (int u = 0; u < PB_UNROLL; ++u) {
       const int r = min(r0 + u * stride, P - 1);
       load8(x, dtype, (int64_t)r * C + cg * 8, xv[u]);
-      const int ix = r % W, q = r / W, iy = q % H, b = q / H;
-      const int oy = min(iy / kh, OH - 1), ox = min(ix / kw, OW - 1);
+      const int q = (int)fdiv(r, dW), ix = r - q * W;
+      const int b = (int)fdiv(q, dH), iy = q - b * H;
+      const int oy = min((int)fdiv(iy, dkh), OH - 1), ox = min((int)fdiv(ix, dkw), OW - 1);
       const int64_t coff = (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8;
       am[u] = *reinterpret_cast<const uint2*>(argmax + coff);
       g0[u] = reinterpret_cast<const float4*>(gm + coff)[0];
@@ -255,8 +269,9 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_kernel(const float* __re
     for (int u = 0; u < PB_UNROLL; ++u) {
       const int r = r0 + u * stride;
       if (r >= P) break;
-      const int ix = r % W, q = r / W, iy = q % H;
-      const int oy = iy / kh, ox = ix / kw;
+      const int q = (int)fdiv(r, dW), ix = r - q * W;
+      const int iy = q - (int)fdiv(q, dH) * H;
+      const int oy = (int)fdiv(iy, dkh), ox = (int)fdiv(ix, dkw);
       const int pos = oy < OH && ox < OW ? (iy - oy * kh) * kw + (ix - ox * kw) : -1;
       const float gv[8] = {g0[u].x, g0[u].y, g0[u].z, g0[u].w, g1[u].x, g1[u].y, g1[u].z, g1[u].w};
       float g[8];
@@ -384,7 +399,8 @@ extern "C" int mia_pool_bn_relu_bwd_apply(const float* gm, const uint8_t* argmax
   const int64_t P = (int64_t)n * h * w;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
   hipStream_t s = as_stream(stream);
-  pool_bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(gm, argmax, x, dtype, n, h, w, c, kh, kw, gamma, mean, invstd, dgamma,
+  pool_bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(gm, argmax, x, dtype, n, h, w, c, kh, kw, make_fastdiv(w), make_fastdiv(h),
+                                             make_fastdiv(kw), make_fastdiv(kh), gamma, mean, invstd, dgamma,
                                              dbeta, dx, dbias ? (float*)partial : nullptr);
   MIA_LAUNCH_CHECK("pool_bn_bwd_apply");
   if (dbias) {

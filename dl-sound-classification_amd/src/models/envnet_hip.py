@@ -54,6 +54,22 @@ def geometry(T: int):
     return g
 
 
+def _frontend_work(B: int, g: dict, tdt: torch.dtype, backward: bool):
+    """Algorithmic (FLOP, HBM bytes) of the frontend 1-D conv path (conv1 -> BN -> ReLU -> conv2 -> BN
+    -> ReLU -> maxpool), SURVEY.md §8(d): compulsory tensor traffic with X = the f32 waveform,
+    S1 / S2 = the conv1 / conv2 outputs, P = the pooled map (compute dtype).
+    fwd = X + 2 S1 + 2 S2 + P;  bwd = P + 4 S2 + 4 S1 + X."""
+    es = torch.finfo(tdt).bits // 8
+    X = g["T"] * 4
+    S1 = g["W1"] * 32 * es
+    S2 = g["W2"] * 64 * es
+    P = 64 * g["Wp"] * es
+    flop = 2.0 * (g["W1"] * 32 * 64 + g["W2"] * 64 * 512)  # conv1 + conv2 MACs x 2
+    if backward:
+        return B * 2 * flop, B * (P + 4 * S2 + 4 * S1 + X)
+    return B * flop, B * (X + 2 * S1 + 2 * S2 + P)
+
+
 def _param_list(m):
     """Flat parameter order handed to the autograd Function (also the grad order)."""
     ps = [m.frontend[0].weight, m.frontend[0].bias, m.frontend[1].weight, m.frontend[1].bias,
@@ -103,6 +119,8 @@ class EnvNetFunction(torch.autograd.Function):
                                   mod.momentum if mod.momentum is not None else 0.1, mod.eps, training)
 
         # ---- frontend conv1: CONVROW over the (B, T/2, 2) view of the waveform
+        fe = K.probe("frontend.fwd", *_frontend_work(B, g, tdt, backward=False))
+        fe.__enter__()
         w1 = K.pack_weight(p[0], cd, 0)
         y1 = torch.empty(B * W1, 32, dtype=tdt, device=dev)
         A = K.conv(x, L.KC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
@@ -121,6 +139,7 @@ class EnvNetFunction(torch.autograd.Function):
         X0 = torch.empty(B, 64, Wp, dtype=tdt, device=dev)
         am0 = torch.empty(B, Wp, 64, dtype=torch.uint8, device=dev)
         K.pool_fwd(y2, B, 1, W2, 64, 1, 64, bn2, X0, 1, am0)
+        fe.__exit__(None, None, None)
         saved.update(x=x, y1=y1, y2=y2, bn1=bn1, bn2=bn2, X0=X0, am0=am0)
 
         # ---- trunk
@@ -315,6 +334,8 @@ class EnvNetFunction(torch.autograd.Function):
             emit(pa, pa + 8)
 
         # ---- frontend backward
+        fe = K.probe("frontend.bwd", *_frontend_work(B, g, tdt, backward=True))
+        fe.__enter__()
         W1, W2, Wp = g["W1"], g["W2"], g["Wp"]
         P2, P1 = B * W2, B * W1
         gm, dg2, db2 = K.pool_bwd_gather(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"])
@@ -350,6 +371,7 @@ class EnvNetFunction(torch.autograd.Function):
         K.gemm(K.dense(da1, L.RC, P1, 32), K.conv(s["x"], L.RC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True),
                K.epilogue(dW1, 64), 32, 64, P1, cd, tag="conv1.wgrad")
         grads[0] = dW1.view_as(p[0])
+        fe.__exit__(None, None, None)
         emit(0, 8)
         ctx.saved = None
         return (None, None, None, *grads)

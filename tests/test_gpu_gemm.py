@@ -437,3 +437,27 @@ def test_dense256_layouts(cuda, monkeypatch, la, lb, M, N, Kd, split):
     ref = torch.relu(a.float() @ b.float().t() + bias)
     torch.cuda.synchronize()
     assert rel(out.float(), ref) < 1e-2
+
+
+def test_wgrad8_many_items(cuda):
+    """Rolling-window 8x8 wgrad (trunk conv4) with more (clip, chunk) items than blocks, ragged
+    column chunks: vs a PyTorch fp32 autograd weight gradient of the same bf16 operands."""
+    n, c, h, w = 70, 32, 20, 400
+    g = torch.Generator(device=cuda).manual_seed(11)
+    x = torch.randn(n, h, w, c, generator=g, device=cuda).to(torch.bfloat16)
+    sc = torch.rand(c, generator=g, device=cuda) + 0.5
+    sh = torch.randn(c, generator=g, device=cuda) * 0.1
+    oh, ow = h - 7, w - 7
+    dy = torch.randn(n, oh, ow, c, generator=g, device=cuda).to(torch.bfloat16)
+    xin = torch.relu(x.float() * sc + sh).to(torch.bfloat16).float()
+    wr = torch.zeros(c, c, 8, 8, device=cuda, requires_grad=True)
+    F.conv2d(xin.permute(0, 3, 1, 2), wr).backward(dy.float().permute(0, 3, 1, 2))
+    P, Kc = n * oh * ow, 64 * c
+    A = K.dense(dy, L.RC, P, c)
+    Bo = K.conv(x, L.RC, n, h, w, c, oh, ow, 8, 8, pre=L.PRE_AFFINE_RELU, scale=sc, shift=sh)
+    dW = torch.empty(c, Kc, dtype=torch.float32, device=cuda)
+    K.gemm(A, Bo, K.epilogue(dW, Kc), c, Kc, P, L.BF16)
+    gw = torch.empty(c, c, 8, 8, device=cuda)
+    K.unpack_ohwi_grad(dW, (c, c, 8, 8), gw)
+    torch.cuda.synchronize()
+    assert rel(gw, wr.grad) < 1e-2
