@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", choices=["envnet", "ast"], default="envnet")
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256 EnvNet, 64 AST)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256 for both models)")
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default=None, help="comma list of GEMM tags to time live (default: auto)")
@@ -197,7 +197,7 @@ def main():
     else:
         sys.path.insert(0, str(REPO))
         from bench_ast import build_ast_step  # noqa: E402
-        B = args.batch or 64
+        B = args.batch or 256  # AST at batch 256 on one MI355X (~84 GB of activations)
         step, flop_per_clip, probe_tags, workload = build_ast_step(args, dev, rank, world, B)
 
     if world > 1:

@@ -112,7 +112,8 @@ __global__ __launch_bounds__(NT8) void dgemm256_kernel(DArgs g) {
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int bm = wgid % g.nbm, bn = wgid / g.nbm;
+  const int bm = g.nfast ? wgid / g.nbn : wgid % g.nbm;
+  const int bn = g.nfast ? wgid % g.nbn : wgid / g.nbm;
   const int64_t m0 = (int64_t)bm * 256, n0 = (int64_t)bn * 256;
   const int z = blockIdx.y;
   const int64_t kbeg = (int64_t)z * g.kper;
@@ -262,6 +263,7 @@ hipError_t launch(const DArgs& d, hipStream_t s) {
   DArgs e = d;
   e.nbm = (int)cdiv(d.M, 256);
   e.nbn = (int)cdiv(d.N, 256);
+  e.nfast = (d.split == 1 && e.nbn <= 16 && e.nbm >= 4 * e.nbn) ? 1 : 0;
   dim3 grid((unsigned)(e.nbm * e.nbn), (unsigned)d.split);
   dgemm256_kernel<LA, LB><<<grid, NT8, 0, s>>>(e);
   return hipGetLastError();

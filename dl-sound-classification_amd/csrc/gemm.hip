@@ -1387,7 +1387,8 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int bm = wgid % g.nbm, bn = wgid / g.nbm;
+  const int bm = g.nfast ? wgid / g.nbn : wgid % g.nbm;
+  const int bn = g.nfast ? wgid % g.nbn : wgid / g.nbm;
   const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
   const int z = blockIdx.y;
   const int64_t kbeg = (int64_t)z * g.kper;
@@ -1668,6 +1669,10 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     d.split = split_k < 1 ? 1 : split_k;
     d.kper = cdiv(cdiv(K, d.split), 64) * 64;
     d.nbm = (int)cdiv(M, 128); d.nbn = (int)cdiv(N, 128);
+    // tall GEMMs (AST linears: M = tokens, N <= 3072): walk N fastest so each A row block is read
+    // from HBM once (at batch 256 the activations exceed the 256 MB Infinity Cache, and an
+    // M-fastest walk re-streamed them once per column tile: 12-15 GB per launch, rocprof FETCH_SIZE)
+    d.nfast = (d.split == 1 && d.nbn <= 32 && d.nbm >= 4 * d.nbn) ? 1 : 0;
     d.ws = reinterpret_cast<float*>(workspace);
     d.e = to_dev(*E);
     hipStream_t s = as_stream(stream);

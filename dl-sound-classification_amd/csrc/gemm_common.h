@@ -20,6 +20,8 @@ struct DArgs {
   const bf16* b;
   int64_t lda, ldb, M, N, K, kper;
   int split, nbm, nbn;
+  int nfast;  // 1: consecutive tiles walk N (the few column tiles of a tall GEMM share one A row
+              // block, so A streams from HBM once instead of once per column tile)
   float* ws;
   EpiDev e;
 };
