@@ -1,0 +1,316 @@
+// EnvNet-v2 frontend conv2 (reference src/models/envnet_v2.py:19 Conv2d(32, 64, (1, 16), stride
+// (1, 2)), input relu(bn1(conv1 output))) forward, and its backward-data, as persistent
+// weight-stationary 1-D convolutions, bf16 MFMA, gfx950.
+//
+//   forward:  y2[b][o][co]      = bias[co] + sum_{kx,ci} W[co][kx][ci] * relu(bn1(y1))[b][2o+kx][ci]
+//   dgrad:    da1[b][2m+r][ci]  = sum_{j,co} Wpar[r][ci][j][co] * dy2[b][m+j-7][co]      (r = 0, 1)
+//
+// Both are "64 output channels x K = 512" contractions over a window of input pixels (forward: 32
+// channels x 16 taps at stride 2; dgrad: the two output parities stacked as 64 virtual channels,
+// 64 channels x 8 taps at stride 1; the parity pair (2m, 2m+1) x 32 channels is one contiguous
+// 64-element row of da1, so the dgrad output is a plain (pixel, 64) image with a per-clip stride).
+// The op sits on the HBM/MFMA balance point (256 FLOP per HBM byte), so the kernel is built to
+// stream: each wave keeps its 32 output channels x 512 weights in registers for the whole launch
+// (A operand, 128 VGPRs); two 4-wave workgroups per CU walk (clip, 128-pixel) items; the input
+// window of item i+2 is loaded raw into registers while item i computes, and item i+1's window
+// (loaded one item earlier) is BN-affine+ReLU'd and bf16-packed on its way into the other half of
+// a double-buffered LDS window (one LDS-only barrier per item; output stores are never waited
+// for).  Every input byte is read from HBM once per item (window overlap 16 / 8 pixels), every
+// output byte written once, weights never re-streamed (the row-window kernel re-read 64 KB of
+// weights per 256 output pixels).  MFMA: D[co][px] = W[co][k] x window^T[k][px], the accumulator
+// rows are output channels, so after one v_permlane32_swap per register pair each lane holds two
+// runs of 8 contiguous channels of one pixel and stores them as 16-B vectors without an LDS pass.
+// Measured at B=256 (tools/bench_fe.py): the load+store stream alone (no MFMA) takes 0.71 ms
+// (5.1 TB/s), the MFMA work alone 0.30-0.37 ms; the kernel lands at 0.98-1.15 ms.
+#include "common.h"
+
+namespace {
+
+constexpr int FE_NT = 256;
+constexpr int FE_BM = 128;  // output pixels per item (4 waves: 2 channel halves x 2 pixel halves)
+constexpr int FE_N = 64;    // output channels
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <int CIN, int KW, int S>
+struct FeCfg {
+  static constexpr int CG = CIN / 8;                    // 16-B chunks per pixel
+  static constexpr int WPX = (FE_BM - 1) * S + KW;      // window pixels per item
+  static constexpr int HALF = (WPX + 1) / 2;            // stride 2: even pixels, then odd pixels
+  static constexpr int NSLOT = S == 1 ? WPX : 2 * HALF;
+  static constexpr int PSB = CIN * 2 + 16;              // LDS bytes per pixel (conflict-free b128 reads)
+  static constexpr int WBYTES = NSLOT * PSB;
+  static constexpr int NCH = WPX * CG;
+  static constexpr int LCH = (NCH + FE_NT - 1) / FE_NT;  // window chunks per thread
+  static constexpr int KS = KW * CIN / 16;              // MFMA k-steps
+  static_assert(FE_NT % CG == 0, "channel chunk must be constant per thread");
+  static_assert(KS == 32, "weights-in-registers layout assumes K = 512");
+};
+
+struct FeArgs {
+  const bf16* x;      // (n, win, CIN)
+  const float* ps;    // pre-op scale/shift per input channel (BN1 affine, then ReLU) or null
+  const float* pt;
+  const bf16* w;      // (64, KW*CIN), k = kx*CIN + ci
+  const float* bias;  // (64) or null
+  bf16* y;            // y[b*ystride + m*64 + n], stored while m < wout and m*64+n < ylen
+  int n, win, wout, pw, nitem;
+  int64_t ystride, ylen;
+};
+
+template <int S, int HALF>
+__device__ __forceinline__ int fe_slot(int p) {
+  if constexpr (S == 1) return p;
+  else return (p & 1) * HALF + (p >> 1);
+}
+
+__device__ __forceinline__ u32x4 fe_cook(u32x4 u, bool ok, bool pre, const float* sc, const float* sh) {
+  if (!ok) return u32x4{0u, 0u, 0u, 0u};
+  if (!pre) return u;
+  uint32_t w4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = fmaxf(fmaf(__uint_as_float(u[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(u[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
+    const bf16 bl = (bf16)lo, bh = (bf16)hi;
+    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+  }
+  return u32x4{w4[0], w4[1], w4[2], w4[3]};
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const bf16 bl = (bf16)lo, bh = (bf16)hi;
+  return (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+}
+
+template <int CIN, int KW, int S, bool PRE>
+__global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void feconv_kernel(FeArgs g) {
+  using Cfg = FeCfg<CIN, KW, S>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * Cfg::WBYTES];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nh = wave & 1, pq = wave >> 1;
+  const int cg = t % Cfg::CG;
+  const int items = g.n * g.nitem;
+  if ((int)blockIdx.x >= items) return;  // whole block
+
+  // weights as MFMA A fragments: row co = nh*32 + (lane & 31), k = ks*16 + 8*(lane >> 5) .. +7
+  bf16x8 wf[Cfg::KS];
+  {
+    const bf16* wr = g.w + (int64_t)(nh * 32 + (lane & 31)) * (KW * CIN) + 8 * (lane >> 5);
+#pragma unroll
+    for (int ks = 0; ks < Cfg::KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 16);
+  }
+  // after the half swap this lane owns channels c0..c0+7 and c0+16..c0+23 of its pixel; the bias
+  // lives in LDS (read back per tile) to leave registers for the second window set
+  const int c0 = nh * 32 + 8 * (lane >> 5);
+  // (bias and the input pre-op scale/shift live in LDS and are read where used: registers go to the
+  // weights, the accumulators and the two in-flight window sets)
+  __shared__ __attribute__((aligned(16))) float sbias[FE_N];
+  __shared__ __attribute__((aligned(16))) float spre[2][CIN];
+  if (t < FE_N) sbias[t] = g.bias ? g.bias[t] : 0.f;
+  if (PRE && t < CIN) {
+    spre[0][t] = g.ps[t];
+    spre[1][t] = g.pt[t];
+  }
+
+  // Two register sets of raw window chunks: while item k computes, item k+1's window (loaded during
+  // item k-1) waits in one set and item k+2's loads are in flight into the other.
+  u32x4 rawa[Cfg::LCH], rawb[Cfg::LCH];
+  uint32_t oka = 0, okb = 0;
+  // Buffer loads with 32-bit byte offsets (the host keeps a launch's input under 2 GB): a chunk
+  // outside the window or the clip gets an offset past num_records and reads zeros, so no load
+  // is predicated and no 64-bit address temporaries compete with the in-flight register sets.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(g.x), (short)0, (int)((int64_t)g.n * g.win * CIN * 2), 0x00020000);
+  auto load = [&](int it, u32x4 (&raw)[Cfg::LCH], uint32_t& rok) __attribute__((always_inline)) {
+    it = it < items ? it : items - 1;  // past the end: a harmless redundant load
+    const int b = it / g.nitem;
+    const int px0 = (it - b * g.nitem) * FE_BM * S - g.pw;
+    rok = 0;
+#pragma unroll
+    for (int s = 0; s < Cfg::LCH; ++s) {
+      const int q = t + FE_NT * s;
+      const int p = q / Cfg::CG;
+      const int ix = px0 + p;
+      const bool ok = p < Cfg::WPX && ix >= 0 && ix < g.win;
+      const unsigned off = ok ? (unsigned)((b * g.win + ix) * Cfg::CG + cg) * 16u : 0x80000000u;
+      raw[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      rok |= (uint32_t)ok << s;
+    }
+  };
+  auto store = [&](int buf, const u32x4 (&raw)[Cfg::LCH], uint32_t rok) __attribute__((always_inline)) {
+    float sc[8], sh[8];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&spre[0][cg * 8 + 4 * h]);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(&spre[1][cg * 8 + 4 * h]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { sc[4 * h + q] = a[q]; sh[4 * h + q] = c[q]; }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < Cfg::LCH; ++s) {
+      const int q = t + FE_NT * s;
+      const int p = q / Cfg::CG;
+      if (Cfg::NCH % FE_NT == 0 || p < Cfg::WPX)
+        *reinterpret_cast<u32x4*>(smem + buf * Cfg::WBYTES + fe_slot<S, Cfg::HALF>(p) * Cfg::PSB + cg * 16) =
+            fe_cook(raw[s], (rok >> s) & 1u, PRE, sc, sh);
+    }
+  };
+  auto compute = [&](int buf, f32x16 (&acc)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    const char* win = smem + buf * Cfg::WBYTES;
+#pragma unroll
+    for (int ks = 0; ks < Cfg::KS; ++ks) {
+      constexpr int KPC = CIN / 16;  // k-steps per tap
+      const int kx = ks / KPC;
+      const int ci = (ks % KPC) * 16 + 8 * (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int px = pq * 64 + i * 32 + (lane & 31);
+        int slot;
+        if constexpr (S == 1) slot = px + kx;
+        else slot = (kx & 1) * Cfg::HALF + px + (kx >> 1);
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(win + slot * Cfg::PSB + ci * 2);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], fb, acc[i], 0, 0, 0);
+      }
+    }
+  };
+  // epilogue: rows of acc are channels nh*32 + (r&3) + 8*(r>>2) + 4*(lane>>5); swap halves so the
+  // lane holds channels c0..c0+7 (v[0..7]) and c0+16..c0+23 (v[8..15]) of one pixel
+  auto epilogue = [&](int item, const f32x16 (&acc)[2]) __attribute__((always_inline)) {
+    const int b = item / g.nitem;
+    const int m0 = (item - b * g.nitem) * FE_BM + pq * 64;
+    bf16* yb = g.y + (int64_t)b * g.ystride;
+    float bv[16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(sbias + c0 + 16 * h);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(sbias + c0 + 16 * h + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { bv[8 * h + q] = u0[q]; bv[8 * h + 4 + q] = u1[q]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float v[16];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // (__float_as_uint of a copied element: clang folds __builtin_bit_cast of a vector-element
+          // lvalue to element 0)
+          const float lo = acc[i][8 * h + j], hi = acc[i][8 * h + 4 + j];
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+          v[8 * h + j] = __builtin_bit_cast(float, (unsigned)r[0]);
+          v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)r[1]);
+        }
+      const int m = m0 + i * 32 + (lane & 31);
+      if (m < g.wout) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int64_t e = (int64_t)m * FE_N + c0 + 16 * h;
+          if (e < g.ylen) {
+            const u32x4 o = {pack2(v[8 * h] + bv[8 * h], v[8 * h + 1] + bv[8 * h + 1]),
+                             pack2(v[8 * h + 2] + bv[8 * h + 2], v[8 * h + 3] + bv[8 * h + 3]),
+                             pack2(v[8 * h + 4] + bv[8 * h + 4], v[8 * h + 5] + bv[8 * h + 5]),
+                             pack2(v[8 * h + 6] + bv[8 * h + 6], v[8 * h + 7] + bv[8 * h + 7])};
+            *reinterpret_cast<u32x4*>(yb + e) = o;
+          }
+        }
+      }
+    }
+  };
+  // one item: issue item+2G's loads into `ld`, compute from LDS half `buf`, store the outputs, move
+  // item+G's raw window (`st`, loaded one item earlier) into the other half, barrier (LDS only: the
+  // global stores stay in flight across it)
+  auto step = [&](int item, int buf, u32x4 (&ld)[Cfg::LCH], uint32_t& ldok, const u32x4 (&st)[Cfg::LCH],
+                  uint32_t stok) __attribute__((always_inline)) {
+    load(item + 2 * (int)gridDim.x, ld, ldok);
+    f32x16 acc[2];
+    compute(buf, acc);
+    epilogue(item, acc);      // global stores issue behind the in-flight loads; nothing waits for them
+    store(buf ^ 1, st, stok);  // waits only for `st`'s loads (issued an item ago)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+  };
+
+  int item = blockIdx.x;
+  load(item, rawa, oka);
+  load(item + (int)gridDim.x, rawb, okb);
+  __syncthreads();  // sbias / spre visible
+  store(0, rawa, oka);
+  __syncthreads();
+  for (;;) {
+    step(item, 0, rawa, oka, rawb, okb);
+    item += gridDim.x;
+    if (item >= items) break;
+    step(item, 1, rawb, okb, rawa, oka);
+    item += gridDim.x;
+    if (item >= items) break;
+  }
+}
+
+int fe_grid(int items) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  return items < 2 * ncu ? items : 2 * ncu;  // two workgroups per CU: their item phases drift apart, so
+                                              // one's VALU epilogue/staging overlaps the other's MFMAs
+}
+
+// clips per launch so that one launch's input stays below 2 GB (32-bit buffer offsets)
+int fe_clips_per_launch(int64_t clip_bytes) { return (int)(((1ll << 31) - 1) / clip_bytes); }
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mia_fe_conv2_fwd(const void* y1, const float* scale, const float* shift, const void* w,
+                                const float* bias, void* y2, int32_t n, int32_t w1, int32_t w2,
+                                mia_stream_t stream) {
+  MIA_CHECK_ARG(y1 && w && y2 && n > 0 && w1 >= 16, "fe_conv2_fwd: bad arguments");
+  MIA_CHECK_ARG(!scale == !shift, "fe_conv2_fwd: scale and shift go together");
+  MIA_CHECK_ARG(w2 == (w1 - 16) / 2 + 1, "fe_conv2_fwd: w2 must be (w1-16)/2+1 (got w1=%d w2=%d)", w1, w2);
+  MIA_CHECK_ARG(aligned16(y1) && aligned16(w) && aligned16(y2), "fe_conv2_fwd: operands must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int per = fe_clips_per_launch((int64_t)w1 * 32 * 2);
+  MIA_CHECK_ARG(per > 0, "fe_conv2_fwd: one clip exceeds 2 GB");
+  for (int c = 0; c < n; c += per) {
+    const int nc = n - c < per ? n - c : per;
+    FeArgs a{reinterpret_cast<const bf16*>(y1) + (int64_t)c * w1 * 32, scale, shift, reinterpret_cast<const bf16*>(w),
+             bias, reinterpret_cast<bf16*>(y2) + (int64_t)c * w2 * FE_N, nc, w1, w2, 0, (int)cdiv(w2, FE_BM),
+             (int64_t)w2 * FE_N, (int64_t)w2 * FE_N};
+    const int grid = fe_grid(nc * a.nitem);
+    if (scale) feconv_kernel<32, 16, 2, true><<<grid, FE_NT, 0, s>>>(a);
+    else feconv_kernel<32, 16, 2, false><<<grid, FE_NT, 0, s>>>(a);
+    MIA_LAUNCH_CHECK("fe_conv2_fwd");
+  }
+  return 0;
+}
+
+extern "C" int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, int32_t n, int32_t w1,
+                                  int32_t w2, mia_stream_t stream) {
+  MIA_CHECK_ARG(dy2 && wpar && da1 && n > 0 && w1 >= 16, "fe_conv2_dgrad: bad arguments");
+  MIA_CHECK_ARG(w2 == (w1 - 16) / 2 + 1, "fe_conv2_dgrad: w2 must be (w1-16)/2+1 (got w1=%d w2=%d)", w1, w2);
+  MIA_CHECK_ARG(aligned16(dy2) && aligned16(wpar) && aligned16(da1), "fe_conv2_dgrad: operands must be 16-byte aligned");
+  MIA_CHECK_ARG(((int64_t)w1 * 32) % 8 == 0, "fe_conv2_dgrad: clip stride must keep 16-byte alignment");
+  const int wout = (w1 + 1) / 2;  // parity pairs (2m, 2m+1)
+  const int per = fe_clips_per_launch((int64_t)w2 * 64 * 2);
+  MIA_CHECK_ARG(per > 0, "fe_conv2_dgrad: one clip exceeds 2 GB");
+  for (int c = 0; c < n; c += per) {
+    const int nc = n - c < per ? n - c : per;
+    FeArgs a{reinterpret_cast<const bf16*>(dy2) + (int64_t)c * w2 * 64, nullptr, nullptr,
+             reinterpret_cast<const bf16*>(wpar), nullptr, reinterpret_cast<bf16*>(da1) + (int64_t)c * w1 * 32, nc,
+             w2, wout, 7, (int)cdiv(wout, FE_BM), (int64_t)w1 * 32, (int64_t)w1 * 32};
+    feconv_kernel<64, 8, 1, false><<<fe_grid(nc * a.nitem), FE_NT, 0, as_stream(stream)>>>(a);
+    MIA_LAUNCH_CHECK("fe_conv2_dgrad");
+  }
+  return 0;
+}

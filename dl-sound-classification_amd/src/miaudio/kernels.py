@@ -30,6 +30,10 @@ def _s():
     return L.stream_ptr()
 
 
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
 # ------------------------------------------------------------------------------------ GEMM
 def dense(t: torch.Tensor, layout: int, rows: int, cols: int, ld: int | None = None,
           pre: int = L.PRE_NONE, scale=None, shift=None, dtype: int | None = None) -> L.MiaOperand:
@@ -289,6 +293,32 @@ def conv1ch_dgrad(dy: torch.Tensor, w: torch.Tensor, n: int, oh: int, ow: int, o
     with probe(tag or "", flop, dy.numel() * 2 + out.numel() * 2):
         L.check(L.load().mia_conv1ch_dgrad(dy.data_ptr(), w.data_ptr(), out.data_ptr(), n, oh, ow, _s()),
                 "mia_conv1ch_dgrad")
+
+
+def fe_conv2_fwd(y1: torch.Tensor, scale, shift, w: torch.Tensor, bias, y2: torch.Tensor, n: int, w1: int,
+                 w2: int, tag: str | None = None):
+    """EnvNet conv2 forward (bf16): y1 (n*w1, 32), optional BN1 scale/shift (+ReLU) applied to the
+    input, w packed OHWI (64, 16*32), bias f32 (64) or None -> y2 (n*w2, 64)."""
+    assert y1.dtype == torch.bfloat16 and y2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    assert y1.numel() == n * w1 * 32 and y2.numel() == n * w2 * 64 and w.numel() == 64 * 512
+    assert y1.is_contiguous() and y2.is_contiguous() and w.is_contiguous()
+    flop = 2.0 * n * w2 * 64 * 512
+    with probe(tag or "", flop, y1.numel() * 2 + y2.numel() * 2):
+        L.check(L.load().mia_fe_conv2_fwd(y1.data_ptr(), _ptr(scale), _ptr(shift), w.data_ptr(), _ptr(bias),
+                                          y2.data_ptr(), n, w1, w2, _s()), "mia_fe_conv2_fwd")
+
+
+def fe_conv2_dgrad(dy2: torch.Tensor, wpar: torch.Tensor, da1: torch.Tensor, n: int, w1: int, w2: int,
+                   tag: str | None = None):
+    """Backward-data of EnvNet conv2 (bf16): dy2 (n*w2, 64), wpar = pack_weight(W, bf16, 2)
+    (2*32, 8*64) -> da1 (n*w1, 32)."""
+    assert dy2.dtype == torch.bfloat16 and da1.dtype == torch.bfloat16 and wpar.dtype == torch.bfloat16
+    assert dy2.numel() == n * w2 * 64 and da1.numel() == n * w1 * 32 and wpar.numel() == 64 * 512
+    assert dy2.is_contiguous() and da1.is_contiguous() and wpar.is_contiguous()
+    flop = 2.0 * n * w1 * 32 * 512
+    with probe(tag or "", flop, dy2.numel() * 2 + da1.numel() * 2):
+        L.check(L.load().mia_fe_conv2_dgrad(dy2.data_ptr(), wpar.data_ptr(), da1.data_ptr(), n, w1, w2, _s()),
+                "mia_fe_conv2_dgrad")
 
 
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:

@@ -73,6 +73,8 @@ SIGNATURES = {
     "mia_colsum": (C.c_int, [vp, i32, i64, i32, i64, vp, vp, vp]),
     "mia_col2im_rows": (C.c_int, [vp, i32, i32, i32, i32, vp, i32, vp]),
     "mia_conv1ch_dgrad": (C.c_int, [vp, vp, vp, i32, i32, i32, vp]),
+    "mia_fe_conv2_fwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "mia_fe_conv2_dgrad": (C.c_int, [vp, vp, vp, i32, i32, i32, vp]),
     "mia_pack_weight": (C.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "mia_dropout": (C.c_int, [vp, i32, i64, f32, C.c_uint64, vp]),
     "mia_soft_ce": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp]),

@@ -130,10 +130,13 @@ class EnvNetFunction(torch.autograd.Function):
         # ---- conv2 (stride 2) with BN1+ReLU fused into the operand load
         w2 = K.pack_weight(p[4], cd, 0)
         y2 = torch.empty(B * W2, 64, dtype=tdt, device=dev)
-        A = K.conv(y1, L.KC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU, scale=bn1.scale,
-                   shift=bn1.shift)
-        K.gemm(A, K.dense(w2, L.KC, 64, 512), K.epilogue(y2, 64, bias=p[5]), B * W2, 64, 512, cd,
-               tag="conv2.fwd")
+        if cd == L.BF16:
+            K.fe_conv2_fwd(y1, bn1.scale, bn1.shift, w2, p[5], y2, B, W1, W2, tag="conv2.fwd")
+        else:
+            A = K.conv(y1, L.KC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU, scale=bn1.scale,
+                       shift=bn1.shift)
+            K.gemm(A, K.dense(w2, L.KC, 64, 512), K.epilogue(y2, 64, bias=p[5]), B * W2, 64, 512, cd,
+                   tag="conv2.fwd")
         bn2 = bn(1, y2, B * W2, 64)
         # ---- maxpool (1,64) of relu(bn2(y2)), written as the transposed trunk image (B, 64, Wp)
         X0 = torch.empty(B, 64, Wp, dtype=tdt, device=dev)
@@ -354,13 +357,17 @@ class EnvNetFunction(torch.autograd.Function):
         K.unpack_ohwi_grad(dW2, p[4].shape, gw2)
         grads[4] = gw2
         # stride-2 dgrad as two stride-1 parity convolutions
-        wpar = K.pack_weight(p[4], cd, 2).view(2, 32 * 8 * 64)
+        wpar = K.pack_weight(p[4], cd, 2)
         da1 = torch.empty(P1, 32, dtype=tdt, device=dev)
-        for par in (0, 1):
-            Tp = (W1 - par + 1) // 2
-            K.gemm(K.conv(dy2, L.KC, B, 1, W2, 64, 1, Tp, 1, 8, pw=7),
-                   K.dense(wpar[par], L.KC, 32, 512),
-                   K.epilogue(da1, 32, rowmap=(Tp, W1, 2, par)), B * Tp, 32, 512, cd, tag="conv2.dgrad")
+        if cd == L.BF16:
+            K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2, tag="conv2.dgrad")
+        else:
+            wpar = wpar.view(2, 32 * 8 * 64)
+            for par in (0, 1):
+                Tp = (W1 - par + 1) // 2
+                K.gemm(K.conv(dy2, L.KC, B, 1, W2, 64, 1, Tp, 1, 8, pw=7),
+                       K.dense(wpar[par], L.KC, 32, 512),
+                       K.epilogue(da1, 32, rowmap=(Tp, W1, 2, par)), B * Tp, 32, 512, cd, tag="conv2.dgrad")
         dg1, db1 = K.bn_relu_bwd_reduce(da1, None, s["y1"], P1, 32, s["bn1"])
         grads[2], grads[3] = dg1, db1
         dbias1 = torch.empty(32, dtype=torch.float32, device=dev)

@@ -194,6 +194,22 @@ int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh
 int mia_conv1ch_dgrad(const void* dy, const float* w, void* dx, int32_t n, int32_t oh, int32_t ow,
                       mia_stream_t stream);
 
+/* EnvNet-v2 frontend conv2 forward (reference src/models/envnet_v2.py:19 Conv2d(32, 64, (1, 16),
+ * stride (1, 2)) applied to relu(bn1(y1)), envnet_v2.py:20-21; replaces that cuDNN conv2d):
+ *   y2[b][o][co] = bias[co] + sum_{kx,ci} w[co][kx][ci] * relu(y1[b][2o+kx][ci]*scale[ci] + shift[ci])
+ * bf16 only.  y1 (n, w1, 32), w OHWI (64, 16, 32) (mia_pack_weight mode 0), bias f32 (64) or NULL,
+ * y2 (n, w2, 64) with w2 = (w1-16)/2+1; scale/shift NULL = no BN/ReLU on the input.  Persistent,
+ * weight-stationary (weights in registers), one workgroup per CU.  Deterministic. */
+int mia_fe_conv2_fwd(const void* y1, const float* scale, const float* shift, const void* w,
+                     const float* bias, void* y2, int32_t n, int32_t w1, int32_t w2, mia_stream_t stream);
+
+/* Backward-data of the same conv (replaces cuDNN conv2d backward-data for envnet_v2.py:19):
+ *   da1[b][p][ci] = sum_{o,kx: 2o+kx=p} w[co][kx][ci] * dy2[b][o][co]
+ * dy2 (n, w2, 64) bf16, wpar = mia_pack_weight mode 2 of w (2, 32, 8, 64) bf16, da1 (n, w1, 32) bf16.
+ * Both output parities come from one staged dY window.  Deterministic. */
+int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, int32_t n, int32_t w1, int32_t w2,
+                       mia_stream_t stream);
+
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
  * mode 0: OHWI (cout, kh, kw, cin)            — forward operand
  * mode 1: flipped dgrad operand (cin, kh, kw, cout) with ky->kh-1-ky, kx->kw-1-kx

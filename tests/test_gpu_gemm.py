@@ -461,3 +461,50 @@ def test_wgrad8_many_items(cuda):
     K.unpack_ohwi_grad(dW, (c, c, 8, 8), gw)
     torch.cuda.synchronize()
     assert rel(gw, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("n,w1,pre", [(2, 20001, True), (3, 4112, False), (300, 600, True)])
+def test_fe_conv2_fwd(cuda, n, w1, pre):
+    """Persistent weight-stationary EnvNet conv2 forward (1x16, stride 2, 32->64, BN1+ReLU applied
+    while staging) vs float64 conv1d of the same bf16-rounded operands; ragged last item, more
+    items than workgroups (n=300)."""
+    w2 = (w1 - 16) // 2 + 1
+    g = torch.Generator().manual_seed(w1 + n)
+    y1 = torch.randn(n, w1, 32, generator=g).to(torch.bfloat16)
+    W = torch.randn(64, 32, 1, 16, generator=g) * 0.05
+    bias = torch.randn(64, generator=g)
+    sc = torch.rand(32, generator=g) + 0.5
+    sh = torch.randn(32, generator=g) * 0.3
+    wp = K.pack_weight(W.to(cuda), L.BF16, 0)
+    out = torch.full((n * w2, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.fe_conv2_fwd(y1.to(cuda).reshape(-1, 32), sc.to(cuda) if pre else None, sh.to(cuda) if pre else None,
+                   wp, bias.to(cuda), out, n, w1, w2)
+    torch.cuda.synchronize()
+    a = y1.float()
+    if pre:
+        a = torch.relu(a * sc + sh).to(torch.bfloat16).float()
+    ref = F.conv1d(a.double().permute(0, 2, 1), W.to(torch.bfloat16).double()[:, :, 0], bias.double(), stride=2)
+    got = out.float().cpu().view(n, w2, 64).permute(0, 2, 1).double()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max() / ref.abs().max() < 1e-2
+    assert rel(got, ref) < 5e-3
+
+
+@pytest.mark.parametrize("n,w1", [(2, 20001), (3, 4112), (300, 601)])
+def test_fe_conv2_dgrad(cuda, n, w1):
+    """Backward-data of the same conv (both output parities from one staged dY window) vs float64
+    conv_transpose1d; odd and even input widths (the last odd pixel has no parity-1 partner)."""
+    w2 = (w1 - 16) // 2 + 1
+    g = torch.Generator().manual_seed(w1 * 3 + n)
+    dy = torch.randn(n, w2, 64, generator=g).to(torch.bfloat16)
+    W = torch.randn(64, 32, 1, 16, generator=g) * 0.05
+    wpar = K.pack_weight(W.to(cuda), L.BF16, 2)
+    out = torch.full((n * w1, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.fe_conv2_dgrad(dy.to(cuda).reshape(-1, 64), wpar, out, n, w1, w2)
+    torch.cuda.synchronize()
+    ref = F.conv_transpose1d(dy.double().permute(0, 2, 1), W.to(torch.bfloat16).double()[:, :, 0], stride=2)
+    ref = F.pad(ref, (0, w1 - ref.shape[-1]))  # pixels no output window reaches get zero gradient
+    got = out.float().cpu().view(n, w1, 32).permute(0, 2, 1).double()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max() / ref.abs().max() < 1e-2
+    assert rel(got, ref) < 5e-3

@@ -1,0 +1,44 @@
+"""Time the EnvNet frontend conv kernels at the bench shape (B=256, 5 s clips) in isolation.
+    python tools/bench_fe.py"""
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "dl-sound-classification_amd"))
+import torch  # noqa: E402
+
+from src.miaudio import kernels as K  # noqa: E402
+from src.miaudio import lib as L  # noqa: E402
+
+dev = torch.device("cuda:0")
+B, W1 = 256, 110219
+W2 = (W1 - 16) // 2 + 1
+g = torch.Generator(device=dev).manual_seed(0)
+y1 = torch.randn(B * W1, 32, generator=g, device=dev).to(torch.bfloat16)
+dy2 = torch.randn(B * W2, 64, generator=g, device=dev).to(torch.bfloat16)
+W = torch.randn(64, 32, 1, 16, generator=g, device=dev) * 0.05
+w0 = K.pack_weight(W, L.BF16, 0)
+wpar = K.pack_weight(W, L.BF16, 2)
+sc = torch.rand(32, generator=g, device=dev) + 0.5
+sh = torch.randn(32, generator=g, device=dev)
+bias = torch.randn(64, generator=g, device=dev)
+y2 = torch.empty(B * W2, 64, dtype=torch.bfloat16, device=dev)
+da1 = torch.empty(B * W1, 32, dtype=torch.bfloat16, device=dev)
+runs = {
+    "fe_conv2_fwd": lambda: K.fe_conv2_fwd(y1, sc, sh, w0, bias, y2, B, W1, W2),
+    "fe_conv2_dgrad": lambda: K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2),
+}
+byts = {"fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2}
+flop = 2.0 * B * W2 * 64 * 512
+for name, fn in runs.items():
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e9:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s", flush=True)
