@@ -991,9 +991,17 @@ struct TapWArgs {
   int n, h, wx, oh, ow;
   int Z;
   float* ws;
+  // BNB: dy is the gradient w.r.t. relu(bn(y)) and the kernel stages the BN-input gradient
+  //   dy' = gamma*invstd * (mask(y) * dy - dbeta/P - (y - mean) * invstd * dgamma/P)
+  // (the bn_bwd_apply formula, same op order) instead of dy; per-block partial column sums of dy'
+  // (the conv bias gradient) go to dbp[z][32].
+  const bf16* by;
+  const float *bsc, *bsh, *bgamma, *bmean, *binvstd, *bdgamma, *bdbeta;
+  float* dbp;
+  int64_t bP;
 };
 
-template <typename TD, typename TX, int S, int KH, int KW>
+template <typename TD, typename TX, int S, int KH, int KW, bool BNB = false>
 __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
   constexpr int BP = 256;
   constexpr int NS = KW / S;                       // taps per parity sequence
@@ -1024,17 +1032,45 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
 
   u32x4 dreg[DCH];
   float rreg[RCH];
+  u32x4 yreg[BNB ? DCH : 1];
+  uint32_t dok = 0;
+  // BNB: per-thread channel group (t & 3) constants, as bn_bwd_apply computes them
+  float bsc[8], bsh[8], ba[8], bmu[8], bis[8], bmb[8], bmg[8], dbsum[8];
+  if constexpr (BNB) {
+    const float invP = 1.f / (float)g.bP;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = (t & 3) * 8 + i;
+      bsc[i] = g.bsc[ch];
+      bsh[i] = g.bsh[ch];
+      bis[i] = g.binvstd[ch];
+      ba[i] = (g.bgamma ? g.bgamma[ch] : 1.f) * bis[i];
+      bmu[i] = g.bmean[ch];
+      bmb[i] = g.bdbeta[ch] * invP;
+      bmg[i] = g.bdgamma[ch] * invP;
+      dbsum[i] = 0.f;
+    }
+  }
 
   auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
     const int64_t row = c / CPR;
     const int x0 = (int)(c - row * CPR) * BP;
     const int b = (int)(row / g.oh), oy = (int)(row - (int64_t)b * g.oh);
     const TD* src = dys + ((int64_t)row * g.ow + x0) * 32;
+    dok = 0;
 #pragma unroll
     for (int s2 = 0; s2 < DCH; ++s2) {
       const int q = t + NT * s2;
       const int p = q >> 2, cc = q & 3;
       u32x4 v = {0u, 0u, 0u, 0u};
+      if constexpr (BNB) {
+        const bool ok = x0 + p < g.ow;
+        const int64_t off = ok ? ((int64_t)row * g.ow + x0 + p) * 32 + cc * 8 : 0;
+        dreg[s2] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(g.dy) + off);
+        yreg[s2] = *reinterpret_cast<const u32x4*>(g.by + off);
+        dok |= (uint32_t)ok << s2;
+        continue;
+      }
       if (x0 + p < g.ow) {
         if constexpr (sizeof(TD) == 2) {
           v = *reinterpret_cast<const u32x4*>(src + p * 32 + cc * 8);
@@ -1072,7 +1108,32 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
 #pragma unroll
     for (int s2 = 0; s2 < DCH; ++s2) {
       const int q = t + NT * s2;
-      *reinterpret_cast<u32x4*>(dyt + (q >> 2) * 64 + (q & 3) * 16) = dreg[s2];
+      u32x4 v = dreg[s2];
+      if constexpr (BNB) {
+        uint32_t w4[4] = {0u, 0u, 0u, 0u};
+        if ((dok >> s2) & 1u) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float gv[2], yv[2];
+            gv[0] = __uint_as_float(dreg[s2][i] << 16);
+            gv[1] = __uint_as_float(dreg[s2][i] & 0xffff0000u);
+            yv[0] = __uint_as_float(yreg[s2][i] << 16);
+            yv[1] = __uint_as_float(yreg[s2][i] & 0xffff0000u);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int c = 2 * i + h;
+              float d = fmaf(yv[h], bsc[c], bsh[c]) > 0.f ? gv[h] : 0.f;
+              d = ba[c] * (d - bmb[c] - (yv[h] - bmu[c]) * bis[c] * bmg[c]);
+              dbsum[c] += d;
+              gv[h] = d;
+            }
+            const bf16 lo = (bf16)gv[0], hi = (bf16)gv[1];
+            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          }
+        }
+        v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+      }
+      *reinterpret_cast<u32x4*>(dyt + (q >> 2) * 64 + (q & 3) * 16) = v;
     }
 #pragma unroll
     for (int s2 = 0; s2 < RCH; ++s2) {
@@ -1166,6 +1227,20 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
   float* dst = g.ws + (int64_t)z * 32 * 64;
   for (int e = t; e < 32 * 64; e += NT)
     dst[e] = red[e] + red[2048 + e] + red[4096 + e] + red[6144 + e];
+  if constexpr (BNB) {
+    // bias-gradient partial of this block: channel c = (t&3)*8 + i summed over the 64 threads of
+    // its group in thread order (deterministic)
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[t * 8 + i] = dbsum[i];
+    __syncthreads();
+    if (t < 32) {
+      const int cg = t >> 3, i = t & 7;
+      float acc_b = 0.f;
+      for (int k = 0; k < NT / 4; ++k) acc_b += red[(k * 4 + cg) * 8 + i];
+      g.dbp[(int64_t)z * 32 + t] = acc_b;
+    }
+  }
 }
 
 // 1-channel conv wgrad (path 3): A = dY [P][32] as RC, B = CONVROW/RC with c == 1 (any stride
@@ -1187,9 +1262,9 @@ bool tapwgrad_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N,
   return true;
 }
 
-template <typename TD, typename TX, int S, int KH, int KW>
+template <typename TD, typename TX, int S, int KH, int KW, bool BNB = false>
 hipError_t tapwgrad_launch(const TapWArgs& r, hipStream_t s) {
-  tapwgrad_kernel<TD, TX, S, KH, KW><<<(unsigned)r.Z, NT, 0, s>>>(r);
+  tapwgrad_kernel<TD, TX, S, KH, KW, BNB><<<(unsigned)r.Z, NT, 0, s>>>(r);
   return hipGetLastError();
 }
 
@@ -1718,7 +1793,7 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     return 0;
   }
   if (workspace && tapwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) {
-    TapWArgs r;
+    TapWArgs r{};
     r.x = reinterpret_cast<const char*>(B->ptr);
     r.dy = reinterpret_cast<const char*>(A->ptr);
     r.n = B->n; r.h = B->h; r.wx = B->w * B->c; r.oh = B->oh; r.ow = B->ow;
@@ -1803,6 +1878,42 @@ extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
   if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;
   if (tapwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 3;
+  return 0;
+}
+
+extern "C" int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int32_t n, int32_t t,
+                                     const float* scale, const float* shift, const float* gamma, const float* mean,
+                                     const float* invstd, const float* dgamma, const float* dbeta, float* dw,
+                                     float* dbias, void* workspace, int32_t split, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && dact && y1 && scale && shift && mean && invstd && dgamma && dbeta && dw && dbias && workspace,
+                "fe_conv1_wgrad_bn: null pointer");
+  MIA_CHECK_ARG(n > 0 && t >= 64 && t % 2 == 0 && split > 0, "fe_conv1_wgrad_bn: bad sizes");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(dact) | reinterpret_cast<uintptr_t>(y1)) & 15) == 0,
+                "fe_conv1_wgrad_bn: dact / y1 must be 16-byte aligned");
+  const int w1 = (t - 64) / 2 + 1;
+  TapWArgs r{};
+  r.x = reinterpret_cast<const char*>(x);
+  r.dy = reinterpret_cast<const char*>(dact);
+  r.n = n; r.h = 1; r.wx = t; r.oh = 1; r.ow = w1;
+  r.Z = split;
+  r.ws = reinterpret_cast<float*>(workspace);
+  r.by = reinterpret_cast<const bf16*>(y1);
+  r.bsc = scale; r.bsh = shift; r.bgamma = gamma; r.bmean = mean; r.binvstd = invstd;
+  r.bdgamma = dgamma; r.bdbeta = dbeta;
+  r.dbp = r.ws + (int64_t)split * 32 * 64;
+  r.bP = (int64_t)n * w1;
+  hipStream_t s = as_stream(stream);
+  hipError_t err = tapwgrad_launch<bf16, float, 2, 1, 64, true>(r, s);
+  if (err != hipSuccess) return mia::fail(-(int)err, "fe_conv1_wgrad_bn launch: %s", hipGetErrorString(err));
+  EpiDev e{};
+  e.ptr = reinterpret_cast<char*>(dw); e.dtype = MIA_F32; e.act = MIA_ACT_NONE; e.ldc = 64; e.alpha = 1.f;
+  e.act_scale = 1.f;
+  launch_splitk_reduce(r.ws, split, 32, 64, e, s);
+  EpiDev eb{};
+  eb.ptr = reinterpret_cast<char*>(dbias); eb.dtype = MIA_F32; eb.act = MIA_ACT_NONE; eb.ldc = 32; eb.alpha = 1.f;
+  eb.act_scale = 1.f;
+  launch_splitk_reduce(r.dbp, split, 1, 32, eb, s);
+  MIA_LAUNCH_CHECK("fe_conv1_wgrad_bn reduce");
   return 0;
 }
 

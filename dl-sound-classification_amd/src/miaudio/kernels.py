@@ -30,10 +30,6 @@ def _s():
     return L.stream_ptr()
 
 
-def _ptr(t):
-    return None if t is None else t.data_ptr()
-
-
 # ------------------------------------------------------------------------------------ GEMM
 def dense(t: torch.Tensor, layout: int, rows: int, cols: int, ld: int | None = None,
           pre: int = L.PRE_NONE, scale=None, shift=None, dtype: int | None = None) -> L.MiaOperand:
@@ -304,7 +300,7 @@ def fe_conv2_fwd(y1: torch.Tensor, scale, shift, w: torch.Tensor, bias, y2: torc
     assert y1.is_contiguous() and y2.is_contiguous() and w.is_contiguous()
     flop = 2.0 * n * w2 * 64 * 512
     with probe(tag or "", flop, y1.numel() * 2 + y2.numel() * 2):
-        L.check(L.load().mia_fe_conv2_fwd(y1.data_ptr(), _ptr(scale), _ptr(shift), w.data_ptr(), _ptr(bias),
+        L.check(L.load().mia_fe_conv2_fwd(y1.data_ptr(), L.ptr(scale), L.ptr(shift), w.data_ptr(), L.ptr(bias),
                                           y2.data_ptr(), n, w1, w2, _s()), "mia_fe_conv2_fwd")
 
 
@@ -319,6 +315,26 @@ def fe_conv2_dgrad(dy2: torch.Tensor, wpar: torch.Tensor, da1: torch.Tensor, n: 
     with probe(tag or "", flop, dy2.numel() * 2 + da1.numel() * 2):
         L.check(L.load().mia_fe_conv2_dgrad(dy2.data_ptr(), wpar.data_ptr(), da1.data_ptr(), n, w1, w2, _s()),
                 "mia_fe_conv2_dgrad")
+
+
+def fe_conv1_wgrad_bn(x: torch.Tensor, dact: torch.Tensor, y1: torch.Tensor, n: int, t: int, gamma, bn: BNState,
+                      dgamma: torch.Tensor, dbeta: torch.Tensor, dw: torch.Tensor, dbias: torch.Tensor,
+                      tag: str | None = None):
+    """EnvNet conv1 weight/bias gradient with BN1+ReLU backward fused into the dY staging (bf16):
+    x f32 (n, t) waveform, dact = dL/d relu(bn1(y1)) and y1 bf16 (n*w1, 32) -> dw f32 (32, 64),
+    dbias f32 (32)."""
+    w1 = (t - 64) // 2 + 1
+    assert dact.dtype == torch.bfloat16 and y1.dtype == torch.bfloat16 and x.dtype == torch.float32
+    assert dact.numel() == n * w1 * 32 and y1.numel() == n * w1 * 32 and x.numel() == n * t
+    assert dw.numel() == 32 * 64 and dw.dtype == torch.float32 and dbias.numel() == 32
+    split = 512
+    ws = workspace(split * (32 * 64 + 32) * 4, x.device, "tapw")
+    flop = 2.0 * n * w1 * 32 * 64
+    with probe(tag or "", flop, (dact.numel() + y1.numel()) * 2 + x.numel() * 4):
+        L.check(L.load().mia_fe_conv1_wgrad_bn(
+            x.data_ptr(), dact.data_ptr(), y1.data_ptr(), n, t, bn.scale.data_ptr(), bn.shift.data_ptr(),
+            L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
+            dw.data_ptr(), dbias.data_ptr(), ws.data_ptr(), split, _s()), "mia_fe_conv1_wgrad_bn")
 
 
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:

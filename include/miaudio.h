@@ -210,6 +210,19 @@ int mia_fe_conv2_fwd(const void* y1, const float* scale, const float* shift, con
 int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, int32_t n, int32_t w1, int32_t w2,
                        mia_stream_t stream);
 
+/* EnvNet-v2 conv1 weight + bias gradient with the BatchNorm1+ReLU backward fused into the operand
+ * staging (reference src/models/envnet_v2.py:15-17 Conv2d(1, 32, (1, 64), stride (1, 2)) -> BN ->
+ * ReLU; replaces cuDNN conv2d backward-weight plus the BN backward's elementwise pass):
+ *   g[p][c]  = gamma[c]*invstd[c] * (mask * dact[p][c] - dbeta[c]/P - (y1[p][c]-mean[c])*invstd[c]*dgamma[c]/P),
+ *              mask = y1[p][c]*scale[c] + shift[c] > 0,  P = n*w1,  w1 = (t-64)/2+1
+ *   dw[c][k] = sum_{b,o} g[b,o][c] * x[b][2o+k]   (k < 64),   dbias[c] = sum_p g[p][c]
+ * x f32 (n, t); dact, y1 bf16 (n, w1, 32); dgamma/dbeta from mia_bn_relu_bwd_reduce; dw f32 (32, 64);
+ * workspace >= split*(32*64+32) floats.  Deterministic (fixed-order split-K reduce). */
+int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int32_t n, int32_t t,
+                          const float* scale, const float* shift, const float* gamma, const float* mean,
+                          const float* invstd, const float* dgamma, const float* dbeta, float* dw,
+                          float* dbias, void* workspace, int32_t split, mia_stream_t stream);
+
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
  * mode 0: OHWI (cout, kh, kw, cin)            — forward operand
  * mode 1: flipped dgrad operand (cin, kh, kw, cout) with ky->kh-1-ky, kx->kw-1-kx

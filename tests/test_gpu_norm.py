@@ -5,6 +5,7 @@ import torch
 import torch.nn.functional as F
 
 from src.miaudio import kernels as K
+from src.miaudio import lib as L
 
 pytestmark = pytest.mark.gpu
 
@@ -116,3 +117,44 @@ def test_bn_relu_bwd_masked_apply(cuda, dt):
     assert torch.equal(dx, dx_ref)
     # dbias sums the f32 values before the store rounds them (bf16: compare against the rounded sum loosely)
     assert rel(dbias, dx_ref.double().sum(0)) < (1e-4 if dt == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("n,t", [(3, 220500), (2, 9000)])
+def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
+    """conv1 weight/bias gradient with the BN1+ReLU backward fused into its dY staging == the
+    unfused path (bn_relu_bwd_apply -> bf16 dS1 -> tap wgrad GEMM): identical bf16 dS1 values, so
+    dW agrees to f32 summation order; and within bf16 tolerance of a float64 restatement."""
+    w1 = (t - 64) // 2 + 1
+    P = n * w1
+    g = torch.Generator(device=cuda).manual_seed(t + n)
+    x = torch.randn(n, t, generator=g, device=cuda) * 0.1
+    y1 = (torch.randn(P, 32, generator=g, device=cuda) * 0.7 + 0.2).to(torch.bfloat16)
+    da = (torch.randn(P, 32, generator=g, device=cuda) * 1e-3).to(torch.bfloat16)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda) * 0.1
+    bn = K.bn_fwd_stats(y1, P, 32, gamma, beta, None, None, 0.1, 1e-5, True)
+    dg, db = K.bn_relu_bwd_reduce(da, None, y1, P, 32, bn)
+    dw = torch.empty(32, 64, device=cuda)
+    dbias = torch.empty(32, device=cuda)
+    K.fe_conv1_wgrad_bn(x, da, y1, n, t, gamma, bn, dg, db, dw, dbias)
+    # unfused reference path
+    dx = torch.empty_like(da)
+    dbias_u = torch.empty(32, device=cuda)
+    K.bn_relu_bwd_apply(da, y1, dx, P, 32, gamma, bn, dg, db, dbias_u)
+    dw_u = torch.empty(32, 64, device=cuda)
+    K.gemm(K.dense(dx, L.RC, P, 32), K.conv(x, L.RC, n, 1, t // 2, 2, 1, w1, 1, 32, row_kind=True),
+           K.epilogue(dw_u, 64), 32, 64, P, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(dw, dw_u) < 1e-5
+    scale_b = dx.float().abs().sum(0).max()
+    assert (dbias - dbias_u).abs().max() < 1e-5 * scale_b
+    # float64 restatement
+    y = y1.double()
+    z = y * bn.scale.double() + bn.shift.double()
+    dz = torch.where(z > 0, da.double(), torch.zeros_like(z))
+    xhat = (y - bn.mean.double()) * bn.invstd.double()
+    mdz, mdzx = dz.mean(0), (dz * xhat).mean(0)
+    d64 = gamma.double() * bn.invstd.double() * (dz - mdz - xhat * mdzx)
+    cols = x.double().unfold(1, 64, 2)  # (n, w1, 64)
+    ref = torch.einsum("npc,npk->ck", d64.view(n, w1, 32), cols)
+    assert rel(dw.double(), ref) < 1e-2
