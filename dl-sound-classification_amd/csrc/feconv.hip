@@ -32,6 +32,7 @@ constexpr int FE_N = 64;    // output channels
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+
 template <int CIN, int KW, int S>
 struct FeCfg {
   static constexpr int CG = CIN / 8;                    // 16-B chunks per pixel
@@ -254,6 +255,210 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   }
 }
 
+// ---------------------------------------------------------------- conv2 weight gradient
+//   dW[co][kx*32 + ci] = sum_{b,o} dy2[b][o][co] * relu(bn1(y1))[b][2o+kx][ci]      (64 x 512, K = pixels)
+// Persistent, gradient-stationary: one 8-wave workgroup per CU walks (clip, 128-pixel) items and
+// keeps its 64 x 512 partial sum in registers (wave w: kernel taps kx = 2w, 2w+1 for all 64 output
+// channels, 4 tiles = 64 VGPRs) for the whole launch; per item the dY tile [128 px][64 co] and the
+// BN+ReLU'd input window [270 px][32 ci] (even/odd pixel split, so the stride-2 taps are
+// consecutive slots) go through a double-buffered LDS stage with two register sets of raw loads in
+// flight (items k+1, k+2), and both MFMA operands are transposed LDS reads (ds_read_b64_tr_b16).
+// Every input byte is read once per item (window overlap 14 px); one f32 slab per workgroup, summed
+// by the split-K reducer.
+constexpr int FW_NT = 512;
+constexpr int FW_BP = 128;
+
+struct FwArgs {
+  const bf16* dy;     // (n, wout, 64)
+  const bf16* x;      // (n, win, 32)
+  const float* ps;    // BN1 scale/shift (+ReLU) on x, or null
+  const float* pt;
+  int n, win, wout, nitem;
+  float* ws;          // slab [blockIdx.x][64][512]
+};
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 fw_tr(const char* p0, int stride) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * stride));
+  const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <bool PRE>
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void fe_wgrad_kernel(FwArgs g) {
+  constexpr int C = 32, KW = 16;
+  constexpr int WPX = (FW_BP - 1) * 2 + KW;   // 270 window pixels
+  constexpr int HALF = (WPX + 1) / 2;         // 135: odd pixels start here
+  constexpr int PSB = 64;                     // window pixel stride (conflict-free transposed reads)
+  constexpr int DSB = 192;                    // dY pixel stride (48 dwords: 4 rows hit disjoint banks)
+  constexpr int WBY = 2 * HALF * PSB;
+  constexpr int DBY = FW_BP * DSB;
+  constexpr int BUF = WBY + DBY;
+  constexpr int WCH = WPX * 4;                // 16-B window chunks per item (1080)
+  constexpr int WL = (WCH + FW_NT - 1) / FW_NT;  // 3
+  constexpr int DL = FW_BP * 8 / FW_NT;          // 2
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) float spre[2][C];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int items = g.n * g.nitem;
+  if (PRE && t < C) {
+    spre[0][t] = g.ps[t];
+    spre[1][t] = g.pt[t];
+  }
+  const int cgw = t & 3;   // window chunk: 8 input channels
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(g.x), (short)0, (int)((int64_t)g.n * g.win * C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(g.dy), (short)0, (int)((int64_t)g.n * g.wout * 64 * 2), 0x00020000);
+
+  u32x4 wa[WL], wb[WL], da[DL], db[DL];
+  auto load = [&](int it, u32x4 (&w)[WL], u32x4 (&d)[DL]) __attribute__((always_inline)) {
+    it = it < items ? it : items - 1;
+    const int b = it / g.nitem;
+    const int o0 = (it - b * g.nitem) * FW_BP;
+#pragma unroll
+    for (int s = 0; s < WL; ++s) {
+      const int q = t + FW_NT * s;
+      const int p = q >> 2;
+      const int ix = 2 * o0 + p;
+      const bool ok = q < WCH && ix < g.win;
+      const unsigned off = ok ? (unsigned)((b * g.win + ix) * 4 + cgw) * 16u : 0x80000000u;
+      w[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+#pragma unroll
+    for (int s = 0; s < DL; ++s) {
+      const int q = t + FW_NT * s;
+      const int p = q >> 3, cc = q & 7;
+      const bool ok = o0 + p < g.wout;
+      const unsigned off = ok ? (unsigned)((b * g.wout + o0 + p) * 8 + cc) * 16u : 0x80000000u;
+      d[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
+    }
+  };
+  // zero-filled raw chunks (padding) must stay zero after the pre-op: the window tail past the
+  // clip reads zeros, and relu(0*sc + sh) != 0, so the valid bit is recomputed from the item here
+  auto store = [&](int it, int buf, const u32x4 (&w)[WL], const u32x4 (&d)[DL]) __attribute__((always_inline)) {
+    it = it < items ? it : items - 1;
+    const int b = it / g.nitem;
+    const int o0 = (it - b * g.nitem) * FW_BP;
+    char* win = smem + buf * BUF;
+    char* dyt = win + WBY;
+    float sc[8], sh[8];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&spre[0][cgw * 8 + 4 * h]);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(&spre[1][cgw * 8 + 4 * h]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { sc[4 * h + q] = a[q]; sh[4 * h + q] = c[q]; }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < WL; ++s) {
+      const int q = t + FW_NT * s;
+      const int p = q >> 2;
+      if (q < WCH) {
+        u32x4 v = w[s];
+        if constexpr (PRE) {
+          if (2 * o0 + p < g.win) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float lo = fmaxf(fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
+              const float hi = fmaxf(fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
+              const bf16 bl = (bf16)lo, bh = (bf16)hi;
+              w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) |
+                      ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+            }
+            v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+          }
+        }
+        const int slot = (p & 1) * HALF + (p >> 1);
+        *reinterpret_cast<u32x4*>(win + slot * PSB + cgw * 16) = v;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < DL; ++s) {
+      const int q = t + FW_NT * s;
+      *reinterpret_cast<u32x4*>(dyt + (q >> 3) * DSB + (q & 7) * 16) = d[s];
+    }
+  };
+
+  f32x16 acc[2][2];  // [mt][j]: output channels mt*32.., taps kx = 2*wave + j
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int i16 = lane & 15, gq = lane >> 4;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* win = smem + buf * BUF;
+    const char* dyt = win + WBY;
+#pragma unroll
+    for (int ks = 0; ks < FW_BP / 16; ++ks) {
+      const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        fa[mt] = fw_tr(dyt + kr * DSB + (mt * 32 + 16 * (gq & 1) + 4 * (i16 & 3)) * 2, DSB);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int kx = 2 * wave + j;
+        const int ci = 16 * (gq & 1) + 4 * (i16 & 3);
+        const int slot = (kx & 1) * HALF + kr + (kx >> 1);
+        fb[j] = fw_tr(win + slot * PSB + ci * 2, PSB);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mt][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mt], fb[j], acc[mt][j], 0, 0, 0);
+    }
+  };
+
+  const int G = gridDim.x;
+  int item = blockIdx.x;
+  if (item < items) {
+    load(item, wa, da);
+    load(item + G, wb, db);
+    __syncthreads();  // spre visible
+    store(item, 0, wa, da);
+    __syncthreads();
+    for (;;) {
+      load(item + 2 * G, wa, da);
+      compute(0);
+      store(item + G, 1, wb, db);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      item += G;
+      if (item >= items) break;
+      load(item + 2 * G, wb, db);
+      compute(1);
+      store(item + G, 0, wa, da);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      item += G;
+      if (item >= items) break;
+    }
+  }
+  // slab [64][512]: column n = kx*32 + ci
+  float* dst = g.ws + (int64_t)blockIdx.x * 64 * 512;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = (2 * wave + j) * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        dst[(int64_t)m * 512 + n] = acc[mt][j][r];
+      }
+    }
+}
+
 int fe_grid(int items) {
   static int ncu = 0;
   if (!ncu) {
@@ -267,6 +472,21 @@ int fe_grid(int items) {
 
 // clips per launch so that one launch's input stays below 2 GB (32-bit buffer offsets)
 int fe_clips_per_launch(int64_t clip_bytes) { return (int)(((1ll << 31) - 1) / clip_bytes); }
+
+int fe_grid1(int items) {  // one workgroup per CU
+  const int two = fe_grid(1 << 30);
+  return items < two / 2 ? items : two / 2;
+}
+
+// dw[e] = sum over slabs (fixed order: deterministic)
+__global__ __launch_bounds__(256) void fw_reduce_kernel(const float* __restrict__ ws, int slabs, int len,
+                                                        float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= len) return;
+  float acc = 0.f;
+  for (int k = 0; k < slabs; ++k) acc += ws[(int64_t)k * len + e];
+  out[e] = acc;
+}
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
@@ -312,5 +532,37 @@ extern "C" int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, 
     feconv_kernel<64, 8, 1, false><<<fe_grid(nc * a.nitem), FE_NT, 0, as_stream(stream)>>>(a);
     MIA_LAUNCH_CHECK("fe_conv2_dgrad");
   }
+  return 0;
+}
+
+extern "C" int mia_fe_conv2_wgrad(const void* dy2, const void* y1, const float* scale, const float* shift,
+                                  float* dw, int32_t n, int32_t w1, int32_t w2, void* workspace, int64_t ws_bytes,
+                                  mia_stream_t stream) {
+  MIA_CHECK_ARG(dy2 && y1 && dw && workspace && n > 0 && w1 >= 16, "fe_conv2_wgrad: bad arguments");
+  MIA_CHECK_ARG(!scale == !shift, "fe_conv2_wgrad: scale and shift go together");
+  MIA_CHECK_ARG(w2 == (w1 - 16) / 2 + 1, "fe_conv2_wgrad: w2 must be (w1-16)/2+1 (got w1=%d w2=%d)", w1, w2);
+  MIA_CHECK_ARG(aligned16(dy2) && aligned16(y1), "fe_conv2_wgrad: operands must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int per = fe_clips_per_launch((int64_t)w1 * 32 * 2);
+  MIA_CHECK_ARG(per > 0, "fe_conv2_wgrad: one clip exceeds 2 GB");
+  const int nitem = (int)cdiv(w2, FW_BP);
+  // one slab per workgroup of every launch, summed by one reduce at the end
+  int slabs = 0;
+  for (int c = 0; c < n; c += per) slabs += fe_grid1(((n - c) < per ? (n - c) : per) * nitem);
+  MIA_CHECK_ARG((int64_t)slabs * 64 * 512 * 4 <= ws_bytes, "fe_conv2_wgrad: workspace too small (%lld B needed)",
+                (long long)slabs * 64 * 512 * 4);
+  int slab0 = 0;
+  for (int c = 0; c < n; c += per) {
+    const int nc = n - c < per ? n - c : per;
+    FwArgs a{reinterpret_cast<const bf16*>(dy2) + (int64_t)c * w2 * 64, reinterpret_cast<const bf16*>(y1) + (int64_t)c * w1 * 32,
+             scale, shift, nc, w1, w2, nitem, reinterpret_cast<float*>(workspace) + (int64_t)slab0 * 64 * 512};
+    const int grid = fe_grid1(nc * nitem);
+    if (scale) fe_wgrad_kernel<true><<<grid, FW_NT, 0, s>>>(a);
+    else fe_wgrad_kernel<false><<<grid, FW_NT, 0, s>>>(a);
+    MIA_LAUNCH_CHECK("fe_conv2_wgrad");
+    slab0 += grid;
+  }
+  fw_reduce_kernel<<<64 * 512 / 256, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), slabs, 64 * 512, dw);
+  MIA_LAUNCH_CHECK("fe_conv2_wgrad reduce");
   return 0;
 }

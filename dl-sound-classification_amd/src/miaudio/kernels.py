@@ -317,6 +317,21 @@ def fe_conv2_dgrad(dy2: torch.Tensor, wpar: torch.Tensor, da1: torch.Tensor, n: 
                 "mia_fe_conv2_dgrad")
 
 
+def fe_conv2_wgrad(dy2: torch.Tensor, y1: torch.Tensor, scale, shift, dw: torch.Tensor, n: int, w1: int, w2: int,
+                   tag: str | None = None):
+    """Weight gradient of EnvNet conv2 (bf16 operands): dy2 (n*w2, 64), y1 (n*w1, 32) with BN1
+    scale/shift (+ReLU) applied while staging -> dw f32 (64, 16*32) in OHWI order."""
+    assert dy2.dtype == torch.bfloat16 and y1.dtype == torch.bfloat16 and dw.dtype == torch.float32
+    assert dy2.numel() == n * w2 * 64 and y1.numel() == n * w1 * 32 and dw.numel() == 64 * 512
+    nlaunch = -(-(n * w1 * 64) // (2 ** 31 - 1)) + 1
+    nbytes = 512 * nlaunch * 64 * 512 * 4
+    ws = workspace(nbytes, dy2.device, "fw")
+    flop = 2.0 * n * w2 * 64 * 512
+    with probe(tag or "", flop, (dy2.numel() + y1.numel()) * 2):
+        L.check(L.load().mia_fe_conv2_wgrad(dy2.data_ptr(), y1.data_ptr(), L.ptr(scale), L.ptr(shift), dw.data_ptr(),
+                                            n, w1, w2, ws.data_ptr(), ws.numel(), _s()), "mia_fe_conv2_wgrad")
+
+
 def fe_conv1_wgrad_bn(x: torch.Tensor, dact: torch.Tensor, y1: torch.Tensor, n: int, t: int, gamma, bn: BNState,
                       dgamma: torch.Tensor, dbeta: torch.Tensor, dw: torch.Tensor, dbias: torch.Tensor,
                       tag: str | None = None):

@@ -349,10 +349,13 @@ class EnvNetFunction(torch.autograd.Function):
                                  dbias2)
         grads[5] = dbias2
         dW2 = torch.empty(64, 512, dtype=torch.float32, device=dev)
-        K.gemm(K.dense(dy2, L.RC, P2, 64),
-               K.conv(s["y1"], L.RC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU,
-                      scale=s["bn1"].scale, shift=s["bn1"].shift),
-               K.epilogue(dW2, 512), 64, 512, P2, cd, tag="conv2.wgrad")
+        if cd == L.BF16:
+            K.fe_conv2_wgrad(dy2, s["y1"], s["bn1"].scale, s["bn1"].shift, dW2, B, W1, W2, tag="conv2.wgrad")
+        else:
+            K.gemm(K.dense(dy2, L.RC, P2, 64),
+                   K.conv(s["y1"], L.RC, B, 1, W1, 32, 1, W2, 1, 16, sw=2, pre=L.PRE_AFFINE_RELU,
+                          scale=s["bn1"].scale, shift=s["bn1"].shift),
+                   K.epilogue(dW2, 512), 64, 512, P2, cd, tag="conv2.wgrad")
         gw2 = torch.empty_like(p[4])
         K.unpack_ohwi_grad(dW2, p[4].shape, gw2)
         grads[4] = gw2

@@ -210,6 +210,14 @@ int mia_fe_conv2_fwd(const void* y1, const float* scale, const float* shift, con
 int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, int32_t n, int32_t w1, int32_t w2,
                        mia_stream_t stream);
 
+/* Weight gradient of the same conv (replaces cuDNN conv2d backward-weight for envnet_v2.py:19):
+ *   dw[co][kx*32+ci] = sum_{b,o} dy2[b][o][co] * relu(y1[b][2o+kx][ci]*scale[ci] + shift[ci])
+ * dy2 (n, w2, 64), y1 (n, w1, 32) bf16; dw f32 (64, 16*32) (OHWI); scale/shift NULL = no pre-op.
+ * workspace: one 128 KB f32 slab per workgroup (<= #CU per 2 GB of y1).  Deterministic. */
+int mia_fe_conv2_wgrad(const void* dy2, const void* y1, const float* scale, const float* shift, float* dw,
+                       int32_t n, int32_t w1, int32_t w2, void* workspace, int64_t ws_bytes,
+                       mia_stream_t stream);
+
 /* EnvNet-v2 conv1 weight + bias gradient with the BatchNorm1+ReLU backward fused into the operand
  * staging (reference src/models/envnet_v2.py:15-17 Conv2d(1, 32, (1, 64), stride (1, 2)) -> BN ->
  * ReLU; replaces cuDNN conv2d backward-weight plus the BN backward's elementwise pass):

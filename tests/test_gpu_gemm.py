@@ -508,3 +508,28 @@ def test_fe_conv2_dgrad(cuda, n, w1):
     assert torch.isfinite(got).all()
     assert (got - ref).abs().max() / ref.abs().max() < 1e-2
     assert rel(got, ref) < 5e-3
+
+
+@pytest.mark.parametrize("n,w1,pre", [(2, 20001, True), (3, 4112, False), (300, 601, True)])
+def test_fe_conv2_wgrad(cuda, n, w1, pre):
+    """Gradient-stationary EnvNet conv2 weight gradient (BN1+ReLU applied while staging the input
+    window) vs a float64 restatement on the same bf16-rounded operands; ragged last item, more
+    items than workgroups (n=300)."""
+    w2 = (w1 - 16) // 2 + 1
+    g = torch.Generator().manual_seed(w1 * 7 + n)
+    y1 = torch.randn(n, w1, 32, generator=g).to(torch.bfloat16)
+    dy = (torch.randn(n, w2, 64, generator=g) * 0.1).to(torch.bfloat16)
+    sc = torch.rand(32, generator=g) + 0.5
+    sh = torch.randn(32, generator=g) * 0.3
+    dw = torch.full((64, 512), float("nan"), device=cuda)
+    K.fe_conv2_wgrad(dy.to(cuda).reshape(-1, 64), y1.to(cuda).reshape(-1, 32), sc.to(cuda) if pre else None,
+                     sh.to(cuda) if pre else None, dw, n, w1, w2)
+    torch.cuda.synchronize()
+    a = y1.float()
+    if pre:
+        a = torch.relu(a * sc + sh).to(torch.bfloat16).float()
+    cols = a.double().unfold(1, 16, 2)  # (n, w2, 32, 16): [b][o][ci][kx]
+    ref = torch.einsum("boc,boik->cki", dy.double(), cols)  # [co][kx][ci]
+    got = dw.double().cpu().view(64, 16, 32)
+    assert torch.isfinite(got).all()
+    assert rel(got, ref) < 1e-3
