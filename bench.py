@@ -191,7 +191,7 @@ def main():
         ddp = GradAllReducer(model, world) if world > 1 else None
         step = envnet_step_fn(model, opt, wav, labels, g, world, ddp)
         flop_per_clip = ENVNET_FLOP_PER_CLIP
-        probe_tags = (args.probe.split(",") if args.probe else ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv2.fwd", "conv2.dgrad", "conv2.wgrad"])
+        probe_tags = (args.probe.split(",") if args.probe else ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv1.fwd", "conv1.wgrad", "conv2.fwd", "conv2.dgrad", "conv2.wgrad"])
         probe_tags += ["frontend.fwd", "frontend.bwd"]
         workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
     else:

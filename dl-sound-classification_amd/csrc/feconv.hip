@@ -255,6 +255,137 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   }
 }
 
+// ---------------------------------------------------------------- conv1 forward + BN1 statistics
+//   y1[b][o][c] = bias[c] + sum_{k<64} w[c][k] * x[b][2o+k]        (envnet_v2.py:15, 1 -> 32 channels)
+// Wave-persistent (no LDS, no barriers): a wave owns (clip, 32-pixel) items; the 4 weight fragments
+// (32 channels x 64 taps) stay in registers as the MFMA A operand, the Toeplitz B operand is read
+// straight from the f32 waveform (8 consecutive samples per lane and k-step, L1-resident: the
+// 126-sample segment of an item is shared by all its lanes) and rounded to bf16, and the next
+// item's samples are in flight while the current one computes.  After the half swap each lane holds
+// 16 channels of one pixel: 2 x 16-B stores, and the BN1 batch statistics of the stored (bf16)
+// values are accumulated on the fly about K[c] = bias[c] (the waveform is zero-mean, so the
+// shifted sums are well conditioned) -> per-wave partial [C][2] -> bn finalize in double.
+struct F1Args {
+  const float* x;     // (n, t)
+  const bf16* w;      // (32, 64)
+  const float* bias;  // (32)
+  bf16* y;            // (n, w1, 32)
+  float* part;        // [waves][32][2] shifted sums, or null
+  int n, t, w1, nitem;
+};
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int items = g.n * g.nitem;
+  bf16x8 wa[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) wa[ks] = *reinterpret_cast<const bf16x8*>(g.w + (lane & 31) * 64 + ks * 16 + 8 * (lane >> 5));
+  const int c0 = 8 * (lane >> 5);
+  float bv[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { bv[i] = g.bias[c0 + i]; bv[8 + i] = g.bias[c0 + 16 + i]; }
+  float s1[16], s2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 xa[16], xb[16];
+  auto load = [&](int it, f32x2 (&r)[16]) __attribute__((always_inline)) {
+    it = it < items ? it : items - 1;
+    const int b = it / g.nitem;
+    const int o = (it - b * g.nitem) * 32 + (lane & 31);
+    const int64_t base = o < g.w1 ? (int64_t)b * g.t + 2 * o + 8 * (lane >> 5) : 0;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) r[ks * 4 + h] = *reinterpret_cast<const f32x2*>(g.x + base + 16 * ks + 2 * h);
+  };
+  auto run = [&](int it, const f32x2 (&r)[16]) __attribute__((always_inline)) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 fb;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        fb[2 * h] = (bf16)r[ks * 4 + h][0];
+        fb[2 * h + 1] = (bf16)r[ks * 4 + h][1];
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ks], fb, acc, 0, 0, 0);
+    }
+    float v[16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float lo = acc[8 * h + j], hi = acc[8 * h + 4 + j];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+        v[8 * h + j] = __builtin_bit_cast(float, (unsigned)sw[0]);
+        v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)sw[1]);
+      }
+    const int b = it / g.nitem;
+    const int o = (it - b * g.nitem) * 32 + (lane & 31);
+    if (o < g.w1) {
+      bf16* dst = g.y + ((int64_t)b * g.w1 + o) * 32 + c0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 8 * h + 2 * i;
+          const bf16 lo = (bf16)(v[e] + bv[e]), hi = (bf16)(v[e + 1] + bv[e + 1]);
+          w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          if constexpr (STATS) {
+            const float d0 = (float)lo - bv[e], d1 = (float)hi - bv[e + 1];
+            s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
+            s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
+          }
+        }
+        *reinterpret_cast<u32x4*>(dst + 16 * h) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+      }
+    }
+  };
+
+  int it = gw;
+  if (it < items) {
+    load(it, xa);
+    for (;;) {
+      load(it + nw, xb);
+      run(it, xa);
+      it += nw;
+      if (it >= items) break;
+      load(it + nw, xa);
+      run(it, xb);
+      it += nw;
+      if (it >= items) break;
+    }
+  }
+  if constexpr (STATS) {
+    // sum over the 32 lanes that hold the same channels (lane bit 5 fixed), fixed butterfly order
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int m = 1; m < 32; m <<= 1) {
+        s1[i] += __shfl_xor(s1[i], m, 64);
+        s2[i] += __shfl_xor(s2[i], m, 64);
+      }
+    }
+    if ((lane & 31) == 0) {
+      float* dst = g.part + (int64_t)gw * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dst[(c0 + i) * 2] = s1[i];
+        dst[(c0 + i) * 2 + 1] = s2[i];
+        dst[(c0 + 16 + i) * 2] = s1[8 + i];
+        dst[(c0 + 16 + i) * 2 + 1] = s2[8 + i];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- conv2 weight gradient
 //   dW[co][kx*32 + ci] = sum_{b,o} dy2[b][o][co] * relu(bn1(y1))[b][2o+kx][ci]      (64 x 512, K = pixels)
 // Persistent, gradient-stationary: one 8-wave workgroup per CU walks (clip, 128-pixel) items and
@@ -564,5 +695,21 @@ extern "C" int mia_fe_conv2_wgrad(const void* dy2, const void* y1, const float* 
   }
   fw_reduce_kernel<<<64 * 512 / 256, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), slabs, 64 * 512, dw);
   MIA_LAUNCH_CHECK("fe_conv2_wgrad reduce");
+  return 0;
+}
+
+extern "C" int mia_fe_conv1_fwd(const float* x, const void* w, const float* bias, void* y1, float* partial,
+                                int32_t nwaves, int32_t n, int32_t t, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && w && bias && y1 && n > 0 && t >= 64 && t % 2 == 0, "fe_conv1_fwd: bad arguments");
+  MIA_CHECK_ARG(nwaves > 0 && nwaves % 4 == 0, "fe_conv1_fwd: nwaves must be a positive multiple of 4");
+  MIA_CHECK_ARG(aligned16(w) && aligned16(y1) && (reinterpret_cast<uintptr_t>(x) & 7) == 0,
+                "fe_conv1_fwd: y1/w must be 16-byte and x 8-byte aligned");
+  const int w1 = (t - 64) / 2 + 1;
+  F1Args a{x, reinterpret_cast<const bf16*>(w), bias, reinterpret_cast<bf16*>(y1), partial, n, t, w1,
+           (int)cdiv(w1, 32)};
+  MIA_CHECK_ARG((int64_t)n * a.nitem < (1ll << 31), "fe_conv1_fwd: too many items");
+  if (partial) fe_conv1_kernel<true><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
+  else fe_conv1_kernel<false><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
+  MIA_LAUNCH_CHECK("fe_conv1_fwd");
   return 0;
 }

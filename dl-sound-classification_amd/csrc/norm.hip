@@ -56,13 +56,14 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const void* __restrict__ x
 __global__ void bn_finalize_kernel(const void* __restrict__ x, int dtype, const float* __restrict__ partial,
                                    int nblk, int64_t P, int C, const float* gamma, const float* beta,
                                    float* running_mean, float* running_var, float momentum, float eps,
-                                   float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+                                   float* mean_o, float* invstd_o, float* scale_o, float* shift_o,
+                                   const float* __restrict__ kshift = nullptr) {
   const int c = blockIdx.x;  // one block per channel
   const double s1 = block_sum_strided(partial + (int64_t)c * 2, nblk, (int64_t)C * 2);
   const double s2 = block_sum_strided(partial + (int64_t)c * 2 + 1, nblk, (int64_t)C * 2);
   if (threadIdx.x != 0) return;
   const double n = (double)P;
-  const double K = ld_elem(x, dtype, c);
+  const double K = kshift ? (double)kshift[c] : (double)ld_elem(x, dtype, c);
   const double dm = s1 / n;
   const double mean = K + dm;
   double var = s2 / n - dm * dm;
@@ -464,6 +465,20 @@ extern "C" int mia_bn_fwd_stats(const void* x, int32_t dtype, int64_t P, int32_t
                                                             running_mean, running_var, momentum, eps, mean, invstd,
                                                             scale, shift);
   MIA_LAUNCH_CHECK("bn_finalize");
+  return 0;
+}
+
+extern "C" int mia_bn_finalize_shifted(const float* partial, int32_t nblk, int64_t P, int32_t C, const float* kshift,
+                                       const float* gamma, const float* beta, float* running_mean,
+                                       float* running_var, float momentum, float eps, int32_t training, float* mean,
+                                       float* invstd, float* scale, float* shift, mia_stream_t stream) {
+  MIA_CHECK_ARG(partial && kshift && mean && invstd && scale && shift && nblk > 0 && P > 0 && C > 0,
+                "bn_finalize_shifted: bad arguments");
+  MIA_CHECK_ARG(training, "bn_finalize_shifted: batch statistics are a training-mode path");
+  bn_finalize_kernel<<<(unsigned)C, 256, 0, as_stream(stream)>>>(nullptr, MIA_F32, partial, nblk, P, C, gamma, beta,
+                                                                running_mean, running_var, momentum, eps, mean,
+                                                                invstd, scale, shift, kshift);
+  MIA_LAUNCH_CHECK("bn_finalize_shifted");
   return 0;
 }
 

@@ -291,6 +291,32 @@ def conv1ch_dgrad(dy: torch.Tensor, w: torch.Tensor, n: int, oh: int, ow: int, o
                 "mia_conv1ch_dgrad")
 
 
+def fe_conv1_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, y1: torch.Tensor, n: int, t: int,
+                 stats: bool, tag: str | None = None):
+    """EnvNet conv1 forward (bf16 out): x f32 (n, t), w bf16 (32, 64), bias f32 (32) -> y1 (n*w1, 32).
+    stats=True also returns (partial, nblk): the BN1 shifted sums about bias, for bn_finalize_shifted."""
+    w1 = (t - 64) // 2 + 1
+    assert x.dtype == torch.float32 and w.dtype == torch.bfloat16 and y1.dtype == torch.bfloat16
+    assert x.numel() == n * t and w.numel() == 32 * 64 and y1.numel() == n * w1 * 32 and bias.numel() == 32
+    nw = 4096
+    part = torch.empty(nw, 32, 2, dtype=torch.float32, device=x.device) if stats else None
+    with probe(tag or "", 2.0 * n * w1 * 32 * 64, x.numel() * 4 + y1.numel() * 2):
+        L.check(L.load().mia_fe_conv1_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), y1.data_ptr(), L.ptr(part),
+                                          nw, n, t, _s()), "mia_fe_conv1_fwd")
+    return (part, nw) if stats else None
+
+
+def bn_finalize_shifted(partial: torch.Tensor, nblk: int, P: int, C: int, kshift: torch.Tensor, gamma, beta,
+                        running_mean, running_var, momentum: float, eps: float) -> BNState:
+    """Training-mode BN statistics from shifted partial sums (mia_bn_finalize_shifted)."""
+    st = torch.empty(4, C, dtype=torch.float32, device=partial.device)
+    L.check(L.load().mia_bn_finalize_shifted(partial.data_ptr(), nblk, P, C, kshift.data_ptr(), L.ptr(gamma),
+                                             L.ptr(beta), L.ptr(running_mean), L.ptr(running_var), momentum, eps, 1,
+                                             st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(),
+                                             _s()), "mia_bn_finalize_shifted")
+    return BNState(st[0], st[1], st[2], st[3])
+
+
 def fe_conv2_fwd(y1: torch.Tensor, scale, shift, w: torch.Tensor, bias, y2: torch.Tensor, n: int, w1: int,
                  w2: int, tag: str | None = None):
     """EnvNet conv2 forward (bf16): y1 (n*w1, 32), optional BN1 scale/shift (+ReLU) applied to the

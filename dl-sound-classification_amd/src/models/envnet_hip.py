@@ -123,10 +123,20 @@ class EnvNetFunction(torch.autograd.Function):
         fe.__enter__()
         w1 = K.pack_weight(p[0], cd, 0)
         y1 = torch.empty(B * W1, 32, dtype=tdt, device=dev)
-        A = K.conv(x, L.KC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
-        Bo = K.dense(w1, L.KC, 32, 64)
-        K.gemm(A, Bo, K.epilogue(y1, 32, bias=p[1]), B * W1, 32, 64, cd, tag="conv1.fwd")
-        bn1 = bn(0, y1, B * W1, 32)
+        if cd == L.BF16:
+            # wave-persistent conv1 with the BN1 batch statistics accumulated in its epilogue
+            st = K.fe_conv1_fwd(x, w1, p[1], y1, B, T, stats=training, tag="conv1.fwd")
+            if training:
+                m0 = bns[0]
+                bn1 = K.bn_finalize_shifted(st[0], st[1], B * W1, 32, p[1], m0.weight, m0.bias, m0.running_mean,
+                                            m0.running_var, m0.momentum if m0.momentum is not None else 0.1, m0.eps)
+            else:
+                bn1 = bn(0, y1, B * W1, 32)
+        else:
+            A = K.conv(x, L.KC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True)
+            Bo = K.dense(w1, L.KC, 32, 64)
+            K.gemm(A, Bo, K.epilogue(y1, 32, bias=p[1]), B * W1, 32, 64, cd, tag="conv1.fwd")
+            bn1 = bn(0, y1, B * W1, 32)
         # ---- conv2 (stride 2) with BN1+ReLU fused into the operand load
         w2 = K.pack_weight(p[4], cd, 0)
         y2 = torch.empty(B * W2, 64, dtype=tdt, device=dev)

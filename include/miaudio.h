@@ -194,6 +194,24 @@ int mia_col2im_rows(const float* p, int32_t n, int32_t ph, int32_t w, int32_t kh
 int mia_conv1ch_dgrad(const void* dy, const float* w, void* dx, int32_t n, int32_t oh, int32_t ow,
                       mia_stream_t stream);
 
+/* EnvNet-v2 frontend conv1 forward (reference src/models/envnet_v2.py:15 Conv2d(1, 32, (1, 64),
+ * stride (1, 2)) on the raw waveform; replaces that cuDNN conv2d) with the BatchNorm1 batch
+ * statistics (envnet_v2.py:16, training mode) accumulated from the stored bf16 values:
+ *   y1[b][o][c] = bias[c] + sum_{k<64} w[c][k] * x[b][2o+k],  o < w1 = (t-64)/2+1
+ * x f32 (n, t) (8-byte aligned), w bf16 (32, 64), bias f32 (32), y1 bf16 (n, w1, 32).
+ * partial (or NULL): f32 [nwaves][32][2] sums of (y1 - bias[c]) and its square, for
+ * mia_bn_finalize_shifted(kshift = bias).  nwaves: multiple of 4 (the launch is nwaves/4 x 256). */
+int mia_fe_conv1_fwd(const float* x, const void* w, const float* bias, void* y1, float* partial, int32_t nwaves,
+                     int32_t n, int32_t t, mia_stream_t stream);
+
+/* BatchNorm finalize from per-block shifted sums partial[nblk][C][2] about kshift[c]: writes mean,
+ * invstd, the fused scale/shift (gamma*invstd, beta - mean*gamma*invstd) and updates the running
+ * statistics (momentum, unbiased variance) exactly as mia_bn_fwd_stats.  Training mode only. */
+int mia_bn_finalize_shifted(const float* partial, int32_t nblk, int64_t P, int32_t C, const float* kshift,
+                            const float* gamma, const float* beta, float* running_mean, float* running_var,
+                            float momentum, float eps, int32_t training, float* mean, float* invstd,
+                            float* scale, float* shift, mia_stream_t stream);
+
 /* EnvNet-v2 frontend conv2 forward (reference src/models/envnet_v2.py:19 Conv2d(32, 64, (1, 16),
  * stride (1, 2)) applied to relu(bn1(y1)), envnet_v2.py:20-21; replaces that cuDNN conv2d):
  *   y2[b][o][co] = bias[co] + sum_{kx,ci} w[co][kx][ci] * relu(y1[b][2o+kx][ci]*scale[ci] + shift[ci])

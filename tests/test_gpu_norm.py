@@ -158,3 +158,32 @@ def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
     cols = x.double().unfold(1, 64, 2)  # (n, w1, 64)
     ref = torch.einsum("npc,npk->ck", d64.view(n, w1, 32), cols)
     assert rel(dw.double(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("n,t", [(3, 220500), (5, 9000)])
+def test_fe_conv1_fwd_with_bn_stats(cuda, n, t):
+    """Wave-persistent conv1 (1x64, stride 2) vs float64 conv1d of the same bf16 operands, and the BN1
+    statistics it accumulates (shifted about the bias) == mia_bn_fwd_stats over its own output,
+    running statistics included."""
+    w1 = (t - 64) // 2 + 1
+    g = torch.Generator(device=cuda).manual_seed(t * 3 + n)
+    x = torch.randn(n, t, generator=g, device=cuda) * 0.1
+    W = torch.randn(32, 1, 1, 64, generator=g, device=cuda) * 0.1
+    bias = torch.randn(32, generator=g, device=cuda) * 0.5
+    wp = K.pack_weight(W, L.BF16, 0)
+    y1 = torch.empty(n * w1, 32, dtype=torch.bfloat16, device=cuda)
+    part, nblk = K.fe_conv1_fwd(x, wp, bias, y1, n, t, stats=True)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda)
+    rm1, rv1 = torch.zeros(32, device=cuda), torch.ones(32, device=cuda)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    st = K.bn_finalize_shifted(part, nblk, n * w1, 32, bias, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    ref_st = K.bn_fwd_stats(y1, n * w1, 32, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
+    torch.cuda.synchronize()
+    ref = F.conv1d(x.to(torch.bfloat16).double()[:, None], W.to(torch.bfloat16).double()[:, :, 0], bias.double(),
+                   stride=2)
+    got = y1.double().view(n, w1, 32).permute(0, 2, 1)
+    assert (got - ref).abs().max() / ref.abs().max() < 1e-2
+    for a, b in ((st.mean, ref_st.mean), (st.invstd, ref_st.invstd), (st.scale, ref_st.scale),
+                 (st.shift, ref_st.shift), (rm1, rm2), (rv1, rv2)):
+        assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
