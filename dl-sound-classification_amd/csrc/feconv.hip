@@ -257,11 +257,10 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 
 // ---------------------------------------------------------------- conv1 forward + BN1 statistics
 //   y1[b][o][c] = bias[c] + sum_{k<64} w[c][k] * x[b][2o+k]        (envnet_v2.py:15, 1 -> 32 channels)
-// Wave-persistent (no LDS, no barriers): a wave owns (clip, 32-pixel) items; the 4 weight fragments
-// (32 channels x 64 taps) stay in registers as the MFMA A operand, the Toeplitz B operand is read
-// straight from the f32 waveform (8 consecutive samples per lane and k-step, L1-resident: the
-// 126-sample segment of an item is shared by all its lanes) and rounded to bf16, and the next
-// item's samples are in flight while the current one computes.  After the half swap each lane holds
+// Wave-persistent (no barriers): a wave owns (clip, 32-pixel) items; the 4 weight fragments (32
+// channels x 64 taps) stay in registers as the MFMA A operand; the item's 126-sample waveform
+// segment is one 8-byte load per lane (the next item's is in flight while this one computes),
+// rounded to bf16 into a per-wave LDS strip from which the Toeplitz B fragments are read.  After the half swap each lane holds
 // 16 channels of one pixel: 2 x 16-B stores, and the BN1 batch statistics of the stored (bf16)
 // values are accumulated on the fly about K[c] = bias[c] (the waveform is zero-mean, so the
 // shifted sums are well conditioned) -> per-wave partial [C][2] -> bn finalize in double.
@@ -276,9 +275,14 @@ struct F1Args {
 
 template <bool STATS>
 __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  // per-wave LDS: the item's 126-sample segment as bf16 dwords (2 samples each), twice: copy 0 at
+  // dword 0 and copy 1 shifted by one dword at dword 96 (+32 banks), so every 8-sample B fragment
+  // is two 8-byte-aligned ds_read_b64 from the copy matching its start parity, conflict-free
+  __shared__ __attribute__((aligned(16))) uint32_t seg[4][160];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
   const int items = g.n * g.nitem;
+  uint32_t* sg = seg[wv];
   bf16x8 wa[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) wa[ks] = *reinterpret_cast<const bf16x8*>(g.w + (lane & 31) * 64 + ks * 16 + 8 * (lane >> 5));
@@ -291,55 +295,58 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
   for (int i = 0; i < 16; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
 
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-  f32x2 xa[16], xb[16];
-  auto load = [&](int it, f32x2 (&r)[16]) __attribute__((always_inline)) {
+  // lane l loads samples 2l, 2l+1 of the item's segment x[b][2*o0 .. 2*o0+125] (clamped in-clip)
+  auto load = [&](int it) __attribute__((always_inline)) {
     it = it < items ? it : items - 1;
     const int b = it / g.nitem;
-    const int o = (it - b * g.nitem) * 32 + (lane & 31);
-    const int64_t base = o < g.w1 ? (int64_t)b * g.t + 2 * o + 8 * (lane >> 5) : 0;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int h = 0; h < 4; ++h) r[ks * 4 + h] = *reinterpret_cast<const f32x2*>(g.x + base + 16 * ks + 2 * h);
+    const int o0 = (it - b * g.nitem) * 32;
+    int s0 = 2 * o0 + 2 * lane;
+    s0 = s0 < g.t - 2 ? s0 : g.t - 2;
+    return *reinterpret_cast<const f32x2*>(g.x + (int64_t)b * g.t + s0);
   };
-  auto run = [&](int it, const f32x2 (&r)[16]) __attribute__((always_inline)) {
+  auto run = [&](int it, f32x2 xr) __attribute__((always_inline)) {
+    const bf16 lo = (bf16)xr[0], hi = (bf16)xr[1];
+    const uint32_t d = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    sg[lane] = d;
+    if (lane >= 1) sg[96 + lane - 1] = d;
     f32x16 acc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    const int o = lane & 31;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 fb;
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        fb[2 * h] = (bf16)r[ks * 4 + h][0];
-        fb[2 * h + 1] = (bf16)r[ks * 4 + h][1];
-      }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ks], fb, acc, 0, 0, 0);
+      const int D = o + 4 * (lane >> 5) + 8 * ks;  // first dword of this lane's 8 samples
+      const uint32_t* src = (D & 1) ? sg + 96 + D - 1 : sg + D;
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 p0 = *reinterpret_cast<const u32x2*>(src);
+      const u32x2 p1 = *reinterpret_cast<const u32x2*>(src + 2);
+      const u32x4 f = {p0[0], p0[1], p1[0], p1[1]};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ks], __builtin_bit_cast(bf16x8, f), acc, 0, 0, 0);
     }
     float v[16];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float lo = acc[8 * h + j], hi = acc[8 * h + 4 + j];
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+        const float a0 = acc[8 * h + j], a1 = acc[8 * h + 4 + j];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a1), false, false);
         v[8 * h + j] = __builtin_bit_cast(float, (unsigned)sw[0]);
         v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)sw[1]);
       }
     const int b = it / g.nitem;
-    const int o = (it - b * g.nitem) * 32 + (lane & 31);
-    if (o < g.w1) {
-      bf16* dst = g.y + ((int64_t)b * g.w1 + o) * 32 + c0;
+    const int op = (it - b * g.nitem) * 32 + o;
+    if (op < g.w1) {
+      bf16* dst = g.y + ((int64_t)b * g.w1 + op) * 32 + c0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         uint32_t w4[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int e = 8 * h + 2 * i;
-          const bf16 lo = (bf16)(v[e] + bv[e]), hi = (bf16)(v[e + 1] + bv[e + 1]);
-          w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
+          w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
           if constexpr (STATS) {
-            const float d0 = (float)lo - bv[e], d1 = (float)hi - bv[e + 1];
+            const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
             s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
             s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
           }
@@ -351,13 +358,13 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
 
   int it = gw;
   if (it < items) {
-    load(it, xa);
+    f32x2 xa = load(it), xb;
     for (;;) {
-      load(it + nw, xb);
+      xb = load(it + nw);
       run(it, xa);
       it += nw;
       if (it >= items) break;
-      load(it + nw, xa);
+      xa = load(it + nw);
       run(it, xb);
       it += nw;
       if (it >= items) break;

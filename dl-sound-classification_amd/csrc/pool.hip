@@ -221,6 +221,96 @@ __global__ __launch_bounds__(NT) void pool_bwd_sparse_kernel(const void* __restr
 // carries the ReLU mask).  Reads x once, writes dx once; the masked dense gradient is never
 // materialised.  s1 partials = dbias.  All loads are unconditional (a conditional load makes hipcc
 // wait vmcnt(0) in the loop); four pixels per thread-iteration.
+// Same pass for pool windows kw % 8 == 0 (the frontend (1, 64) pool): a thread owns 8 channels x
+// 8 consecutive pixels of one row, which always fall in ONE pooled cell, so the cell's argmax bytes
+// and masked gradient (40 B) are read once per 8 pixels instead of once per pixel, and the index
+// math runs once per octet.  All 8 pixel loads are issued before any use.
+__global__ __launch_bounds__(NT) void pool_bn_bwd_apply_oct_kernel(const float* __restrict__ gm,
+                                                                   const uint8_t* __restrict__ argmax,
+                                                                   const bf16* __restrict__ x, int n, int H, int W,
+                                                                   int C, int kh, int kw, FastDiv dNO, FastDiv dH,
+                                                                   FastDiv dG, const float* __restrict__ gamma,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ invstd,
+                                                                   const float* __restrict__ dgamma,
+                                                                   const float* __restrict__ dbeta, bf16* dx,
+                                                                   float* __restrict__ partial) {
+  const int OH = H / kh, OW = W / kw, G = C / 8, NO = (W + 7) / 8;
+  const int t = threadIdx.x;
+  const int cg = t % G;
+  const int P = n * H * W;
+  float mu[8], is[8], a[8], mb[8], mg[8];
+  const float invP = 1.f / (float)P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = cg * 8 + i;
+    mu[i] = mean[c]; is[i] = invstd[c];
+    a[i] = (gamma ? gamma[c] : 1.f) * is[i];
+    mb[i] = dbeta[c] * invP;
+    mg[i] = dgamma[c] * invP;
+  }
+  float s1[8] = {0};
+  const int64_t units = (int64_t)n * H * NO * G;
+  for (int64_t u = (int64_t)blockIdx.x * NT + t; u < units; u += (int64_t)gridDim.x * NT) {
+    const int rest = (int)fdiv((uint32_t)(u), dG);       // (b*H + iy)*NO + o8   (units < 2^31 checked)
+    const int rowi = (int)fdiv((uint32_t)rest, dNO);     // b*H + iy
+    const int o8 = rest - rowi * NO;
+    const int iy = rowi - (int)fdiv((uint32_t)rowi, dH) * H;
+    const int b = (rowi - iy) / H;
+    const int ix0 = o8 * 8;
+    const int oy = iy / kh, ox = ix0 / kw;
+    const bool cell = oy < OH && ox < OW;
+    const int64_t coff = cell ? (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8 : 0;
+    const uint2 am = *reinterpret_cast<const uint2*>(argmax + coff);
+    const float4 g0 = reinterpret_cast<const float4*>(gm + coff)[0];
+    const float4 g1 = reinterpret_cast<const float4*>(gm + coff)[1];
+    const int64_t xoff = ((int64_t)rowi * W + ix0) * C + cg * 8;
+    uint4 xr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t o = ix0 + j < W ? xoff + (int64_t)j * C : xoff;
+      xr[j] = *reinterpret_cast<const uint4*>(x + o);
+    }
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const int pos0 = (iy - oy * kh) * kw + (ix0 - ox * kw);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (ix0 + j >= W) break;
+      const uint32_t w4[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+      uint32_t o4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float g[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * q + h;
+          const float xv = __uint_as_float(h ? (w4[q] & 0xffff0000u) : (w4[q] << 16));
+          const uint32_t word = i < 4 ? am.x : am.y;
+          const int av = (int)((word >> (8 * (i & 3))) & 0xffu);
+          const float gi = cell && av == pos0 + j ? gv[i] : 0.f;
+          g[h] = a[i] * (gi - mb[i] - (xv - mu[i]) * is[i] * mg[i]);
+          s1[i] += g[h];
+        }
+        const bf16 lo = (bf16)g[0], hi = (bf16)g[1];
+        o4[q] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      }
+      *reinterpret_cast<uint4*>(dx + xoff + (int64_t)j * C) = uint4{o4[0], o4[1], o4[2], o4[3]};
+    }
+  }
+  if (!partial) return;
+  __shared__ float red[NT * 8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[t * 8 + i] = s1[i];
+  __syncthreads();
+  const int rslots = NT / G;
+  for (int c = t; c < C; c += NT) {
+    const int g2 = c / 8, ci = c % 8;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < rslots; ++r2) acc += red[(r2 * G + g2) * 8 + ci];
+    partial[((int64_t)blockIdx.x * C + c) * 2] = acc;
+  }
+}
+
 constexpr int PB_UNROLL = 4;
 __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_kernel(const float* __restrict__ gm,
                                                                const uint8_t* __restrict__ argmax,
@@ -397,8 +487,23 @@ extern "C" int mia_pool_bn_relu_bwd_apply(const float* gm, const uint8_t* argmax
   MIA_CHECK_ARG(h >= kh && w >= kw && kh * kw <= 256, "pool_bn_bwd_apply: bad geometry");
   const int rslots = NT / (c / 8);
   const int64_t P = (int64_t)n * h * w;
-  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
   hipStream_t s = as_stream(stream);
+  const int64_t units = (int64_t)n * h * ((w + 7) / 8) * (c / 8);
+  if (kw % 8 == 0 && dtype == MIA_BF16 && units < (1ll << 31) &&
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0) {
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(units, NT), 1024));  // partial slab: <= 1024 blocks
+    pool_bn_bwd_apply_oct_kernel<<<nb, NT, 0, s>>>(gm, argmax, reinterpret_cast<const bf16*>(x), n, h, w, c, kh, kw,
+                                                   make_fastdiv((w + 7) / 8), make_fastdiv(h), make_fastdiv(c / 8),
+                                                   gamma, mean, invstd, dgamma, dbeta, reinterpret_cast<bf16*>(dx),
+                                                   dbias ? (float*)partial : nullptr);
+    MIA_LAUNCH_CHECK("pool_bn_bwd_apply");
+    if (dbias) {
+      partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, nullptr, dbias);
+      MIA_LAUNCH_CHECK("pool_bn_bwd_apply_final");
+    }
+    return 0;
+  }
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(P, (int64_t)rslots * 8), 1024));
   pool_bn_bwd_apply_kernel<<<nb, NT, 0, s>>>(gm, argmax, x, dtype, n, h, w, c, kh, kw, make_fastdiv(w), make_fastdiv(h),
                                              make_fastdiv(kw), make_fastdiv(kh), gamma, mean, invstd, dgamma,
                                              dbeta, dx, dbias ? (float*)partial : nullptr);

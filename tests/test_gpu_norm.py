@@ -187,3 +187,42 @@ def test_fe_conv1_fwd_with_bn_stats(cuda, n, t):
     for a, b in ((st.mean, ref_st.mean), (st.invstd, ref_st.invstd), (st.scale, ref_st.scale),
                  (st.shift, ref_st.shift), (rm1, rm2), (rv1, rv2)):
         assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64), (3, 1, 1001, 64, 1, 64), (2, 6, 67, 32, 2, 8)])
+def test_pool_bn_bwd_apply_octets_bf16(cuda, geom):
+    """bf16 pooled BN backward with kw % 8 == 0 (row-octet kernel: one cell lookup per 8 pixels;
+    ragged rows, pixels past the last whole cell) vs a float64 restatement: dx = BN backward of the
+    max-pool's routed, ReLU-masked gradient."""
+    n, h, w, c, kh, kw = geom
+    g = torch.Generator().manual_seed(h * w + c)
+    y = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16)
+    scale = torch.rand(c, generator=g) + 0.5
+    shift = torch.randn(c, generator=g) * 0.3
+    mean = torch.randn(c, generator=g) * 0.1
+    invstd = torch.rand(c, generator=g) + 0.5
+    st = K.BNState(mean.to(cuda), invstd.to(cuda), scale.to(cuda), shift.to(cuda))
+    oh, ow = h // kh, w // kw
+    out = torch.empty(n, oh, ow, c, device=cuda, dtype=torch.bfloat16)
+    am = torch.empty(n, oh, ow, c, dtype=torch.uint8, device=cuda)
+    ty = y.to(cuda)
+    K.pool_fwd(ty, n, h, w, c, kh, kw, st, out, 0, am)
+    dout = torch.randn(n, oh, ow, c, generator=g).to(torch.bfloat16)  # same dtype as the activations
+    gm, dg, db = K.pool_bwd_gather(dout.to(cuda), 0, am, ty, n, h, w, c, kh, kw, st)
+    gamma = (torch.rand(c, generator=g) + 0.5)
+    dx = torch.empty_like(ty)
+    dbias = torch.empty(c, device=cuda)
+    K.pool_bn_relu_bwd_apply(gm, am, ty, n, h, w, c, kh, kw, gamma.to(cuda), st, dg, db, dx, dbias)
+    torch.cuda.synchronize()
+    # float64 restatement: route dout to the argmax of relu(z) per cell, mask, BN backward
+    yd = y.double()
+    a = torch.relu(yd * scale.double() + shift.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    F.max_pool2d(a, (kh, kw), (kh, kw)).backward(dout.double().permute(0, 3, 1, 2))
+    zmask = (yd * scale.double() + shift.double() > 0)
+    dz = a.grad.permute(0, 2, 3, 1) * zmask
+    P = n * h * w
+    xhat = (yd - mean.double()) * invstd.double()
+    ref = gamma.double() * invstd.double() * (dz - dz.sum((0, 1, 2)) / P - xhat * (dz * xhat).sum((0, 1, 2)) / P)
+    assert rel(dx.double().cpu(), ref) < 1e-2
+    assert rel(dg.double().cpu(), (dz * xhat).sum((0, 1, 2))) < 1e-4
+    assert rel(db.double().cpu(), dz.sum((0, 1, 2))) < 1e-4
