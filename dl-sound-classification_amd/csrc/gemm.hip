@@ -991,12 +991,14 @@ struct TapWArgs {
   int n, h, wx, oh, ow;
   int Z;
   float* ws;
-  // BNB: dy is the gradient w.r.t. relu(bn(y)) and the kernel stages the BN-input gradient
-  //   dy' = gamma*invstd * (mask(y) * dy - dbeta/P - (y - mean) * invstd * dgamma/P)
-  // (the bn_bwd_apply formula, same op order) instead of dy; per-block partial column sums of dy'
-  // (the conv bias gradient) go to dbp[z][32].
+  // BNB (single pass, BN-backward reductions not yet known): dy is the gradient w.r.t. relu(bn(y));
+  // the kernel stages dz = mask(y) * dy and y itself as two A operands and accumulates
+  //   G1 = sum dz x,  G3 = sum y x   (slabs ws[z][2][32][64])
+  // and per channel sum dz, sum dz*xhat, sum y (dbp[z][32][3]).  The BN-input gradient is linear,
+  //   g = A dz + B + C y  (A = gamma*invstd, B = -A*dbeta/P + A*invstd*mean*dgamma/P, C = -A*invstd*dgamma/P),
+  // so dW = A G1 + B G2 + C G3 with G2[k] = sum x[2p+k] (fe_conv1_lin_final).
   const bf16* by;
-  const float *bsc, *bsh, *bgamma, *bmean, *binvstd, *bdgamma, *bdbeta;
+  const float *bsc, *bsh, *bmean, *binvstd;
   float* dbp;
   int64_t bP;
 };
@@ -1013,7 +1015,8 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
   constexpr int DYB = BP * 64;                     // dY tile [BP][32] bf16
   constexpr int RAWB = NSEQ * LR * 2;
   constexpr int CPYB = NSEQ * SQB;
-  constexpr int MAINB = DYB + RAWB + CPYB;
+  constexpr int MAINB0 = DYB + RAWB + CPYB;
+  constexpr int MAINB = MAINB0 + (BNB ? DYB : 0);
   constexpr int REDB = 4 * 32 * 64 * 4;
   constexpr int RCH = (NSEQ * LR + NT - 1) / NT;
   constexpr int DCH = BP * 32 / 8 / NT;            // 4
@@ -1034,23 +1037,19 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
   float rreg[RCH];
   u32x4 yreg[BNB ? DCH : 1];
   uint32_t dok = 0;
-  // BNB: per-thread channel group (t & 3) constants, as bn_bwd_apply computes them
-  float bsc[8], bsh[8], ba[8], bmu[8], bis[8], bmb[8], bmg[8], dbsum[8];
+  float bsc[8], bsh[8], bmu[8], bis[8], sdz[8], sdx[8], sy[8];
   if constexpr (BNB) {
-    const float invP = 1.f / (float)g.bP;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int ch = (t & 3) * 8 + i;
       bsc[i] = g.bsc[ch];
       bsh[i] = g.bsh[ch];
       bis[i] = g.binvstd[ch];
-      ba[i] = (g.bgamma ? g.bgamma[ch] : 1.f) * bis[i];
       bmu[i] = g.bmean[ch];
-      bmb[i] = g.bdbeta[ch] * invP;
-      bmg[i] = g.bdgamma[ch] * invP;
-      dbsum[i] = 0.f;
+      sdz[i] = 0.f; sdx[i] = 0.f; sy[i] = 0.f;
     }
   }
+  char* yt = smem + MAINB0;  // BNB: second A tile (y), [BP][32] bf16
 
   auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
     const int64_t row = c / CPR;
@@ -1110,7 +1109,7 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
       const int q = t + NT * s2;
       u32x4 v = dreg[s2];
       if constexpr (BNB) {
-        uint32_t w4[4] = {0u, 0u, 0u, 0u};
+        uint32_t w4[4] = {0u, 0u, 0u, 0u}, y4[4] = {0u, 0u, 0u, 0u};
         if ((dok >> s2) & 1u) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -1119,19 +1118,23 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
             gv[1] = __uint_as_float(dreg[s2][i] & 0xffff0000u);
             yv[0] = __uint_as_float(yreg[s2][i] << 16);
             yv[1] = __uint_as_float(yreg[s2][i] & 0xffff0000u);
+            uint32_t m = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const int c = 2 * i + h;
-              float d = fmaf(yv[h], bsc[c], bsh[c]) > 0.f ? gv[h] : 0.f;
-              d = ba[c] * (d - bmb[c] - (yv[h] - bmu[c]) * bis[c] * bmg[c]);
-              dbsum[c] += d;
-              gv[h] = d;
+              const bool on = fmaf(yv[h], bsc[c], bsh[c]) > 0.f;
+              const float d = on ? gv[h] : 0.f;
+              sdz[c] += d;
+              sdx[c] = fmaf(d, (yv[h] - bmu[c]) * bis[c], sdx[c]);
+              sy[c] += yv[h];
+              m |= on ? (0xffffu << (16 * h)) : 0u;
             }
-            const bf16 lo = (bf16)gv[0], hi = (bf16)gv[1];
-            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+            w4[i] = dreg[s2][i] & m;  // dz = mask * dy exactly (bf16 bits kept or zeroed)
+            y4[i] = yreg[s2][i];
           }
         }
         v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        *reinterpret_cast<u32x4*>(yt + (q >> 2) * 64 + (q & 3) * 16) = u32x4{y4[0], y4[1], y4[2], y4[3]};
       }
       *reinterpret_cast<u32x4*>(dyt + (q >> 2) * 64 + (q & 3) * 16) = v;
     }
@@ -1155,11 +1158,17 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
     }
   };
 
-  f32x16 acc[2];
+  f32x16 acc[2], acc3[BNB ? 2 : 1];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  if constexpr (BNB) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc3[j][r] = 0.f;
+  }
 
   const int i16 = lane & 15, gq = lane >> 4, g2 = lane >> 5;
   // this lane's tap per n-tile: n = nt*32 + (lane&31) -> (ky, kx) -> (seq, j)
@@ -1195,6 +1204,14 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
       typedef short s16x8 __attribute__((ext_vector_type(8)));
       const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const bf16x8 fa = __builtin_bit_cast(bf16x8, cc);
+      bf16x8 fy;
+      if constexpr (BNB) {
+        const char* py = yt + kr * 64 + col * 2;
+        const s16x4 ylo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(py));
+        const s16x4 yhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(py + 4 * 64));
+        const s16x8 yc = {ylo[0], ylo[1], ylo[2], ylo[3], yhi[0], yhi[1], yhi[2], yhi[3]};
+        fy = __builtin_bit_cast(bf16x8, yc);
+      }
       const int ox0 = ks * 16 + 8 * g2;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
@@ -1202,6 +1219,7 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
         const int sh = q & 7;
         const bf16x8 fb = *reinterpret_cast<const bf16x8*>(cpy + bseq[nt] * SQB + sh * CPB + (q - sh) * 2);
         acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[nt], 0, 0, 0);
+        if constexpr (BNB) acc3[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fy, fb, acc3[nt], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -1213,32 +1231,41 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
     }
   }
 
-  // sum the 4 waves' partials, write the block's slab ws[z][32][64]
+  // sum the 4 waves' partials, write the block's slab ws[z][32][64] (BNB: ws[z][2][32][64], G1 then G3)
   float* red = reinterpret_cast<float*>(smem);
-  __syncthreads();
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+  for (int which = 0; which < (BNB ? 2 : 1); ++which) {
+    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = (r & 3) + 8 * (r >> 2) + 4 * g2;
-      red[(wave * 32 + m) * 64 + nt * 32 + (lane & 31)] = acc[nt][r];
-    }
-  __syncthreads();
-  float* dst = g.ws + (int64_t)z * 32 * 64;
-  for (int e = t; e < 32 * 64; e += NT)
-    dst[e] = red[e] + red[2048 + e] + red[4096 + e] + red[6144 + e];
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (r & 3) + 8 * (r >> 2) + 4 * g2;
+        float v = acc[nt][r];
+        if constexpr (BNB) if (which) v = acc3[nt][r];
+        red[(wave * 32 + m) * 64 + nt * 32 + (lane & 31)] = v;
+      }
+    __syncthreads();
+    float* dst = g.ws + ((int64_t)z * (BNB ? 2 : 1) + which) * 32 * 64;
+    for (int e = t; e < 32 * 64; e += NT)
+      dst[e] = red[e] + red[2048 + e] + red[4096 + e] + red[6144 + e];
+  }
   if constexpr (BNB) {
-    // bias-gradient partial of this block: channel c = (t&3)*8 + i summed over the 64 threads of
-    // its group in thread order (deterministic)
+    // per-channel sums of this block: channel c = (t&3)*8 + i summed over the 64 threads of its
+    // group in thread order (deterministic) -> dbp[z][c][0..2] = (sum dz, sum dz*xhat, sum y)
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[t * 8 + i] = dbsum[i];
+    for (int i = 0; i < 8; ++i) {
+      red[t * 8 + i] = sdz[i];
+      red[2048 + t * 8 + i] = sdx[i];
+      red[4096 + t * 8 + i] = sy[i];
+    }
     __syncthreads();
-    if (t < 32) {
-      const int cg = t >> 3, i = t & 7;
-      float acc_b = 0.f;
-      for (int k = 0; k < NT / 4; ++k) acc_b += red[(k * 4 + cg) * 8 + i];
-      g.dbp[(int64_t)z * 32 + t] = acc_b;
+    if (t < 96) {
+      const int q = t / 32, ch = t % 32, cg = ch >> 3, i = ch & 7;
+      float a = 0.f;
+      for (int k = 0; k < NT / 4; ++k) a += red[q * 2048 + (k * 4 + cg) * 8 + i];
+      g.dbp[((int64_t)z * 32 + ch) * 3 + q] = a;
     }
   }
 }
@@ -1881,9 +1908,80 @@ extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M
   return 0;
 }
 
+// G2[k] = sum_{b, p < w1} x[b][2p + k] (k < 64): per-clip partials, one block per clip.  With
+// r = k & 1, j0 = k >> 1 the window is x_r[j0 .. j0+w1) of the parity sequence x_r[j] = x[2j+r], so
+// G2_b[k] = T_r - (head j < j0) - (tail j >= j0 + w1): one coalesced pass for the two parity
+// totals T_0, T_1 plus at most 31 + 31 boundary samples per k.
+__global__ __launch_bounds__(256) void conv1_colsum_kernel(const float* __restrict__ x, int t, int w1,
+                                                           float* __restrict__ part) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* xb = x + (int64_t)b * t;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  float e = 0.f, o = 0.f;
+  for (int j = tid; j < t / 2; j += 256) {
+    const f32x2 v = *reinterpret_cast<const f32x2*>(xb + 2 * j);
+    e += v[0];
+    o += v[1];
+  }
+  __shared__ float red[2][256];
+  red[0][tid] = e;
+  red[1][tid] = o;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (tid < h) { red[0][tid] += red[0][tid + h]; red[1][tid] += red[1][tid + h]; }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    const int r = tid & 1, j0 = tid >> 1, L = t / 2;
+    float a = red[r][0];
+    for (int j = 0; j < j0; ++j) a -= xb[2 * j + r];
+    for (int j = j0 + w1; j < L; ++j) a -= xb[2 * j + r];
+    part[(int64_t)b * 64 + tid] = a;
+  }
+}
+
+// dgamma/dbeta, A/B/C per channel (double), dW = A G1 + B G2 + C G3, dbias = A sum dz + B P + C sum y
+__global__ __launch_bounds__(256) void conv1_lin_final_kernel(const float* __restrict__ g13, const float* __restrict__ dbp,
+                                                              int Z, const float* __restrict__ g2part, int n,
+                                                              int64_t P, const float* gamma, const float* mean,
+                                                              const float* invstd, float* dgamma, float* dbeta,
+                                                              float* dw, float* dbias) {
+  __shared__ double cA[32], cB[32], cC[32], g2[64];
+  const int t = threadIdx.x;
+  if (t < 96) {
+    const int ch = t % 32, q = t / 32;
+    double a = 0.0;
+    for (int z = 0; z < Z; ++z) a += (double)dbp[((int64_t)z * 32 + ch) * 3 + q];
+    if (q == 0) cA[ch] = a;       // sum dz  (= dbeta)
+    else if (q == 1) cB[ch] = a;  // sum dz*xhat (= dgamma)
+    else cC[ch] = a;              // sum y
+  }
+  if (t >= 128 && t < 192) {
+    double a = 0.0;
+    for (int b = 0; b < n; ++b) a += (double)g2part[(int64_t)b * 64 + (t - 128)];
+    g2[t - 128] = a;
+  }
+  __syncthreads();
+  if (t < 32) {
+    const double sdz = cA[t], sdx = cB[t], sy = cC[t];
+    dbeta[t] = (float)sdz;
+    dgamma[t] = (float)sdx;
+    const double is = invstd[t], A = (gamma ? (double)gamma[t] : 1.0) * is;
+    const double mb = sdz / (double)P, mg = sdx / (double)P;
+    const double B = -A * mb + A * is * mg * (double)mean[t], C = -A * is * mg;
+    dbias[t] = (float)(A * sdz + B * (double)P + C * sy);
+    cA[t] = A; cB[t] = B; cC[t] = C;
+  }
+  __syncthreads();
+  for (int e = t; e < 32 * 64; e += 256) {
+    const int ch = e / 64, k = e % 64;
+    dw[e] = (float)(cA[ch] * (double)g13[e] + cB[ch] * g2[k] + cC[ch] * (double)g13[2048 + e]);
+  }
+}
+
 extern "C" int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int32_t n, int32_t t,
                                      const float* scale, const float* shift, const float* gamma, const float* mean,
-                                     const float* invstd, const float* dgamma, const float* dbeta, float* dw,
+                                     const float* invstd, float* dgamma, float* dbeta, float* dw,
                                      float* dbias, void* workspace, int32_t split, mia_stream_t stream) {
   MIA_CHECK_ARG(x && dact && y1 && scale && shift && mean && invstd && dgamma && dbeta && dw && dbias && workspace,
                 "fe_conv1_wgrad_bn: null pointer");
@@ -1891,29 +1989,30 @@ extern "C" int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const voi
   MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(dact) | reinterpret_cast<uintptr_t>(y1)) & 15) == 0,
                 "fe_conv1_wgrad_bn: dact / y1 must be 16-byte aligned");
   const int w1 = (t - 64) / 2 + 1;
+  float* ws = reinterpret_cast<float*>(workspace);
   TapWArgs r{};
   r.x = reinterpret_cast<const char*>(x);
   r.dy = reinterpret_cast<const char*>(dact);
   r.n = n; r.h = 1; r.wx = t; r.oh = 1; r.ow = w1;
   r.Z = split;
-  r.ws = reinterpret_cast<float*>(workspace);
+  r.ws = ws;                                       // [split][2][32][64]
   r.by = reinterpret_cast<const bf16*>(y1);
-  r.bsc = scale; r.bsh = shift; r.bgamma = gamma; r.bmean = mean; r.binvstd = invstd;
-  r.bdgamma = dgamma; r.bdbeta = dbeta;
-  r.dbp = r.ws + (int64_t)split * 32 * 64;
+  r.bsc = scale; r.bsh = shift; r.bmean = mean; r.binvstd = invstd;
+  r.dbp = ws + (int64_t)split * 2 * 2048;          // [split][32][3]
   r.bP = (int64_t)n * w1;
+  float* g13 = r.dbp + (int64_t)split * 96;        // [2][32][64]
+  float* g2p = g13 + 2 * 2048;                     // [n][64]
   hipStream_t s = as_stream(stream);
   hipError_t err = tapwgrad_launch<bf16, float, 2, 1, 64, true>(r, s);
   if (err != hipSuccess) return mia::fail(-(int)err, "fe_conv1_wgrad_bn launch: %s", hipGetErrorString(err));
   EpiDev e{};
-  e.ptr = reinterpret_cast<char*>(dw); e.dtype = MIA_F32; e.act = MIA_ACT_NONE; e.ldc = 64; e.alpha = 1.f;
+  e.ptr = reinterpret_cast<char*>(g13); e.dtype = MIA_F32; e.act = MIA_ACT_NONE; e.ldc = 2 * 2048; e.alpha = 1.f;
   e.act_scale = 1.f;
-  launch_splitk_reduce(r.ws, split, 32, 64, e, s);
-  EpiDev eb{};
-  eb.ptr = reinterpret_cast<char*>(dbias); eb.dtype = MIA_F32; eb.act = MIA_ACT_NONE; eb.ldc = 32; eb.alpha = 1.f;
-  eb.act_scale = 1.f;
-  launch_splitk_reduce(r.dbp, split, 1, 32, eb, s);
-  MIA_LAUNCH_CHECK("fe_conv1_wgrad_bn reduce");
+  launch_splitk_reduce(ws, split, 1, 2 * 2048, e, s);  // slabs [split][4096] -> g13
+  conv1_colsum_kernel<<<n, 256, 0, s>>>(x, t, w1, g2p);
+  conv1_lin_final_kernel<<<1, 256, 0, s>>>(g13, r.dbp, split, g2p, n, r.bP, gamma, mean, invstd, dgamma, dbeta, dw,
+                                           dbias);
+  MIA_LAUNCH_CHECK("fe_conv1_wgrad_bn final");
   return 0;
 }
 

@@ -359,23 +359,24 @@ def fe_conv2_wgrad(dy2: torch.Tensor, y1: torch.Tensor, scale, shift, dw: torch.
 
 
 def fe_conv1_wgrad_bn(x: torch.Tensor, dact: torch.Tensor, y1: torch.Tensor, n: int, t: int, gamma, bn: BNState,
-                      dgamma: torch.Tensor, dbeta: torch.Tensor, dw: torch.Tensor, dbias: torch.Tensor,
-                      tag: str | None = None):
-    """EnvNet conv1 weight/bias gradient with BN1+ReLU backward fused into the dY staging (bf16):
+                      dw: torch.Tensor, dbias: torch.Tensor, tag: str | None = None):
+    """BN1+ReLU backward and EnvNet conv1 weight/bias gradient in one pass (bf16 operands):
     x f32 (n, t) waveform, dact = dL/d relu(bn1(y1)) and y1 bf16 (n*w1, 32) -> dw f32 (32, 64),
-    dbias f32 (32)."""
+    dbias f32 (32); returns (dgamma, dbeta) of BN1."""
     w1 = (t - 64) // 2 + 1
     assert dact.dtype == torch.bfloat16 and y1.dtype == torch.bfloat16 and x.dtype == torch.float32
     assert dact.numel() == n * w1 * 32 and y1.numel() == n * w1 * 32 and x.numel() == n * t
     assert dw.numel() == 32 * 64 and dw.dtype == torch.float32 and dbias.numel() == 32
     split = 512
-    ws = workspace(split * (32 * 64 + 32) * 4, x.device, "tapw")
-    flop = 2.0 * n * w1 * 32 * 64
+    ws = workspace((split * (2 * 2048 + 96) + 2 * 2048 + n * 64) * 4, x.device, "tapw")
+    g = torch.empty(2, 32, dtype=torch.float32, device=x.device)
+    flop = 4.0 * n * w1 * 32 * 64
     with probe(tag or "", flop, (dact.numel() + y1.numel()) * 2 + x.numel() * 4):
         L.check(L.load().mia_fe_conv1_wgrad_bn(
             x.data_ptr(), dact.data_ptr(), y1.data_ptr(), n, t, bn.scale.data_ptr(), bn.shift.data_ptr(),
-            L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
+            L.ptr(gamma), bn.mean.data_ptr(), bn.invstd.data_ptr(), g[0].data_ptr(), g[1].data_ptr(),
             dw.data_ptr(), dbias.data_ptr(), ws.data_ptr(), split, _s()), "mia_fe_conv1_wgrad_bn")
+    return g[0], g[1]
 
 
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:

@@ -381,16 +381,18 @@ class EnvNetFunction(torch.autograd.Function):
                 K.gemm(K.conv(dy2, L.KC, B, 1, W2, 64, 1, Tp, 1, 8, pw=7),
                        K.dense(wpar[par], L.KC, 32, 512),
                        K.epilogue(da1, 32, rowmap=(Tp, W1, 2, par)), B * Tp, 32, 512, cd, tag="conv2.dgrad")
-        dg1, db1 = K.bn_relu_bwd_reduce(da1, None, s["y1"], P1, 32, s["bn1"])
-        grads[2], grads[3] = dg1, db1
         dbias1 = torch.empty(32, dtype=torch.float32, device=dev)
         dW1 = torch.empty(32, 64, dtype=torch.float32, device=dev)
         T = g["T"]
         if cd == L.BF16:
-            # BN1+ReLU backward folded into the conv1 weight-gradient staging: dS1 never hits HBM
-            K.fe_conv1_wgrad_bn(s["x"], da1, s["y1"], B, T, bns[0].weight, s["bn1"], dg1, db1, dW1, dbias1,
-                                tag="conv1.wgrad")
+            # BN1+ReLU backward and conv1 weight gradient in one pass (linear form): dS1 is never
+            # formed, the BN reductions come out of the same read of da1 / y1
+            dg1, db1 = K.fe_conv1_wgrad_bn(s["x"], da1, s["y1"], B, T, bns[0].weight, s["bn1"], dW1, dbias1,
+                                           tag="conv1.wgrad")
+            grads[2], grads[3] = dg1, db1
         else:
+            dg1, db1 = K.bn_relu_bwd_reduce(da1, None, s["y1"], P1, 32, s["bn1"])
+            grads[2], grads[3] = dg1, db1
             K.bn_relu_bwd_apply(da1, s["y1"], da1, P1, 32, bns[0].weight, s["bn1"], dg1, db1, dbias1)
             K.gemm(K.dense(da1, L.RC, P1, 32), K.conv(s["x"], L.RC, B, 1, T // 2, 2, 1, W1, 1, 32, row_kind=True),
                    K.epilogue(dW1, 64), 32, 64, P1, cd, tag="conv1.wgrad")

@@ -236,17 +236,19 @@ int mia_fe_conv2_wgrad(const void* dy2, const void* y1, const float* scale, cons
                        int32_t n, int32_t w1, int32_t w2, void* workspace, int64_t ws_bytes,
                        mia_stream_t stream);
 
-/* EnvNet-v2 conv1 weight + bias gradient with the BatchNorm1+ReLU backward fused into the operand
- * staging (reference src/models/envnet_v2.py:15-17 Conv2d(1, 32, (1, 64), stride (1, 2)) -> BN ->
- * ReLU; replaces cuDNN conv2d backward-weight plus the BN backward's elementwise pass):
- *   g[p][c]  = gamma[c]*invstd[c] * (mask * dact[p][c] - dbeta[c]/P - (y1[p][c]-mean[c])*invstd[c]*dgamma[c]/P),
- *              mask = y1[p][c]*scale[c] + shift[c] > 0,  P = n*w1,  w1 = (t-64)/2+1
- *   dw[c][k] = sum_{b,o} g[b,o][c] * x[b][2o+k]   (k < 64),   dbias[c] = sum_p g[p][c]
- * x f32 (n, t); dact, y1 bf16 (n, w1, 32); dgamma/dbeta from mia_bn_relu_bwd_reduce; dw f32 (32, 64);
- * workspace >= split*(32*64+32) floats.  Deterministic (fixed-order split-K reduce). */
+/* EnvNet-v2 BatchNorm1+ReLU backward and conv1 weight + bias gradient in ONE pass over
+ * (dact, y1, x) (reference src/models/envnet_v2.py:15-17 Conv2d(1, 32, (1, 64), stride (1, 2)) ->
+ * BN -> ReLU; replaces the BN backward reductions, its elementwise pass and cuDNN conv2d
+ * backward-weight).  With dz = mask * dact (mask = y1*scale + shift > 0), xhat = (y1-mean)*invstd:
+ *   dbeta[c] = sum_p dz,  dgamma[c] = sum_p dz*xhat      (outputs)
+ *   g = A dz + B + C y1,  A = gamma*invstd, B = -A dbeta/P + A invstd mean dgamma/P, C = -A invstd dgamma/P
+ *   dw[c][k] = sum_p g[p][c] x[2p+k] = A G1 + B G2 + C G3,  dbias[c] = sum_p g[p][c]
+ * where G1 = sum dz x, G3 = sum y1 x (bf16 MFMA, f32 accumulate), G2[k] = sum x[2p+k]; the
+ * combination runs in double.  P = n*w1, w1 = (t-64)/2+1.  x f32 (n, t); dact, y1 bf16 (n, w1, 32);
+ * dw f32 (32, 64); workspace >= (split*(2*2048+96) + 2*2048 + n*64) floats.  Deterministic. */
 int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int32_t n, int32_t t,
                           const float* scale, const float* shift, const float* gamma, const float* mean,
-                          const float* invstd, const float* dgamma, const float* dbeta, float* dw,
+                          const float* invstd, float* dgamma, float* dbeta, float* dw,
                           float* dbias, void* workspace, int32_t split, mia_stream_t stream);
 
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.

@@ -121,9 +121,9 @@ def test_bn_relu_bwd_masked_apply(cuda, dt):
 
 @pytest.mark.parametrize("n,t", [(3, 220500), (2, 9000)])
 def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
-    """conv1 weight/bias gradient with the BN1+ReLU backward fused into its dY staging == the
-    unfused path (bn_relu_bwd_apply -> bf16 dS1 -> tap wgrad GEMM): identical bf16 dS1 values, so
-    dW agrees to f32 summation order; and within bf16 tolerance of a float64 restatement."""
+    """One-pass BN1+ReLU backward + conv1 weight/bias gradient (linear form) vs the two-pass path
+    (bn_relu_bwd_reduce -> bn_relu_bwd_apply -> bf16 dS1 -> tap wgrad GEMM) and a float64
+    restatement."""
     w1 = (t - 64) // 2 + 1
     P = n * w1
     g = torch.Generator(device=cuda).manual_seed(t + n)
@@ -136,7 +136,7 @@ def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
     dg, db = K.bn_relu_bwd_reduce(da, None, y1, P, 32, bn)
     dw = torch.empty(32, 64, device=cuda)
     dbias = torch.empty(32, device=cuda)
-    K.fe_conv1_wgrad_bn(x, da, y1, n, t, gamma, bn, dg, db, dw, dbias)
+    dg1, db1 = K.fe_conv1_wgrad_bn(x, da, y1, n, t, gamma, bn, dw, dbias)
     # unfused reference path
     dx = torch.empty_like(da)
     dbias_u = torch.empty(32, device=cuda)
@@ -145,9 +145,12 @@ def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
     K.gemm(K.dense(dx, L.RC, P, 32), K.conv(x, L.RC, n, 1, t // 2, 2, 1, w1, 1, 32, row_kind=True),
            K.epilogue(dw_u, 64), 32, 64, P, L.BF16)
     torch.cuda.synchronize()
-    assert rel(dw, dw_u) < 1e-5
+    # one-pass linear form: same BN reductions as the reduce kernel (summation order aside); dW
+    # differs from the two-pass path only by the bf16 rounding of dS1 that the linear form avoids
+    assert rel(dg1, dg) < 1e-5 and rel(db1, db) < 1e-5
+    assert rel(dw, dw_u) < 1e-2
     scale_b = dx.float().abs().sum(0).max()
-    assert (dbias - dbias_u).abs().max() < 1e-5 * scale_b
+    assert (dbias - dbias_u).abs().max() < 1e-3 * scale_b
     # float64 restatement
     y = y1.double()
     z = y * bn.scale.double() + bn.shift.double()
@@ -158,6 +161,7 @@ def test_fe_conv1_wgrad_bn_fused(cuda, n, t):
     cols = x.double().unfold(1, 64, 2)  # (n, w1, 64)
     ref = torch.einsum("npc,npk->ck", d64.view(n, w1, 32), cols)
     assert rel(dw.double(), ref) < 1e-2
+    assert rel(dg1.double(), (dz * xhat).sum(0)) < 1e-4 and rel(db1.double(), dz.sum(0)) < 1e-4
 
 
 @pytest.mark.parametrize("n,t", [(3, 220500), (5, 9000)])
