@@ -1908,17 +1908,20 @@ extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M
   return 0;
 }
 
-// G2[k] = sum_{b, p < w1} x[b][2p + k] (k < 64): per-clip partials, one block per clip.  With
-// r = k & 1, j0 = k >> 1 the window is x_r[j0 .. j0+w1) of the parity sequence x_r[j] = x[2j+r], so
-// G2_b[k] = T_r - (head j < j0) - (tail j >= j0 + w1): one coalesced pass for the two parity
-// totals T_0, T_1 plus at most 31 + 31 boundary samples per k.
+// G2[k] = sum_{b, p < w1} x[b][2p + k] (k < 64).  With r = k & 1, j0 = k >> 1 the window is
+// x_r[j0 .. j0+w1) of the parity sequence x_r[j] = x[2j+r], so G2 = sum_b T_r - (head j < j0) -
+// (tail j >= j0 + w1): C1_SPLIT blocks per clip sum disjoint ranges of the two parities (coalesced
+// 8-byte loads), the first block of each clip also writes the per-k head/tail corrections.
+constexpr int C1_SPLIT = 8;
 __global__ __launch_bounds__(256) void conv1_colsum_kernel(const float* __restrict__ x, int t, int w1,
                                                            float* __restrict__ part) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x / C1_SPLIT, sp = blockIdx.x % C1_SPLIT, tid = threadIdx.x;
   const float* xb = x + (int64_t)b * t;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const int L = t / 2, per = (L + C1_SPLIT - 1) / C1_SPLIT;
+  const int j1 = min(L, (sp + 1) * per);
   float e = 0.f, o = 0.f;
-  for (int j = tid; j < t / 2; j += 256) {
+  for (int j = sp * per + tid; j < j1; j += 256) {
     const f32x2 v = *reinterpret_cast<const f32x2*>(xb + 2 * j);
     e += v[0];
     o += v[1];
@@ -1931,39 +1934,57 @@ __global__ __launch_bounds__(256) void conv1_colsum_kernel(const float* __restri
     if (tid < h) { red[0][tid] += red[0][tid + h]; red[1][tid] += red[1][tid + h]; }
     __syncthreads();
   }
-  if (tid < 64) {
-    const int r = tid & 1, j0 = tid >> 1, L = t / 2;
-    float a = red[r][0];
+  // part[b][sp][0..1] = parity totals of this range; part[b][C1_SPLIT][k] = -(head + tail) of k
+  float* pb = part + (int64_t)b * (C1_SPLIT * 2 + 64);
+  if (tid < 2) pb[sp * 2 + tid] = red[tid][0];
+  if (sp == 0 && tid < 64) {
+    const int r = tid & 1, j0 = tid >> 1;
+    float a = 0.f;
     for (int j = 0; j < j0; ++j) a -= xb[2 * j + r];
     for (int j = j0 + w1; j < L; ++j) a -= xb[2 * j + r];
-    part[(int64_t)b * 64 + tid] = a;
+    pb[C1_SPLIT * 2 + tid] = a;
   }
 }
 
+// per-channel sums over the Z block partials (dbp) and per-k G2 over the clips, in double with a
+// block-wide tree (one block per output quantity: 96 channel sums + 64 G2 entries)
+__global__ __launch_bounds__(256) void conv1_lin_sums_kernel(const float* __restrict__ dbp, int Z,
+                                                             const float* __restrict__ g2part, int n,
+                                                             double* __restrict__ out) {
+  const int q = blockIdx.x, tid = threadIdx.x;
+  double a = 0.0;
+  if (q < 96) {
+    const int ch = q % 32, which = q / 32;
+    for (int z = tid; z < Z; z += 256) a += (double)dbp[((int64_t)z * 32 + ch) * 3 + which];
+  } else {
+    const int k = q - 96, r = k & 1;
+    constexpr int PS = C1_SPLIT * 2 + 64;
+    for (int b = tid; b < n; b += 256) {
+      const float* pb = g2part + (int64_t)b * PS;
+      double s = pb[C1_SPLIT * 2 + k];
+      for (int sp = 0; sp < C1_SPLIT; ++sp) s += (double)pb[sp * 2 + r];
+      a += s;
+    }
+  }
+  __shared__ double red[256];
+  red[tid] = a;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  if (tid == 0) out[q] = red[0];
+}
+
 // dgamma/dbeta, A/B/C per channel (double), dW = A G1 + B G2 + C G3, dbias = A sum dz + B P + C sum y
-__global__ __launch_bounds__(256) void conv1_lin_final_kernel(const float* __restrict__ g13, const float* __restrict__ dbp,
-                                                              int Z, const float* __restrict__ g2part, int n,
+__global__ __launch_bounds__(256) void conv1_lin_final_kernel(const float* __restrict__ g13, const double* __restrict__ sums,
                                                               int64_t P, const float* gamma, const float* mean,
                                                               const float* invstd, float* dgamma, float* dbeta,
                                                               float* dw, float* dbias) {
-  __shared__ double cA[32], cB[32], cC[32], g2[64];
+  __shared__ double cA[32], cB[32], cC[32];
   const int t = threadIdx.x;
-  if (t < 96) {
-    const int ch = t % 32, q = t / 32;
-    double a = 0.0;
-    for (int z = 0; z < Z; ++z) a += (double)dbp[((int64_t)z * 32 + ch) * 3 + q];
-    if (q == 0) cA[ch] = a;       // sum dz  (= dbeta)
-    else if (q == 1) cB[ch] = a;  // sum dz*xhat (= dgamma)
-    else cC[ch] = a;              // sum y
-  }
-  if (t >= 128 && t < 192) {
-    double a = 0.0;
-    for (int b = 0; b < n; ++b) a += (double)g2part[(int64_t)b * 64 + (t - 128)];
-    g2[t - 128] = a;
-  }
-  __syncthreads();
   if (t < 32) {
-    const double sdz = cA[t], sdx = cB[t], sy = cC[t];
+    const double sdz = sums[t], sdx = sums[32 + t], sy = sums[64 + t];
     dbeta[t] = (float)sdz;
     dgamma[t] = (float)sdx;
     const double is = invstd[t], A = (gamma ? (double)gamma[t] : 1.0) * is;
@@ -1975,7 +1996,7 @@ __global__ __launch_bounds__(256) void conv1_lin_final_kernel(const float* __res
   __syncthreads();
   for (int e = t; e < 32 * 64; e += 256) {
     const int ch = e / 64, k = e % 64;
-    dw[e] = (float)(cA[ch] * (double)g13[e] + cB[ch] * g2[k] + cC[ch] * (double)g13[2048 + e]);
+    dw[e] = (float)(cA[ch] * (double)g13[e] + cB[ch] * sums[96 + k] + cC[ch] * (double)g13[2048 + e]);
   }
 }
 
@@ -2001,7 +2022,9 @@ extern "C" int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const voi
   r.dbp = ws + (int64_t)split * 2 * 2048;          // [split][32][3]
   r.bP = (int64_t)n * w1;
   float* g13 = r.dbp + (int64_t)split * 96;        // [2][32][64]
-  float* g2p = g13 + 2 * 2048;                     // [n][64]
+  float* g2p = g13 + 2 * 2048;                     // [n][C1_SPLIT*2 + 64]
+  double* sums = reinterpret_cast<double*>(g2p + (int64_t)n * (C1_SPLIT * 2 + 64) + 1);  // [160], 8-B aligned below
+  sums = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(sums) + 7) & ~uintptr_t(7));
   hipStream_t s = as_stream(stream);
   hipError_t err = tapwgrad_launch<bf16, float, 2, 1, 64, true>(r, s);
   if (err != hipSuccess) return mia::fail(-(int)err, "fe_conv1_wgrad_bn launch: %s", hipGetErrorString(err));
@@ -2009,9 +2032,9 @@ extern "C" int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const voi
   e.ptr = reinterpret_cast<char*>(g13); e.dtype = MIA_F32; e.act = MIA_ACT_NONE; e.ldc = 2 * 2048; e.alpha = 1.f;
   e.act_scale = 1.f;
   launch_splitk_reduce(ws, split, 1, 2 * 2048, e, s);  // slabs [split][4096] -> g13
-  conv1_colsum_kernel<<<n, 256, 0, s>>>(x, t, w1, g2p);
-  conv1_lin_final_kernel<<<1, 256, 0, s>>>(g13, r.dbp, split, g2p, n, r.bP, gamma, mean, invstd, dgamma, dbeta, dw,
-                                           dbias);
+  conv1_colsum_kernel<<<n * C1_SPLIT, 256, 0, s>>>(x, t, w1, g2p);
+  conv1_lin_sums_kernel<<<96 + 64, 256, 0, s>>>(r.dbp, split, g2p, n, sums);
+  conv1_lin_final_kernel<<<1, 256, 0, s>>>(g13, sums, r.bP, gamma, mean, invstd, dgamma, dbeta, dw, dbias);
   MIA_LAUNCH_CHECK("fe_conv1_wgrad_bn final");
   return 0;
 }

@@ -368,7 +368,7 @@ def fe_conv1_wgrad_bn(x: torch.Tensor, dact: torch.Tensor, y1: torch.Tensor, n: 
     assert dact.numel() == n * w1 * 32 and y1.numel() == n * w1 * 32 and x.numel() == n * t
     assert dw.numel() == 32 * 64 and dw.dtype == torch.float32 and dbias.numel() == 32
     split = 512
-    ws = workspace((split * (2 * 2048 + 96) + 2 * 2048 + n * 64) * 4, x.device, "tapw")
+    ws = workspace((split * (2 * 2048 + 96) + 2 * 2048 + n * 80 + 2 * 160 + 4) * 4, x.device, "tapw")
     g = torch.empty(2, 32, dtype=torch.float32, device=x.device)
     flop = 4.0 * n * w1 * 32 * 64
     with probe(tag or "", flop, (dact.numel() + y1.numel()) * 2 + x.numel() * 4):

@@ -245,7 +245,7 @@ int mia_fe_conv2_wgrad(const void* dy2, const void* y1, const float* scale, cons
  *   dw[c][k] = sum_p g[p][c] x[2p+k] = A G1 + B G2 + C G3,  dbias[c] = sum_p g[p][c]
  * where G1 = sum dz x, G3 = sum y1 x (bf16 MFMA, f32 accumulate), G2[k] = sum x[2p+k]; the
  * combination runs in double.  P = n*w1, w1 = (t-64)/2+1.  x f32 (n, t); dact, y1 bf16 (n, w1, 32);
- * dw f32 (32, 64); workspace >= (split*(2*2048+96) + 2*2048 + n*64) floats.  Deterministic. */
+ * dw f32 (32, 64); workspace >= (split*(2*2048+96) + 2*2048 + n*80 + 2*160 + 4) floats.  Deterministic. */
 int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int32_t n, int32_t t,
                           const float* scale, const float* shift, const float* gamma, const float* mean,
                           const float* invstd, float* dgamma, float* dbeta, float* dw,
