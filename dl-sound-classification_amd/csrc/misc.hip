@@ -205,24 +205,46 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
                     reinterpret_cast<uintptr_t>(v)) & 15) == 0 && (reinterpret_cast<uintptr_t>(sw) & 7) == 0;
   int64_t done = 0;
   if (al) {
+    // four float4 groups per iteration, all 16 loads issued before any use (one HBM round trip per
+    // 4 groups); every byte is touched once, so loads and stores are non-temporal (no L2/MALL
+    // allocation for a 10 GB once-through stream)
     const int64_t n4 = n >> 2;
-    for (int64_t i = tid; i < n4; i += nthr) {
-      float4 pv = reinterpret_cast<float4*>(p)[i];
-      const float4 gv = reinterpret_cast<const float4*>(g)[i];
-      float4 mv = reinterpret_cast<float4*>(m)[i];
-      float4 vv = reinterpret_cast<float4*>(v)[i];
-      pv.x = upd(pv.x, gv.x, mv.x, vv.x);
-      pv.y = upd(pv.y, gv.y, mv.y, vv.y);
-      pv.z = upd(pv.z, gv.z, mv.z, vv.z);
-      pv.w = upd(pv.w, gv.w, mv.w, vv.w);
-      reinterpret_cast<float4*>(p)[i] = pv;
-      reinterpret_cast<float4*>(m)[i] = mv;
-      reinterpret_cast<float4*>(v)[i] = vv;
-      if (sw) {
-        const bf16x4 b4 = {(bf16)pv.x, (bf16)pv.y, (bf16)pv.z, (bf16)pv.w};
-        reinterpret_cast<bf16x4*>(sw)[i] = b4;
+    constexpr int U = 4;
+    f32x4* p4 = reinterpret_cast<f32x4*>(p);
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+    f32x4* m4 = reinterpret_cast<f32x4*>(m);
+    f32x4* v4 = reinterpret_cast<f32x4*>(v);
+    auto step4 = [&](int64_t i, f32x4 pv, f32x4 gv, f32x4 mv, f32x4 vv) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = mv[e], b = vv[e];
+        pv[e] = upd(pv[e], gv[e], a, b);
+        mv[e] = a;
+        vv[e] = b;
       }
+      __builtin_nontemporal_store(pv, p4 + i);
+      __builtin_nontemporal_store(mv, m4 + i);
+      __builtin_nontemporal_store(vv, v4 + i);
+      if (sw) {
+        const bf16x4 b4 = {(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+        __builtin_nontemporal_store(b4, reinterpret_cast<bf16x4*>(sw) + i);
+      }
+    };
+    int64_t i = tid;
+    for (; i + (U - 1) * nthr < n4; i += U * nthr) {
+      f32x4 pv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = i + u * nthr;
+        pv[u] = __builtin_nontemporal_load(p4 + j);
+        gv[u] = __builtin_nontemporal_load(g4 + j);
+        mv[u] = __builtin_nontemporal_load(m4 + j);
+        vv[u] = __builtin_nontemporal_load(v4 + j);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) step4(i + u * nthr, pv[u], gv[u], mv[u], vv[u]);
     }
+    for (; i < n4; i += nthr) step4(i, p4[i], g4[i], m4[i], v4[i]);
     done = n4 << 2;
   }
   for (int64_t i = done + tid; i < n; i += nthr) {
@@ -436,7 +458,7 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   MIA_LAUNCH_CHECK("norm_final");
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  const int ablocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(max_numel, 256 * 16)));
+  const int ablocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(max_numel, 256 * 32)));
   adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, shadow_bf16, sizes, coef,
                                                      (float)(lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
                                                      weight_decay);
