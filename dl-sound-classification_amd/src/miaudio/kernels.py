@@ -379,6 +379,25 @@ def fe_conv1_wgrad_bn(x: torch.Tensor, dact: torch.Tensor, y1: torch.Tensor, n: 
     return g[0], g[1]
 
 
+def bn_relu_apply(x: torch.Tensor, P: int, C: int, bn: BNState, out: torch.Tensor):
+    """out = bf16(relu(x * bn.scale + bn.shift)) for bf16 (P, C) activations."""
+    assert x.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and x.numel() == P * C == out.numel()
+    L.check(L.load().mia_bn_relu_apply(x.data_ptr(), P, C, bn.scale.data_ptr(), bn.shift.data_ptr(), out.data_ptr(),
+                                       _s()), "mia_bn_relu_apply")
+
+
+def trunk_wgrad_w2(dy: torch.Tensor, a: torch.Tensor, rows: int, w: int, cout: int, cin: int, dw: torch.Tensor,
+                   tag: str | None = None):
+    """Weight gradient of a (1, 2) conv, stride 1 (EnvNet trunk blocks 3-4) as one dense GEMM:
+    dy bf16 (rows*(w-1), cout), a bf16 (rows*w, cin) = the conv input -> dw f32 (cout, 2*cin) OHWI."""
+    assert dy.dtype == torch.bfloat16 and a.dtype == torch.bfloat16 and dw.dtype == torch.float32
+    assert dy.numel() == rows * (w - 1) * cout and a.numel() == rows * w * cin and dw.numel() == cout * 2 * cin
+    P = rows * w
+    ash = workspace(P * 2 * cout * 2, dy.device, "w2shift")[: P * 2 * cout * 2].view(torch.bfloat16)
+    L.check(L.load().mia_shift_pad_w2(dy.data_ptr(), rows, w, cout, ash.data_ptr(), _s()), "mia_shift_pad_w2")
+    gemm(dense(ash, L.RC, P, 2 * cout), dense(a, L.RC, P, cin), epilogue(dw, cin), 2 * cout, cin, P, L.BF16, tag=tag)
+
+
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:
     cout, cin, kh, kw = src.shape
     out = torch.empty(src.numel(), dtype=L.torch_dtype(dtype), device=src.device)

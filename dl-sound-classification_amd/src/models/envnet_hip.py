@@ -291,10 +291,16 @@ class EnvNetFunction(torch.autograd.Function):
             # wgrad b: dW[co][(ky,kx,ci)] = sum_pix dyb[pix][co] * relu(bn_a(ya))[pix + tap][ci]
             Kb = kh2 * kw2 * cin2
             dWb = torch.empty(cout2, Kb, dtype=torch.float32, device=dev)
-            K.gemm(K.dense(dyb, L.RC, Pb, cout2),
-                   K.conv(ts["ya"], L.RC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU,
-                          scale=ts["bna"].scale, shift=ts["bna"].shift),
-                   K.epilogue(dWb, Kb), cout2, Kb, Pb, cd, tag=f"t{blk}b.wgrad")
+            if cd == L.BF16 and kh2 == 1 and kw2 == 2:
+                # (1, 2) conv: one dense GEMM over shifted dY and the BN+ReLU'd input
+                act = torch.empty(B * ha * wa, cin2, dtype=tdt, device=dev)
+                K.bn_relu_apply(ts["ya"], B * ha * wa, cin2, ts["bna"], act)
+                K.trunk_wgrad_w2(dyb, act, B * ha, wa, cout2, cin2, dWb, tag=f"t{blk}b.wgrad")
+            else:
+                K.gemm(K.dense(dyb, L.RC, Pb, cout2),
+                       K.conv(ts["ya"], L.RC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU,
+                              scale=ts["bna"].scale, shift=ts["bna"].shift),
+                       K.epilogue(dWb, Kb), cout2, Kb, Pb, cd, tag=f"t{blk}b.wgrad")
             gwb = torch.empty_like(p[pa + 4])
             K.unpack_ohwi_grad(dWb, p[pa + 4].shape, gwb)
             grads[pa + 4] = gwb
@@ -314,11 +320,16 @@ class EnvNetFunction(torch.autograd.Function):
             # wgrad a
             Ka = kh * kw * cin
             dWa = torch.empty(cout, Ka, dtype=torch.float32, device=dev)
-            if cin == 1:
-                Bop = K.conv(ts["inp"], L.RC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+            if cd == L.BF16 and kh == 1 and kw == 2 and cin > 1:
+                K.trunk_wgrad_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, dWa,
+                                 tag=f"t{blk}a.wgrad")
             else:
-                Bop = K.conv(ts["inp"], L.RC, B, H, W, cin, ha, wa, kh, kw)
-            K.gemm(K.dense(dya, L.RC, Pa, cout), Bop, K.epilogue(dWa, Ka), cout, Ka, Pa, cd, tag=f"t{blk}a.wgrad")
+                if cin == 1:
+                    Bop = K.conv(ts["inp"], L.RC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+                else:
+                    Bop = K.conv(ts["inp"], L.RC, B, H, W, cin, ha, wa, kh, kw)
+                K.gemm(K.dense(dya, L.RC, Pa, cout), Bop, K.epilogue(dWa, Ka), cout, Ka, Pa, cd,
+                       tag=f"t{blk}a.wgrad")
             gwa = torch.empty_like(p[pa])
             K.unpack_ohwi_grad(dWa, p[pa].shape, gwa)
             grads[pa] = gwa

@@ -251,6 +251,18 @@ int mia_fe_conv1_wgrad_bn(const float* x, const void* dact, const void* y1, int3
                           const float* invstd, float* dgamma, float* dbeta, float* dw,
                           float* dbias, void* workspace, int32_t split, mia_stream_t stream);
 
+/* EnvNet-v2 trunk (1, 2) conv weight gradient as one dense GEMM (reference
+ * src/models/envnet_v2.py:38-49; replaces cuDNN conv2d backward-weight for those layers):
+ *   dW[co][kx][ci] = sum_q Ashift[q][co*2+kx] * a[q][ci]  over the input pixels q,
+ * Ashift from mia_shift_pad_w2, a = the conv input (after mia_bn_relu_apply when the layer's input
+ * is relu(bn(.))); the GEMM itself is mia_gemm on two DENSE K-major (RC) bf16 operands. */
+/* out = bf16(relu(x*scale + shift)), x/out bf16 (P, C), C % 8 == 0, 16-byte aligned. */
+int mia_bn_relu_apply(const void* x, int64_t P, int32_t C, const float* scale, const float* shift, void* out,
+                      mia_stream_t stream);
+/* out[r][x][2c+kx] = dy[r][x-kx][c] (0 <= x-kx < w-1, else 0): dy bf16 (rows, w-1, c), out bf16
+ * (rows, w, 2c), c % 8 == 0, 16-byte aligned. */
+int mia_shift_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t c, void* out, mia_stream_t stream);
+
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
  * mode 0: OHWI (cout, kh, kw, cin)            — forward operand
  * mode 1: flipped dgrad operand (cin, kh, kw, cout) with ky->kh-1-ky, kx->kw-1-kx
