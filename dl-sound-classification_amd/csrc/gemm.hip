@@ -1704,7 +1704,9 @@ int check_operand(const MiaOperand& o, const char* name) {
     MIA_CHECK_ARG(o.pre_scale && o.pre_shift && o.kind != MIA_OP_CONVROW,
                   "gemm: operand %s affine pre-op needs scale/shift and a DENSE/CONV source", name);
   if (o.kind == MIA_OP_DENSE) {
-    MIA_CHECK_ARG(o.rows >= 0 && o.cols >= 0 && o.ld >= o.cols, "gemm: operand %s dense extents", name);
+    // ld < cols is allowed: overlapping rows are a valid read-only view (the (1, 2)-conv im2col of
+    // a channels-last map is the map itself with ld = C, cols = 2C)
+    MIA_CHECK_ARG(o.rows >= 0 && o.cols >= 0 && o.ld > 0, "gemm: operand %s dense extents", name);
   } else {
     MIA_CHECK_ARG(o.n > 0 && o.h > 0 && o.w > 0 && o.c > 0 && o.oh > 0 && o.ow > 0 && o.kh > 0 &&
                       o.kw > 0 && o.sh > 0 && o.sw > 0,

@@ -5,6 +5,11 @@
 //   dW[co][kx][ci] = sum_{b,y,x<W-1} dY[b][y][x][co] * a[b][y][x+kx][ci]
 //                  = sum_{input pixels q} Ashift[q][co*2 + kx] * a[q][ci]
 // with Ashift[b][y][x][co*2 + kx] = dY[b][y][x-kx][co] (zero where x-kx is outside [0, W-1)).
+// The forward over every input pixel q (the last column of each row is computed and dropped) is
+//   y[q][co] = sum_{kx,ci} W[co][kx][ci] * a[q + kx][ci] = a_view[q][kx*Cin + ci] . W^T
+// with a_view the map itself read with row stride Cin and row length 2 Cin (overlapping rows), and
+// the input gradient is dX[q][ci] = sum_{co,kx} Ashift[q][co*2 + kx] * W[co][kx][ci]: all three
+// are dense GEMMs on the LDS-DMA kernel.
 // So the weight gradient is a plain (2 Cout) x Cin x (pixels) GEMM of two dense K-major operands,
 // whose output rows (co*2 + kx) are already the OHWI gradient layout.  The two helpers below build
 // Ashift (one pass over dY) and the BN+ReLU'd input a = bf16(relu(x*scale + shift)) (one pass over
@@ -71,6 +76,20 @@ __global__ __launch_bounds__(256) void shift_pad2_kernel(const bf16* __restrict_
   }
 }
 
+// dst[r][x] = src[r][x] for x < w-1 (drops the padded last column of a (1, 2)-conv forward
+// computed over every input pixel), 16 B per thread
+__global__ __launch_bounds__(256) void drop_last_col_kernel(const u32x4* __restrict__ src, int64_t rows, int w,
+                                                            int c16, u32x4* __restrict__ dst) {
+  const int64_t total = rows * (w - 1) * c16;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / c16;
+    const int k = (int)(i - pix * c16);
+    const int64_t r = pix / (w - 1);
+    const int x = (int)(pix - r * (w - 1));
+    dst[i] = src[(r * w + x) * c16 + k];
+  }
+}
+
 int grid_for(int64_t work) {
   const int64_t b = (work + 255) / 256;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -96,5 +115,14 @@ extern "C" int mia_shift_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t
   shift_pad2_kernel<<<grid_for(rows * w * (c / 8)), 256, 0, as_stream(stream)>>>(
       reinterpret_cast<const bf16*>(dy), rows, w, c, reinterpret_cast<bf16*>(out));
   MIA_LAUNCH_CHECK("shift_pad_w2");
+  return 0;
+}
+
+extern "C" int mia_drop_last_col(const void* src, int64_t rows, int32_t w, int32_t c, void* dst, mia_stream_t stream) {
+  MIA_CHECK_ARG(src && dst && rows > 0 && w >= 2 && c > 0 && c % 8 == 0, "drop_last_col: bad arguments");
+  MIA_CHECK_ARG(al16(src) && al16(dst), "drop_last_col: src / dst must be 16-byte aligned");
+  drop_last_col_kernel<<<grid_for(rows * (w - 1) * (c / 8)), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const u32x4*>(src), rows, w, c / 8, reinterpret_cast<u32x4*>(dst));
+  MIA_LAUNCH_CHECK("drop_last_col");
   return 0;
 }

@@ -386,16 +386,39 @@ def bn_relu_apply(x: torch.Tensor, P: int, C: int, bn: BNState, out: torch.Tenso
                                        _s()), "mia_bn_relu_apply")
 
 
-def trunk_wgrad_w2(dy: torch.Tensor, a: torch.Tensor, rows: int, w: int, cout: int, cin: int, dw: torch.Tensor,
-                   tag: str | None = None):
-    """Weight gradient of a (1, 2) conv, stride 1 (EnvNet trunk blocks 3-4) as one dense GEMM:
-    dy bf16 (rows*(w-1), cout), a bf16 (rows*w, cin) = the conv input -> dw f32 (cout, 2*cin) OHWI."""
+def conv_w2_fwd(x: torch.Tensor, rows: int, w: int, cin: int, wpk: torch.Tensor, bias, out: torch.Tensor,
+                tag: str | None = None):
+    """(1, 2) conv forward, stride 1 (EnvNet trunk blocks 3-4), as one dense GEMM over every input
+    pixel (rows of the im2col view overlap: ld = cin, length 2*cin) + a drop of the last column.
+    x bf16 (rows*w, cin) whose storage holds ONE extra pixel (read by the dropped last output);
+    wpk bf16 (cout, 2*cin) OHWI; out bf16 (rows*(w-1), cout)."""
+    cout = wpk.numel() // (2 * cin)
+    assert x.dtype == torch.bfloat16 and wpk.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
+    assert x.numel() == rows * w * cin and out.numel() == rows * (w - 1) * cout
+    assert x.untyped_storage().nbytes() - x.storage_offset() * 2 >= (rows * w + 1) * cin * 2, "x needs a pad pixel"
+    P = rows * w
+    ypad = workspace(P * cout * 2, x.device, "w2fwd")[: P * cout * 2].view(torch.bfloat16)
+    gemm(dense(x, L.KC, P, 2 * cin, ld=cin), dense(wpk, L.KC, cout, 2 * cin), epilogue(ypad, cout, bias=bias),
+         P, cout, 2 * cin, L.BF16, tag=tag)
+    L.check(L.load().mia_drop_last_col(ypad.data_ptr(), rows, w, cout, out.data_ptr(), _s()), "mia_drop_last_col")
+
+
+def trunk_bwd_w2(dy: torch.Tensor, a: torch.Tensor, rows: int, w: int, cout: int, cin: int, wpk: torch.Tensor,
+                 dw: torch.Tensor, dx: torch.Tensor, tag: str = ""):
+    """Backward of a (1, 2) conv, stride 1 (EnvNet trunk blocks 3-4): one pass builds the shifted
+    gradient Ashift[q][co*2+kx] = dy[q-kx][co] over the input pixels, then two dense GEMMs:
+    dw (cout, 2*cin) OHWI f32 = Ashift^T a, and dx (rows*w, cin) bf16 = Ashift W (W = wpk (cout, 2*cin),
+    read as the (2*cout, cin) K-major matrix it already is)."""
     assert dy.dtype == torch.bfloat16 and a.dtype == torch.bfloat16 and dw.dtype == torch.float32
     assert dy.numel() == rows * (w - 1) * cout and a.numel() == rows * w * cin and dw.numel() == cout * 2 * cin
+    assert dx.numel() == rows * w * cin and dx.dtype == torch.bfloat16 and wpk.numel() == cout * 2 * cin
     P = rows * w
     ash = workspace(P * 2 * cout * 2, dy.device, "w2shift")[: P * 2 * cout * 2].view(torch.bfloat16)
     L.check(L.load().mia_shift_pad_w2(dy.data_ptr(), rows, w, cout, ash.data_ptr(), _s()), "mia_shift_pad_w2")
-    gemm(dense(ash, L.RC, P, 2 * cout), dense(a, L.RC, P, cin), epilogue(dw, cin), 2 * cout, cin, P, L.BF16, tag=tag)
+    gemm(dense(ash, L.RC, P, 2 * cout), dense(a, L.RC, P, cin), epilogue(dw, cin), 2 * cout, cin, P, L.BF16,
+         tag=f"{tag}.wgrad" if tag else None)
+    gemm(dense(ash, L.KC, P, 2 * cout), dense(wpk, L.RC, 2 * cout, cin), epilogue(dx, cin), P, cin, 2 * cout,
+         L.BF16, tag=f"{tag}.dgrad" if tag else None)
 
 
 def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:

@@ -164,28 +164,42 @@ class EnvNetFunction(torch.autograd.Function):
             pa = 8 + 8 * blk
             wa_ = K.pack_weight(p[pa], cd, 0)
             ya = torch.empty(B * ha * wa, cout, dtype=tdt, device=dev)
-            if cin == 1:
-                A = K.conv(inp, L.KC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+            dense_w2 = cd == L.BF16 and kh == 1 and kw == 2 and cin > 1  # blocks 3-4: (1, 2) convs
+            if dense_w2:
+                # (1, 2) conv as one dense GEMM over every input pixel (the input map carries a pad pixel)
+                K.conv_w2_fwd(inp.reshape(B * H * W, cin), B * H, W, cin, wa_, p[pa + 1], ya, tag=f"t{blk}a.fwd")
             else:
-                A = K.conv(inp, L.KC, B, H, W, cin, ha, wa, kh, kw)
-            K.gemm(A, K.dense(wa_, L.KC, cout, kh * kw * cin), K.epilogue(ya, cout, bias=p[pa + 1]),
-                   B * ha * wa, cout, kh * kw * cin, cd, tag=f"t{blk}a.fwd")
+                if cin == 1:
+                    A = K.conv(inp, L.KC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
+                else:
+                    A = K.conv(inp, L.KC, B, H, W, cin, ha, wa, kh, kw)
+                K.gemm(A, K.dense(wa_, L.KC, cout, kh * kw * cin), K.epilogue(ya, cout, bias=p[pa + 1]),
+                       B * ha * wa, cout, kh * kw * cin, cd, tag=f"t{blk}a.fwd")
             bna = bn(2 + 2 * blk, ya, B * ha * wa, cout)
             _, _, cin2, cout2, kh2, kw2 = TRUNK[2 * blk + 1]
             wb_ = K.pack_weight(p[pa + 4], cd, 0)
             yb = torch.empty(B * hb * wb, cout2, dtype=tdt, device=dev)
-            A = K.conv(ya, L.KC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU, scale=bna.scale,
-                       shift=bna.shift)
-            K.gemm(A, K.dense(wb_, L.KC, cout2, kh2 * kw2 * cin2), K.epilogue(yb, cout2, bias=p[pa + 5]),
-                   B * hb * wb, cout2, kh2 * kw2 * cin2, cd, tag=f"t{blk}b.fwd")
+            act = None
+            if dense_w2:
+                # relu(bn_a(ya)) materialised once (bf16, + pad pixel): the forward GEMM's A operand and
+                # the backward weight-gradient operand
+                act = torch.empty(B * ha * wa + 1, cin2, dtype=tdt, device=dev)[: B * ha * wa]
+                K.bn_relu_apply(ya, B * ha * wa, cin2, bna, act)
+                K.conv_w2_fwd(act, B * ha, wa, cin2, wb_, p[pa + 5], yb, tag=f"t{blk}b.fwd")
+            else:
+                A = K.conv(ya, L.KC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU, scale=bna.scale,
+                           shift=bna.shift)
+                K.gemm(A, K.dense(wb_, L.KC, cout2, kh2 * kw2 * cin2), K.epilogue(yb, cout2, bias=p[pa + 5]),
+                       B * hb * wb, cout2, kh2 * kw2 * cin2, cd, tag=f"t{blk}b.fwd")
             bnb = bn(3 + 2 * blk, yb, B * hb * wb, cout2)
             ph, pw = TRUNK_POOL[blk]
             last = blk == 3
+            # (non-last pools carry one pad pixel: the next block's dense (1, 2)-conv view reads it)
             pooled = torch.empty(B, cout2, hp, wp, dtype=tdt, device=dev) if last else \
-                torch.empty(B, hp, wp, cout2, dtype=tdt, device=dev)
+                torch.empty(B * hp * wp + 1, cout2, dtype=tdt, device=dev)[: B * hp * wp].view(B, hp, wp, cout2)
             am = torch.empty(B, hp, wp, cout2, dtype=torch.uint8, device=dev)
             K.pool_fwd(yb, B, hb, wb, cout2, ph, pw, bnb, pooled, 2 if last else 0, am)
-            trunk_saved.append(dict(inp=inp, ya=ya, yb=yb, bna=bna, bnb=bnb, am=am))
+            trunk_saved.append(dict(inp=inp, ya=ya, yb=yb, bna=bna, bnb=bnb, am=am, act=act))
             inp = pooled
         flat = inp.reshape(B, -1)
         saved["trunk"] = trunk_saved
@@ -291,26 +305,25 @@ class EnvNetFunction(torch.autograd.Function):
             # wgrad b: dW[co][(ky,kx,ci)] = sum_pix dyb[pix][co] * relu(bn_a(ya))[pix + tap][ci]
             Kb = kh2 * kw2 * cin2
             dWb = torch.empty(cout2, Kb, dtype=torch.float32, device=dev)
-            if cd == L.BF16 and kh2 == 1 and kw2 == 2:
-                # (1, 2) conv: one dense GEMM over shifted dY and the BN+ReLU'd input
-                act = torch.empty(B * ha * wa, cin2, dtype=tdt, device=dev)
-                K.bn_relu_apply(ts["ya"], B * ha * wa, cin2, ts["bna"], act)
-                K.trunk_wgrad_w2(dyb, act, B * ha, wa, cout2, cin2, dWb, tag=f"t{blk}b.wgrad")
+            Pa = B * ha * wa
+            da = torch.empty(Pa, cout, dtype=tdt, device=dev)
+            if ts["act"] is not None:
+                # (1, 2) conv: shifted dY once, then wgrad and dgrad as two dense GEMMs
+                K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, K.pack_weight(p[pa + 4], cd, 0), dWb, da,
+                               tag=f"t{blk}b")
             else:
                 K.gemm(K.dense(dyb, L.RC, Pb, cout2),
                        K.conv(ts["ya"], L.RC, B, ha, wa, cin2, hb, wb, kh2, kw2, pre=L.PRE_AFFINE_RELU,
                               scale=ts["bna"].scale, shift=ts["bna"].shift),
                        K.epilogue(dWb, Kb), cout2, Kb, Pb, cd, tag=f"t{blk}b.wgrad")
+                # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
+                wbf = K.pack_weight(p[pa + 4], cd, 1)
+                Kdb = kh2 * kw2 * cout2
+                K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
+                       K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd, tag=f"t{blk}b.dgrad")
             gwb = torch.empty_like(p[pa + 4])
             K.unpack_ohwi_grad(dWb, p[pa + 4].shape, gwb)
             grads[pa + 4] = gwb
-            # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
-            Pa = B * ha * wa
-            wbf = K.pack_weight(p[pa + 4], cd, 1)
-            da = torch.empty(Pa, cout, dtype=tdt, device=dev)
-            Kdb = kh2 * kw2 * cout2
-            K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
-                   K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd, tag=f"t{blk}b.dgrad")
             dga, dba = K.bn_relu_bwd_reduce(da, None, ts["ya"], Pa, cout, ts["bna"])
             grads[pa + 2], grads[pa + 3] = dga, dba
             dbias_a = torch.empty(cout, dtype=torch.float32, device=dev)
@@ -320,9 +333,11 @@ class EnvNetFunction(torch.autograd.Function):
             # wgrad a
             Ka = kh * kw * cin
             dWa = torch.empty(cout, Ka, dtype=torch.float32, device=dev)
-            if cd == L.BF16 and kh == 1 and kw == 2 and cin > 1:
-                K.trunk_wgrad_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, dWa,
-                                 tag=f"t{blk}a.wgrad")
+            dense_w2 = ts["act"] is not None
+            if dense_w2:
+                dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
+                K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, K.pack_weight(p[pa], cd, 0),
+                               dWa, dinp, tag=f"t{blk}a")
             else:
                 if cin == 1:
                     Bop = K.conv(ts["inp"], L.RC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
@@ -334,7 +349,9 @@ class EnvNetFunction(torch.autograd.Function):
             K.unpack_ohwi_grad(dWa, p[pa].shape, gwa)
             grads[pa] = gwa
             # dgrad a -> gradient of the block input (pooled map of the previous stage)
-            if cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32:
+            if dense_w2:
+                pass  # computed with the weight gradient above
+            elif cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32:
                 # 1-channel 8x8 conv: one sweep over dY rows, kernel row ky on the MFMA N side
                 dinp = torch.empty(B, H, W, dtype=tdt, device=dev)
                 K.conv1ch_dgrad(dya, p[pa], B, ha, wa, dinp, tag=f"t{blk}a.dgrad")

@@ -262,6 +262,8 @@ int mia_bn_relu_apply(const void* x, int64_t P, int32_t C, const float* scale, c
 /* out[r][x][2c+kx] = dy[r][x-kx][c] (0 <= x-kx < w-1, else 0): dy bf16 (rows, w-1, c), out bf16
  * (rows, w, 2c), c % 8 == 0, 16-byte aligned. */
 int mia_shift_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t c, void* out, mia_stream_t stream);
+/* dst[r][x] = src[r][x] for x < w-1: src bf16 (rows, w, c) -> dst (rows, w-1, c); c % 8 == 0. */
+int mia_drop_last_col(const void* src, int64_t rows, int32_t w, int32_t c, void* dst, mia_stream_t stream);
 
 /* Weight repack: src f32 (cout, cin, kh, kw) (PyTorch OIHW) -> dst dtype.
  * mode 0: OHWI (cout, kh, kw, cin)            — forward operand

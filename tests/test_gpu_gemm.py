@@ -536,26 +536,40 @@ def test_fe_conv2_wgrad(cuda, n, w1, pre):
 
 
 @pytest.mark.parametrize("B,H,W,cin,cout", [(3, 4, 37, 64, 128), (2, 10, 67, 256, 256)])
-def test_trunk_wgrad_w2_dense(cuda, B, H, W, cin, cout):
-    """(1, 2)-conv weight gradient as one dense GEMM over the shifted dY and the BN+ReLU'd input
-    (EnvNet trunk blocks 3-4) vs a float64 restatement on the same bf16 operands."""
+def test_trunk_w2_dense(cuda, B, H, W, cin, cout):
+    """(1, 2) conv (EnvNet trunk blocks 3-4) as dense GEMMs: forward over every input pixel with
+    overlapping im2col rows + last-column drop, and the backward (shifted dY once, then wgrad and
+    dgrad GEMMs) vs float64 restatements on the same bf16 operands; BN+ReLU materialisation."""
     g = torch.Generator().manual_seed(W + cin)
     x = torch.randn(B * H * W, cin, generator=g).to(torch.bfloat16)
     dy = (torch.randn(B * H * (W - 1), cout, generator=g) * 0.1).to(torch.bfloat16)
+    Wt = torch.randn(cout, cin, 1, 2, generator=g) * 0.05
+    bias = torch.randn(cout, generator=g)
     sc = torch.rand(cin, generator=g) + 0.5
     sh = torch.randn(cin, generator=g) * 0.3
     st = K.BNState(torch.zeros(cin, device=cuda), torch.ones(cin, device=cuda), sc.to(cuda), sh.to(cuda))
-    a = torch.empty(B * H * W, cin, dtype=torch.bfloat16, device=cuda)
+    a = torch.empty(B * H * W + 1, cin, dtype=torch.bfloat16, device=cuda)[: B * H * W]
     K.bn_relu_apply(x.to(cuda), B * H * W, cin, st, a)
+    wpk = K.pack_weight(Wt.to(cuda), L.BF16, 0)
+    y = torch.full((B * H * (W - 1), cout), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.conv_w2_fwd(a, B * H, W, cin, wpk, bias.to(cuda), y)
     dw = torch.full((cout, 2 * cin), float("nan"), device=cuda)
-    K.trunk_wgrad_w2(dy.to(cuda), a, B * H, W, cout, cin, dw)
+    dx = torch.full((B * H * W, cin), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.trunk_bwd_w2(dy.to(cuda), a, B * H, W, cout, cin, wpk, dw, dx)
     torch.cuda.synchronize()
     ar = torch.relu(x.float() * sc + sh).to(torch.bfloat16)
     # fused multiply-add in the kernel vs mul+add here: at most one bf16 rounding step apart
     assert torch.allclose(a.cpu().float(), ar.float(), rtol=8e-3, atol=1e-6)
     a4 = a.cpu().double().view(B * H, W, cin)
     d4 = dy.double().view(B * H, W - 1, cout)
+    wb = Wt.to(torch.bfloat16).double()[:, :, 0, :]  # (co, ci, kx)
+    yref = sum(torch.einsum("rxi,oi->rxo", a4[:, kx:kx + W - 1], wb[:, :, kx]) for kx in range(2)) + bias.double()
+    assert rel(y.double().cpu().view(B * H, W - 1, cout), yref) < 1e-2
     ref = torch.stack([torch.einsum("rxo,rxi->oi", d4, a4[:, kx:kx + W - 1]) for kx in range(2)], 1)  # (co, kx, ci)
     got = dw.double().cpu().view(cout, 2, cin)
     assert torch.isfinite(got).all()
     assert rel(got, ref) < 1e-3
+    dxref = torch.zeros(B * H, W, cin, dtype=torch.float64)
+    for kx in range(2):
+        dxref[:, kx:kx + W - 1] += torch.einsum("rxo,oi->rxi", d4, wb[:, :, kx])
+    assert rel(dx.double().cpu().view(B * H, W, cin), dxref) < 1e-2
