@@ -116,7 +116,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def pmc_traffic(model: str, ks: dict):
+# probe tag -> substring of its kernel symbol (disambiguates launches with similar durations)
+KERNEL_HINT = {
+    "t0b.fwd": "rowconv_kernelIDF16bLi256ELi32ELi1ELi32ELi8ELb1E",
+    "t0b.dgrad": "rowconv_kernelIDF16bLi256ELi32ELi1ELi32ELi8ELb0E",
+    "t0b.wgrad": "wgrad8_kernel",
+    "conv2.fwd": "feconv_kernel<32, 16, 2, true>",
+    "conv2.dgrad": "feconv_kernel<64, 8, 1, false>",
+    "conv2.wgrad": "fe_wgrad_kernel",
+    "conv1.fwd": "fe_conv1_kernel",
+    "attn.fwd": "attn_fwd_kernel",
+}
+
+
+def pmc_traffic(model: str, ks: dict, tag: str | None = None):
     """HBM bytes per launch of the probed kernel from the committed rocprofv3 PMC summary of the same
     bench command (profiles/<round>_pmc_<model>.json, written by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes).  The probed launch is matched to a kernel symbol by launches per
@@ -125,6 +138,9 @@ def pmc_traffic(model: str, ks: dict):
     if not files:
         return None, None
     table = json.loads(files[-1].read_text())["kernels"]
+    hint = KERNEL_HINT.get(tag or "")
+    if hint and any(hint in n for n in table):
+        table = {n: e for n, e in table.items() if hint in n}
     best = None
     for name, e in table.items():
         if "hbm_bytes" not in e or e["launches_per_step"] != round(ks["launches_per_step"]):
@@ -245,7 +261,7 @@ def main():
         ks = kstats[dom]
         kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel"}.get(
             dom, "igemm_kernel")
-        traffic, tsrc = pmc_traffic(args.model, ks)
+        traffic, tsrc = pmc_traffic(args.model, ks, dom)
         if tsrc and tsrc.get("kernel"):
             kname = tsrc["kernel"].replace("_ZN12_GLOBAL__N_1", "").replace("(anonymous namespace)::", "").split("(")[0]
         roof = {"bound": "mfma", "kernel": f"{kname} [{dom}]", "achieved": round(ks["tflops"], 2),
