@@ -393,6 +393,160 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
   }
 }
 
+// ---------------------------------------------------------------- trunk conv3 forward + BN stats
+//   y3[b][oy][ox][c] = bias[c] + sum_{ky,kx<8} w[c][ky][kx] * X0[b][oy+ky][ox+kx]   (envnet_v2.py:31,
+// the 1 -> 32 channel 8x8 conv on the pooled frontend image).  Wave-persistent like conv1: the 4
+// weight fragments (32 channels x 64 taps) are the MFMA A operand; per (clip, output row, 32-px)
+// item the wave stages the 8 input rows x 40 samples it needs into a per-wave LDS strip as four
+// copies shifted by 0..3 samples (row pitch 88 B, copy pitch 8 rows), so every 8-sample B fragment
+// (k-step ks: kernel rows 2ks, 2ks+1 on the lane halves, kx = 0..7) is two aligned ds_read_b64 and
+// the 32 lanes of a half hit 32 distinct bank pairs; BN3 statistics accumulate in the epilogue.
+struct F3Args {
+  const bf16* x;      // (n, h, w) 1-channel image
+  const bf16* w;      // (32, 64) taps ky*8 + kx
+  const float* bias;  // (32)
+  bf16* y;            // (n, h-7, w-7, 32)
+  float* part;        // [waves][32][2] or null
+  int n, h, wd, oh, ow, nseg;
+};
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
+  constexpr int ROWB = 88, CPYB = 8 * ROWB;
+  __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
+  const int items = g.n * g.oh * g.nseg;
+  char* sg = strip[wv];
+  bf16x8 wa[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) wa[ks] = *reinterpret_cast<const bf16x8*>(g.w + (lane & 31) * 64 + ks * 16 + 8 * (lane >> 5));
+  const int c0 = 8 * (lane >> 5);
+  float bv[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { bv[i] = g.bias[c0 + i]; bv[8 + i] = g.bias[c0 + 16 + i]; }
+  float s1[16], s2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  // staging lane l < 40: input row r = l / 5 of the item, samples 8q .. 8q+11 (q = l % 5) as three
+  // 8-byte loads (row pitch 2*wd bytes is 8-byte aligned for wd % 4 == 0); past the row end -> 0
+  struct Raw { u32x2 v[3]; };
+  auto load = [&](int it) __attribute__((always_inline)) {
+    Raw R;
+    it = it < items ? it : items - 1;
+    const int seg = it % g.nseg, rest = it / g.nseg;
+    const int oy = rest % g.oh, b = rest / g.oh;
+    const int l = lane < 40 ? lane : 0;
+    const int r = l / 5, q = l % 5;
+    const int col = seg * 32 + 8 * q;
+    const bf16* src = g.x + ((int64_t)b * g.h + oy + r) * g.wd;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int c = col + 4 * k;
+      R.v[k] = c + 4 <= g.wd ? *reinterpret_cast<const u32x2*>(src + c) : u32x2{0u, 0u};
+    }
+    return R;
+  };
+  auto run = [&](int it, const Raw& R) __attribute__((always_inline)) {
+    if (lane < 40) {
+      const int r = lane / 5, q = lane % 5;
+      const uint32_t d[6] = {R.v[0][0], R.v[0][1], R.v[1][0], R.v[1][1], R.v[2][0], R.v[2][1]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        // copy c dword i = samples (8q + c + 2i, +1)
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = c + 2 * i;  // first sample index within this lane's 12
+          o[i] = (e & 1) ? ((d[e >> 1] >> 16) | (d[(e >> 1) + 1] << 16)) : d[e >> 1];
+        }
+        *reinterpret_cast<u32x4*>(sg + c * CPYB + r * ROWB + 16 * q) = u32x4{o[0], o[1], o[2], o[3]};
+      }
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    const int o = lane & 31, cp = o & 3, dw = (o - cp) >> 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const char* src = sg + cp * CPYB + (2 * ks + (lane >> 5)) * ROWB + dw * 4;
+      const u32x2 p0 = *reinterpret_cast<const u32x2*>(src);
+      const u32x2 p1 = *reinterpret_cast<const u32x2*>(src + 8);
+      const u32x4 f = {p0[0], p0[1], p1[0], p1[1]};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ks], __builtin_bit_cast(bf16x8, f), acc, 0, 0, 0);
+    }
+    float v[16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a0 = acc[8 * h + j], a1 = acc[8 * h + 4 + j];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a1), false, false);
+        v[8 * h + j] = __builtin_bit_cast(float, (unsigned)sw[0]);
+        v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)sw[1]);
+      }
+    const int seg = it % g.nseg, rest = it / g.nseg;
+    const int oy = rest % g.oh, b = rest / g.oh;
+    const int ox = seg * 32 + o;
+    if (ox < g.ow) {
+      bf16* dst = g.y + (((int64_t)b * g.oh + oy) * g.ow + ox) * 32 + c0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 8 * h + 2 * i;
+          const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
+          w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+          if constexpr (STATS) {
+            const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
+            s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
+            s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
+          }
+        }
+        *reinterpret_cast<u32x4*>(dst + 16 * h) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+      }
+    }
+  };
+
+  int it = gw;
+  if (it < items) {
+    Raw ra = load(it), rb;
+    for (;;) {
+      rb = load(it + nw);
+      run(it, ra);
+      it += nw;
+      if (it >= items) break;
+      ra = load(it + nw);
+      run(it, rb);
+      it += nw;
+      if (it >= items) break;
+    }
+  }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int m = 1; m < 32; m <<= 1) {
+        s1[i] += __shfl_xor(s1[i], m, 64);
+        s2[i] += __shfl_xor(s2[i], m, 64);
+      }
+    }
+    if ((lane & 31) == 0) {
+      float* dst = g.part + (int64_t)gw * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dst[(c0 + i) * 2] = s1[i];
+        dst[(c0 + i) * 2 + 1] = s2[i];
+        dst[(c0 + 16 + i) * 2] = s1[8 + i];
+        dst[(c0 + 16 + i) * 2 + 1] = s2[8 + i];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- conv2 weight gradient
 //   dW[co][kx*32 + ci] = sum_{b,o} dy2[b][o][co] * relu(bn1(y1))[b][2o+kx][ci]      (64 x 512, K = pixels)
 // Persistent, gradient-stationary: one 8-wave workgroup per CU walks (clip, 128-pixel) items and
@@ -718,5 +872,21 @@ extern "C" int mia_fe_conv1_fwd(const float* x, const void* w, const float* bias
   if (partial) fe_conv1_kernel<true><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
   else fe_conv1_kernel<false><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
   MIA_LAUNCH_CHECK("fe_conv1_fwd");
+  return 0;
+}
+
+extern "C" int mia_fe_conv3_fwd(const void* x, const void* w, const float* bias, void* y, float* partial,
+                                int32_t nwaves, int32_t n, int32_t h, int32_t wd, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && w && bias && y && n > 0 && h >= 8 && wd >= 8, "fe_conv3_fwd: bad arguments");
+  MIA_CHECK_ARG(nwaves > 0 && nwaves % 4 == 0, "fe_conv3_fwd: nwaves must be a positive multiple of 4");
+  MIA_CHECK_ARG(wd % 4 == 0, "fe_conv3_fwd: image width must be a multiple of 4 (8-byte row alignment)");
+  MIA_CHECK_ARG(aligned16(w) && aligned16(y) && (reinterpret_cast<uintptr_t>(x) & 7) == 0,
+                "fe_conv3_fwd: w/y must be 16-byte and x 8-byte aligned");
+  F3Args a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(w), bias, reinterpret_cast<bf16*>(y),
+           partial, n, h, wd, h - 7, wd - 7, (int)cdiv(wd - 7, 32)};
+  MIA_CHECK_ARG((int64_t)n * a.oh * a.nseg < (1ll << 31), "fe_conv3_fwd: too many items");
+  if (partial) fe_conv3_kernel<true><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
+  else fe_conv3_kernel<false><<<nwaves / 4, 256, 0, as_stream(stream)>>>(a);
+  MIA_LAUNCH_CHECK("fe_conv3_fwd");
   return 0;
 }

@@ -306,6 +306,21 @@ def fe_conv1_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, y1: torch
     return (part, nw) if stats else None
 
 
+def fe_conv3_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, y: torch.Tensor, n: int, h: int, wd: int,
+                 stats: bool, tag: str | None = None):
+    """EnvNet trunk conv3 (1 -> 32, 8x8) forward, bf16: x (n, h, wd), w (32, 64) -> y (n*(h-7)*(wd-7), 32).
+    stats=True also returns (partial, nblk) of the BN shifted sums about bias."""
+    oh, ow = h - 7, wd - 7
+    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and y.dtype == torch.bfloat16
+    assert x.numel() == n * h * wd and w.numel() == 32 * 64 and y.numel() == n * oh * ow * 32
+    nw = 4096
+    part = torch.empty(nw, 32, 2, dtype=torch.float32, device=x.device) if stats else None
+    with probe(tag or "", 2.0 * n * oh * ow * 32 * 64, x.numel() * 2 + y.numel() * 2):
+        L.check(L.load().mia_fe_conv3_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(), L.ptr(part),
+                                          nw, n, h, wd, _s()), "mia_fe_conv3_fwd")
+    return (part, nw) if stats else None
+
+
 def bn_finalize_shifted(partial: torch.Tensor, nblk: int, P: int, C: int, kshift: torch.Tensor, gamma, beta,
                         running_mean, running_var, momentum: float, eps: float) -> BNState:
     """Training-mode BN statistics from shifted partial sums (mia_bn_finalize_shifted)."""

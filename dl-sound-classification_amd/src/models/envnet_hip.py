@@ -165,9 +165,13 @@ class EnvNetFunction(torch.autograd.Function):
             wa_ = K.pack_weight(p[pa], cd, 0)
             ya = torch.empty(B * ha * wa, cout, dtype=tdt, device=dev)
             dense_w2 = cd == L.BF16 and kh == 1 and kw == 2 and cin > 1  # blocks 3-4: (1, 2) convs
+            conv3_st = None
             if dense_w2:
                 # (1, 2) conv as one dense GEMM over every input pixel (the input map carries a pad pixel)
                 K.conv_w2_fwd(inp.reshape(B * H * W, cin), B * H, W, cin, wa_, p[pa + 1], ya, tag=f"t{blk}a.fwd")
+            elif cd == L.BF16 and cin == 1 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0:
+                # conv3: wave-persistent, BN statistics accumulated in its epilogue
+                conv3_st = K.fe_conv3_fwd(inp, wa_, p[pa + 1], ya, B, H, W, stats=training, tag=f"t{blk}a.fwd")
             else:
                 if cin == 1:
                     A = K.conv(inp, L.KC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)
@@ -175,7 +179,13 @@ class EnvNetFunction(torch.autograd.Function):
                     A = K.conv(inp, L.KC, B, H, W, cin, ha, wa, kh, kw)
                 K.gemm(A, K.dense(wa_, L.KC, cout, kh * kw * cin), K.epilogue(ya, cout, bias=p[pa + 1]),
                        B * ha * wa, cout, kh * kw * cin, cd, tag=f"t{blk}a.fwd")
-            bna = bn(2 + 2 * blk, ya, B * ha * wa, cout)
+            if conv3_st is not None:
+                mb = bns[2 + 2 * blk]
+                bna = K.bn_finalize_shifted(conv3_st[0], conv3_st[1], B * ha * wa, cout, p[pa + 1], mb.weight, mb.bias,
+                                            mb.running_mean, mb.running_var,
+                                            mb.momentum if mb.momentum is not None else 0.1, mb.eps)
+            else:
+                bna = bn(2 + 2 * blk, ya, B * ha * wa, cout)
             _, _, cin2, cout2, kh2, kw2 = TRUNK[2 * blk + 1]
             wb_ = K.pack_weight(p[pa + 4], cd, 0)
             yb = torch.empty(B * hb * wb, cout2, dtype=tdt, device=dev)

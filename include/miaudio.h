@@ -204,6 +204,15 @@ int mia_conv1ch_dgrad(const void* dy, const float* w, void* dx, int32_t n, int32
 int mia_fe_conv1_fwd(const float* x, const void* w, const float* bias, void* y1, float* partial, int32_t nwaves,
                      int32_t n, int32_t t, mia_stream_t stream);
 
+/* EnvNet-v2 trunk conv3 forward (reference src/models/envnet_v2.py:31 Conv2d(1, 32, (8, 8)) on the
+ * pooled frontend image; replaces that cuDNN conv2d) with the BatchNorm batch statistics of its
+ * bf16 output accumulated in the epilogue (as mia_fe_conv1_fwd):
+ *   y[b][oy][ox][c] = bias[c] + sum_{ky,kx<8} w[c][ky*8+kx] * x[b][oy+ky][ox+kx]
+ * x bf16 (n, h, wd) (wd % 4 == 0, 8-byte aligned), w bf16 (32, 64), y bf16 (n, h-7, wd-7, 32);
+ * partial (or NULL): f32 [nwaves][32][2] shifted sums about bias for mia_bn_finalize_shifted. */
+int mia_fe_conv3_fwd(const void* x, const void* w, const float* bias, void* y, float* partial, int32_t nwaves,
+                     int32_t n, int32_t h, int32_t wd, mia_stream_t stream);
+
 /* BatchNorm finalize from per-block shifted sums partial[nblk][C][2] about kshift[c]: writes mean,
  * invstd, the fused scale/shift (gamma*invstd, beta - mean*gamma*invstd) and updates the running
  * statistics (momentum, unbiased variance) exactly as mia_bn_fwd_stats.  Training mode only. */

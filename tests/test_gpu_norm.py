@@ -230,3 +230,31 @@ def test_pool_bn_bwd_apply_octets_bf16(cuda, geom):
     assert rel(dx.double().cpu(), ref) < 1e-2
     assert rel(dg.double().cpu(), (dz * xhat).sum((0, 1, 2))) < 1e-4
     assert rel(db.double().cpu(), dz.sum((0, 1, 2))) < 1e-4
+
+
+@pytest.mark.parametrize("n,h,wd", [(3, 64, 860), (5, 12, 100)])
+def test_fe_conv3_fwd_with_bn_stats(cuda, n, h, wd):
+    """Wave-persistent trunk conv3 (1 -> 32, 8x8) vs float64 conv2d of the same bf16 operands, and
+    its fused BN statistics == mia_bn_fwd_stats over its own output (running statistics included)."""
+    g = torch.Generator(device=cuda).manual_seed(h * wd + n)
+    x = (torch.randn(n, h, wd, generator=g, device=cuda) * 0.5).to(torch.bfloat16)
+    W = torch.randn(32, 1, 8, 8, generator=g, device=cuda) * 0.1
+    bias = torch.randn(32, generator=g, device=cuda) * 0.5
+    wp = K.pack_weight(W, L.BF16, 0)
+    oh, ow = h - 7, wd - 7
+    y = torch.full((n * oh * ow, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    part, nblk = K.fe_conv3_fwd(x, wp, bias, y, n, h, wd, stats=True)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda)
+    rm1, rv1 = torch.zeros(32, device=cuda), torch.ones(32, device=cuda)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    st = K.bn_finalize_shifted(part, nblk, n * oh * ow, 32, bias, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    ref_st = K.bn_fwd_stats(y, n * oh * ow, 32, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double()[:, None], W.to(torch.bfloat16).double(), bias.double())
+    got = y.double().view(n, oh, ow, 32).permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max() / ref.abs().max() < 1e-2
+    for a, b in ((st.mean, ref_st.mean), (st.invstd, ref_st.invstd), (st.scale, ref_st.scale),
+                 (st.shift, ref_st.shift), (rm1, rm2), (rv1, rv2)):
+        assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
