@@ -77,14 +77,16 @@ class ESC50Dataset(Dataset):
 
 
 class ESC50DataModule:
+    NUM_FOLDS = 5
+
     def __init__(self, root: str, fold: int = 0, sample_rate: int = SR, n_mels: int = 128, val_split: float = 0.1,
                  batch_size: int = 32, num_workers: int = 4, is_spectrogram: bool = False,
                  enable_bc_mixing: bool = False, enable_mixup: bool = False, mixup_alpha: float = 0.5,
                  time_mask: Union[bool, int] = False, freq_mask: Union[bool, int] = False,
                  preprocessing_mode: str = "envnet_v2", preprocessing_config: Dict | None = None,
                  num_classes: int = 50, augment: Dict | None = None, **unused):
-        if not (0 <= fold <= 4):
-            raise ValueError("fold must be 0…4 (ESC-50 uses five folds).")
+        if not (0 <= fold < self.NUM_FOLDS):
+            raise ValueError(self._fold_error())
         self._validate_config_constraints(is_spectrogram, enable_bc_mixing, enable_mixup, time_mask, freq_mask)
         augment = dict(augment or {})
         if time_mask is not False:
@@ -104,6 +106,10 @@ class ESC50DataModule:
         self._pool = self._pool_labels = None
         self._logmel = None
         self._gen = None
+
+    @classmethod
+    def _fold_error(cls) -> str:
+        return "fold must be 0…4 (ESC-50 uses five folds)."
 
     @staticmethod
     def _validate_config_constraints(is_spectrogram, enable_bc_mixing, enable_mixup, time_mask, freq_mask):
@@ -141,7 +147,7 @@ class ESC50DataModule:
         if self._train_set is not None:
             return
         from sklearn.model_selection import StratifiedShuffleSplit
-        train_folds = [f for f in range(5) if f != self.fold]
+        train_folds = [f for f in range(self.NUM_FOLDS) if f != self.fold]
         full = self._ds(folds=train_folds, training=True)
         labels = [full.load(i)[1] for i in range(len(full))]
         val_size = math.ceil(len(full) * self.val_split)

@@ -82,6 +82,30 @@ def test_esc50_datamodule_files(tmp_path):
     assert yv.shape == (4, 4) and torch.equal(yv.argmax(1), y)
 
 
+def test_urbansound8k_datamodule_files(tmp_path):
+    """UrbanSound8K: ten folds, 10 classes, clips shorter than the 5 s EnvNet window are zero-padded
+    into it (pad T/2 each side, crop); fold 10 is out of range; config composes to the class."""
+    from src.datasets.urbansound8k import UrbanSound8KDataModule
+    with pytest.raises(ValueError, match="ten folds"):
+        UrbanSound8KDataModule(root="x", fold=10)
+    for f in range(10):
+        d = tmp_path / f"fold_{f}"
+        d.mkdir()
+        for i in range(12):
+            torch.save({"waveform": torch.randn(1, 3000), "label": (f + i) % 10}, d / f"{i}.pt")
+    dm = UrbanSound8KDataModule(root=str(tmp_path), fold=9, batch_size=5, num_workers=0,
+                                preprocessing_config={"window_length": 0.1})  # 4410-sample window > 3000
+    dm.setup("fit")
+    assert dm.num_classes == 10
+    assert len(dm._train_set) + len(dm._val_set) == 108 and len(dm._test_set) == 12
+    x, y = next(iter(dm.test_dataloader()))
+    assert x.shape == (5, 1, 4410)
+    _, yv = dm.gpu_transform(x, y, training=False)
+    assert yv.shape == (5, 10)
+    cfg = compose(CFG, "training", ["dataset=urbansound8k"])
+    assert cfg.dataset["_target_"] == "src.datasets.urbansound8k.UrbanSound8KDataModule"
+
+
 def test_train_script_toy(tmp_path, monkeypatch):
     import importlib.util
     spec = importlib.util.spec_from_file_location("train_script", PKG / "scripts" / "train.py")
