@@ -1,0 +1,300 @@
+// EnvNet-v2 trunk conv4 (Conv2d(32, 32, (8, 8)), reference src/models/envnet_v2.py:34) forward and
+// backward-data on bf16 MFMA, gfx950.
+//
+//   y[b][oy][ox][co] = sum_{ky, kx, ci} a[b][oy+ky-ph][ox+kx-pw][ci] * W[co][ky][kx][ci]
+//
+// forward: a = relu(bn(conv3 output)) applied while staging, ph = pw = 0, bias + BN statistics of
+// the stored bf16 output in the epilogue; backward-data: a = dY, ph = pw = 7, W = the flipped OHWI
+// weights of the transposed conv (mia_pack_weight layout 1).
+//
+// Row-rolling schedule, one wave per SIMD: a wave owns (clip, 64 output columns) items and walks the
+// padded input rows top to bottom.  Input row r feeds output rows r-7 .. r (kernel rows ky = 7 .. 0),
+// so the wave keeps EIGHT output rows in flight in its accumulators (8 rows x 2 pixel tiles x 16 =
+// 256 registers) and every input fragment it reads from LDS serves 8 MFMAs (one per ky); after row r
+// the output row r-7 is complete, is stored from the accumulators and its slot restarts at zero.
+// The accumulator slot of (row r, ky) is (r - ky) mod 8: the row loop is unrolled by 8 so the slot is
+// a compile-time register index.  All 64 weight fragments x 2 channel halves (128 KB) sit in LDS in
+// MFMA-fragment order (lane-contiguous 16-B pieces: conflict-free), read once per (row, ky, kx, c)
+// and used for both pixel tiles: 160 ds_read_b128 per 256 MFMAs, ~80 B/clk per CU at the MFMA peak.
+// Each wave stages its own 71-pixel strip (row pitch 80 B: conflict-free b128 reads), so the waves
+// never wait for each other; the next row's raw loads fly while the current row computes.
+#include "common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int C8_NT = 256;
+constexpr int C8_PX = 64;                    // output columns per item (2 MFMA tiles)
+constexpr int C8_SPX = C8_PX + 7;            // staged input columns
+constexpr int C8_PSB = 80;                   // LDS bytes per staged pixel (32 ch bf16 + 16 pad)
+constexpr int C8_STRIP = C8_SPX * C8_PSB;    // 5 680 B per wave
+constexpr int C8_WB = 128 * 1024;            // weight fragments
+constexpr int C8_LDC = (C8_SPX * 4 + 63) / 64;  // 16-B chunks per lane per staged row (5)
+
+struct C8Args {
+  const bf16* x;      // (n, h, wd, 32)
+  const float* ps;    // pre-op scale / shift (32) or null
+  const float* pt;
+  const bf16* w;      // (32 co, 8 ky, 8 kx, 32 ci)
+  const float* bias;  // (32) or null
+  bf16* y;            // (n, oh, ow, 32)
+  float* part;        // [waves][32][2] BN shifted sums about bias, or null
+  int n, h, wd, ph, pw, oh, ow, nchunk;
+  int nfull0, nsplit;  // items < nfull0 cover all output rows; the rest are row parts (nsplit per chunk)
+};
+
+__device__ __forceinline__ u32x4 cook(u32x4 u, bool ok, const float* sc, const float* sh) {
+  if (!ok) return u32x4{0u, 0u, 0u, 0u};
+  if (sc == nullptr) return u;
+  uint32_t w4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = fmaxf(fmaf(__uint_as_float(u[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(u[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
+    const bf16 bl = (bf16)lo, bh = (bf16)hi;
+    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+  }
+  return u32x4{w4[0], w4[1], w4[2], w4[3]};
+}
+
+template <bool PRE, bool STATS>
+__global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv8_kernel(C8Args g) {
+  __shared__ __attribute__((aligned(16))) char smem[C8_WB + 4 * C8_STRIP];
+  __shared__ __attribute__((aligned(16))) float prm[96];  // pre-op scale, shift, bias (kept out of VGPRs)
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t < 32) {
+    prm[t] = g.ps ? g.ps[t] : 1.f;
+    prm[32 + t] = g.pt ? g.pt[t] : 0.f;
+    prm[64 + t] = g.bias ? g.bias[t] : 0.f;
+  }
+
+  // weights -> fragment order: fragment f = (ky*8 + kx)*2 + c, piece [lane] = W[lane&31][ky][kx][16c + 8(lane>>5) .. +8]
+  for (int q = t; q < C8_WB / 16; q += C8_NT) {
+    const int f = q >> 6, l = q & 63;
+    const int kk = (f >> 1) * 32 + (f & 1) * 16 + 8 * (l >> 5);
+    *reinterpret_cast<u32x4*>(smem + q * 16) = *reinterpret_cast<const u32x4*>(g.w + (l & 31) * 2048 + kk);
+  }
+
+  const int cg = lane & 3;  // channel group of every staged 16-B chunk this lane handles
+  const int c0 = 8 * (lane >> 5);
+  float s1[16], s2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+  __syncthreads();
+
+  const int gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
+  const int items = g.nfull0 + (g.n * g.nchunk - g.nfull0) * g.nsplit;
+  char* strip = smem + C8_WB + wv * C8_STRIP;
+  const u32x4* xs = reinterpret_cast<const u32x4*>(g.x);
+
+  f32x16 acc[8][2];
+  u32x4 raw[C8_LDC];
+  uint32_t rok = 0;
+
+  for (int item = gw; item < items; item += nw) {
+    int base = item, oy_lo = 0, oy_hi = g.oh;
+    if (item >= g.nfull0) {  // last round: chunks split into row parts so every wave gets one
+      const int j = item - g.nfull0, part = j % g.nsplit;
+      base = g.nfull0 + j / g.nsplit;
+      oy_lo = part * g.oh / g.nsplit;
+      oy_hi = (part + 1) * g.oh / g.nsplit;
+    }
+    const int b = base / g.nchunk;
+    const int x0 = (base - b * g.nchunk) * C8_PX;
+    const int ix0 = x0 - g.pw;
+    const int r_lo = oy_lo, r_hi = oy_hi + 7;  // padded input rows of this item
+
+    auto load_row = [&](int r) __attribute__((always_inline)) {
+      const int iy = r - g.ph;
+      const bool rowok = iy >= 0 && iy < g.h;
+      rok = 0;
+#pragma unroll
+      for (int s = 0; s < C8_LDC; ++s) {
+        const int p = (lane + 64 * s) >> 2;
+        const int ix = ix0 + p;
+        const bool ok = rowok && p < C8_SPX && ix >= 0 && ix < g.wd;
+        const int64_t off = ok ? (((int64_t)b * g.h + iy) * g.wd + ix) * 4 + cg : 0;
+        raw[s] = xs[off];
+        rok |= (uint32_t)ok << s;
+      }
+    };
+    auto store_row = [&]() __attribute__((always_inline)) {
+      float sc[8], sh[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sc[i] = prm[cg * 8 + i]; sh[i] = prm[32 + cg * 8 + i]; }
+#pragma unroll
+      for (int s = 0; s < C8_LDC; ++s) {
+        const int p = (lane + 64 * s) >> 2;
+        if (p < C8_SPX)
+          *reinterpret_cast<u32x4*>(strip + p * C8_PSB + cg * 16) =
+              cook(raw[s], (rok >> s) & 1u, PRE ? sc : nullptr, sh);
+      }
+    };
+    // output row oy from accumulator slot S: bias, bf16 store, BN statistics
+    auto emit = [&](const f32x16 (&a)[2], int oy) __attribute__((always_inline)) {
+      float bv[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { bv[i] = prm[64 + c0 + i]; bv[8 + i] = prm[64 + c0 + 16 + i]; }
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        float v[16];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[tt][8 * h + j]),
+                                                             __float_as_uint(a[tt][8 * h + 4 + j]), false, false);
+            v[8 * h + j] = __builtin_bit_cast(float, (unsigned)sw[0]);
+            v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)sw[1]);
+          }
+        const int ox = x0 + 32 * tt + (lane & 31);
+        if (ox < g.ow) {
+          bf16* dst = g.y + (((int64_t)b * g.oh + oy) * g.ow + ox) * 32 + c0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int e = 8 * h + 2 * i;
+              const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
+              w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) |
+                      ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+              if constexpr (STATS) {
+                const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
+                s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
+                s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
+              }
+            }
+            *reinterpret_cast<u32x4*>(dst + 16 * h) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+          }
+        }
+      }
+    };
+
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[sl][tt][i] = 0.f;
+
+    // one padded input row r (r % 8 == P): stage it, start the next row's loads, 8 x 32 MFMAs,
+    // then retire output row r - 7 (slot (P + 1) % 8)
+    auto step = [&](auto PC, int r) __attribute__((always_inline)) {
+      constexpr int P = decltype(PC)::value;
+      const int iy = r - g.ph;
+      const bool live = iy >= 0 && iy < g.h;  // wave-uniform: padding rows contribute nothing
+      if (live) store_row();
+      if (r + 1 < r_hi) load_row(r + 1);
+      if (live) {
+        // (kx, c) blocks of 16 MFMAs; the 10 fragments of block j+1 are read while block j computes
+        // (interleaved one DS read per MFMA), so every LDS read has >= 6 MFMAs of cover
+        bf16x8 fw[2][8], fb[2][2];
+        auto fetch = [&](int j, int buf) __attribute__((always_inline)) {
+          const int kx = j >> 1, c = j & 1;
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt)
+            fb[buf][tt] = *reinterpret_cast<const bf16x8*>(strip + (32 * tt + (lane & 31) + kx) * C8_PSB + c * 32 +
+                                                           (lane >> 5) * 16);
+#pragma unroll
+          for (int ky = 0; ky < 8; ++ky)
+            fw[buf][ky] = *reinterpret_cast<const bf16x8*>(smem + ((ky * 8 + kx) * 2 + c) * 1024 + lane * 16);
+        };
+        fetch(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int cur = j & 1;
+          if (j + 1 < 16) fetch(j + 1, cur ^ 1);
+#pragma unroll
+          for (int ky = 0; ky < 8; ++ky)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+              acc[(P - ky + 8) & 7][tt] =
+                  __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[cur][ky], fb[cur][tt], acc[(P - ky + 8) & 7][tt], 0, 0, 0);
+          if (j + 1 < 16) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // keep block j+1's reads inside block j's MFMA stream
+        }
+      }
+      constexpr int S = (P + 1) & 7;
+      if (r - 7 >= oy_lo) emit(acc[S], r - 7);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[S][tt][i] = 0.f;
+    };
+
+    load_row(r_lo);
+    for (int r0 = r_lo & ~7; r0 < r_hi; r0 += 8) {
+#define C8_STEP(k) if (r0 + k >= r_lo && r0 + k < r_hi) step(std::integral_constant<int, k>{}, r0 + k);
+      C8_STEP(0) C8_STEP(1) C8_STEP(2) C8_STEP(3) C8_STEP(4) C8_STEP(5) C8_STEP(6) C8_STEP(7)
+#undef C8_STEP
+    }
+  }
+
+  if constexpr (STATS) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int m = 1; m < 32; m <<= 1) {
+        s1[i] += __shfl_xor(s1[i], m, 64);
+        s2[i] += __shfl_xor(s2[i], m, 64);
+      }
+    }
+    if ((lane & 31) == 0) {
+      float* dst = g.part + (int64_t)gw * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dst[(c0 + i) * 2] = s1[i];
+        dst[(c0 + i) * 2 + 1] = s2[i];
+        dst[(c0 + 16 + i) * 2] = s1[8 + i];
+        dst[(c0 + 16 + i) * 2 + 1] = s2[8 + i];
+      }
+    }
+  }
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mia_trunk_conv8(const void* x, const float* pre_scale, const float* pre_shift, const void* w,
+                               const float* bias, void* y, float* partial, int32_t nblocks, int32_t n, int32_t h,
+                               int32_t wd, int32_t ph, int32_t pw, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && w && y && n > 0 && h > 0 && wd > 0 && ph >= 0 && pw >= 0 && nblocks > 0,
+                "trunk_conv8: bad arguments");
+  MIA_CHECK_ARG((pre_scale == nullptr) == (pre_shift == nullptr), "trunk_conv8: pre_scale/pre_shift come together");
+  MIA_CHECK_ARG(partial == nullptr || bias != nullptr, "trunk_conv8: statistics are shifted about the bias");
+  MIA_CHECK_ARG(al16(x) && al16(w) && al16(y), "trunk_conv8: x/w/y must be 16-byte aligned");
+  const int oh = h + 2 * ph - 7, ow = wd + 2 * pw - 7;
+  MIA_CHECK_ARG(oh > 0 && ow > 0, "trunk_conv8: output is empty");
+  MIA_CHECK_ARG((int64_t)n * h * wd * 4 < (1ll << 40), "trunk_conv8: input too large");
+  C8Args a{reinterpret_cast<const bf16*>(x), pre_scale, pre_shift, reinterpret_cast<const bf16*>(w), bias,
+           reinterpret_cast<bf16*>(y), partial, n, h, wd, ph, pw, oh, ow, (int)cdiv(ow, C8_PX), 0, 1};
+  MIA_CHECK_ARG((int64_t)n * a.nchunk * 8 < (1ll << 31), "trunk_conv8: too many items");
+  // balance the last round: split the chunks left over after the full rounds into row parts
+  const int nw = 4 * nblocks, full = n * a.nchunk, rem = full % nw;
+  a.nfull0 = full - rem;
+  if (rem > 0) a.nsplit = (int)std::max(1, std::min(std::min(nw / rem, 4), oh / 8 > 0 ? oh / 8 : 1));
+  hipStream_t s = as_stream(stream);
+  if (pre_scale) {
+    if (partial) conv8_kernel<true, true><<<nblocks, C8_NT, 0, s>>>(a);
+    else conv8_kernel<true, false><<<nblocks, C8_NT, 0, s>>>(a);
+  } else {
+    if (partial) conv8_kernel<false, true><<<nblocks, C8_NT, 0, s>>>(a);
+    else conv8_kernel<false, false><<<nblocks, C8_NT, 0, s>>>(a);
+  }
+  MIA_LAUNCH_CHECK("trunk_conv8");
+  return 0;
+}

@@ -321,6 +321,24 @@ def fe_conv3_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, y: torch.
     return (part, nw) if stats else None
 
 
+def trunk_conv8(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, n: int, h: int, wd: int, ph: int = 0,
+                pw: int = 0, scale=None, shift=None, bias=None, stats: bool = False, tag: str | None = None):
+    """EnvNet trunk conv4 (32 -> 32, 8x8), bf16, row-rolling kernel: x (n*h*wd, 32) NHWC, w packed OHWI
+    (32, 2048) -> y (n*oh*ow, 32), oh = h+2ph-7, ow = wd+2pw-7.  scale/shift: BN+ReLU applied to x.
+    stats=True (needs bias) also returns (partial, nblk) of the BN shifted sums about bias."""
+    oh, ow = h + 2 * ph - 7, wd + 2 * pw - 7
+    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and y.dtype == torch.bfloat16
+    assert x.numel() == n * h * wd * 32 and w.numel() == 32 * 2048 and y.numel() == n * oh * ow * 32
+    assert x.is_contiguous() and w.is_contiguous() and y.is_contiguous()
+    assert (scale is None) == (shift is None) and (not stats or bias is not None)
+    nblk = 256
+    part = torch.empty(4 * nblk, 32, 2, dtype=torch.float32, device=x.device) if stats else None
+    with probe(tag or "", 2.0 * n * oh * ow * 32 * 2048, x.numel() * 2 + y.numel() * 2):
+        L.check(L.load().mia_trunk_conv8(x.data_ptr(), L.ptr(scale), L.ptr(shift), w.data_ptr(), L.ptr(bias),
+                                         y.data_ptr(), L.ptr(part), nblk, n, h, wd, ph, pw, _s()), "mia_trunk_conv8")
+    return (part, 4 * nblk) if stats else None
+
+
 def bn_finalize_shifted(partial: torch.Tensor, nblk: int, P: int, C: int, kshift: torch.Tensor, gamma, beta,
                         running_mean, running_var, momentum: float, eps: float) -> BNState:
     """Training-mode BN statistics from shifted partial sums (mia_bn_finalize_shifted)."""

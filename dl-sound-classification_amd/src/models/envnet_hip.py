@@ -14,6 +14,7 @@ Reference op sequence: src/models/envnet_v2.py:14-85.
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
@@ -21,6 +22,13 @@ from ..miaudio import kernels as K
 from ..miaudio import lib as L
 
 _SEED = itertools.count(0x5EED)
+
+
+def _use_conv8(cd: int, cin: int, cout: int, kh: int, kw: int) -> bool:
+    """conv4 (32 -> 32, 8x8) forward / backward-data on the row-rolling kernel (csrc/conv8.hip);
+    MIA_CONV8=0 selects the row-window implicit GEMM instead (both HIP)."""
+    return (cd == L.BF16 and cin == 32 and cout == 32 and kh == 8 and kw == 8
+            and os.environ.get("MIA_CONV8", "1") != "0")
 
 # (conv module path, bn module path, cin, cout, kh, kw)
 TRUNK = [
@@ -190,7 +198,13 @@ class EnvNetFunction(torch.autograd.Function):
             wb_ = K.pack_weight(p[pa + 4], cd, 0)
             yb = torch.empty(B * hb * wb, cout2, dtype=tdt, device=dev)
             act = None
-            if dense_w2:
+            conv8_st = None
+            conv8 = _use_conv8(cd, cin2, cout2, kh2, kw2)
+            if conv8:
+                # conv4 (32 -> 32, 8x8): row-rolling MFMA kernel, BN+ReLU on staging, BN stats in its epilogue
+                conv8_st = K.trunk_conv8(ya, wb_, yb, B, ha, wa, scale=bna.scale, shift=bna.shift, bias=p[pa + 5],
+                                         stats=training, tag=f"t{blk}b.fwd")
+            elif dense_w2:
                 # relu(bn_a(ya)) materialised once (bf16, + pad pixel): the forward GEMM's A operand and
                 # the backward weight-gradient operand
                 act = torch.empty(B * ha * wa + 1, cin2, dtype=tdt, device=dev)[: B * ha * wa]
@@ -201,7 +215,13 @@ class EnvNetFunction(torch.autograd.Function):
                            shift=bna.shift)
                 K.gemm(A, K.dense(wb_, L.KC, cout2, kh2 * kw2 * cin2), K.epilogue(yb, cout2, bias=p[pa + 5]),
                        B * hb * wb, cout2, kh2 * kw2 * cin2, cd, tag=f"t{blk}b.fwd")
-            bnb = bn(3 + 2 * blk, yb, B * hb * wb, cout2)
+            if conv8_st is not None:
+                mb = bns[3 + 2 * blk]
+                bnb = K.bn_finalize_shifted(conv8_st[0], conv8_st[1], B * hb * wb, cout2, p[pa + 5], mb.weight, mb.bias,
+                                            mb.running_mean, mb.running_var,
+                                            mb.momentum if mb.momentum is not None else 0.1, mb.eps)
+            else:
+                bnb = bn(3 + 2 * blk, yb, B * hb * wb, cout2)
             ph, pw = TRUNK_POOL[blk]
             last = blk == 3
             # (non-last pools carry one pad pixel: the next block's dense (1, 2)-conv view reads it)
@@ -329,8 +349,12 @@ class EnvNetFunction(torch.autograd.Function):
                 # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
                 wbf = K.pack_weight(p[pa + 4], cd, 1)
                 Kdb = kh2 * kw2 * cout2
-                K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
-                       K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd, tag=f"t{blk}b.dgrad")
+                if _use_conv8(cd, cin2, cout2, kh2, kw2):
+                    K.trunk_conv8(dyb, wbf, da, B, hb, wb, ph=kh2 - 1, pw=kw2 - 1, tag=f"t{blk}b.dgrad")
+                else:
+                    K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
+                           K.dense(wbf, L.KC, cin2, Kdb), K.epilogue(da, cin2), Pa, cin2, Kdb, cd,
+                           tag=f"t{blk}b.dgrad")
             gwb = torch.empty_like(p[pa + 4])
             K.unpack_ohwi_grad(dWb, p[pa + 4].shape, gwb)
             grads[pa + 4] = gwb

@@ -213,6 +213,17 @@ int mia_fe_conv1_fwd(const float* x, const void* w, const float* bias, void* y1,
 int mia_fe_conv3_fwd(const void* x, const void* w, const float* bias, void* y, float* partial, int32_t nwaves,
                      int32_t n, int32_t h, int32_t wd, mia_stream_t stream);
 
+/* EnvNet-v2 trunk conv4 (Conv2d(32, 32, (8, 8)), replaces the cuDNN conv of src/models/envnet_v2.py:34
+ * and its backward-data): y[b][oy][ox][co] = bias[co] + sum a[b][oy+ky-ph][ox+kx-pw][ci] W[co][ky][kx][ci],
+ * a = relu(x*pre_scale + pre_shift) when pre_scale is given (forward, BN+ReLU of the previous conv), else x
+ * (backward-data: x = dY, ph = pw = 7, w = the flipped weights of mia_pack_weight layout 1).  x bf16
+ * (n, h, wd, 32), w bf16 (32, 8, 8, 32) OHWI, y bf16 (n, h+2ph-7, wd+2pw-7, 32), all 16-byte aligned;
+ * bias (or NULL) f32 (32); partial (or NULL, needs bias): f32 [4*nblocks][32][2] shifted sums about bias of
+ * the stored outputs, for mia_bn_finalize_shifted.  Row-rolling MFMA kernel, one workgroup per CU. */
+int mia_trunk_conv8(const void* x, const float* pre_scale, const float* pre_shift, const void* w, const float* bias,
+                    void* y, float* partial, int32_t nblocks, int32_t n, int32_t h, int32_t wd, int32_t ph, int32_t pw,
+                    mia_stream_t stream);
+
 /* BatchNorm finalize from per-block shifted sums partial[nblk][C][2] about kshift[c]: writes mean,
  * invstd, the fused scale/shift (gamma*invstd, beta - mean*gamma*invstd) and updates the running
  * statistics (momentum, unbiased variance) exactly as mia_bn_fwd_stats.  Training mode only. */

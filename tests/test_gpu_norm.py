@@ -258,3 +258,51 @@ def test_fe_conv3_fwd_with_bn_stats(cuda, n, h, wd):
     for a, b in ((st.mean, ref_st.mean), (st.invstd, ref_st.invstd), (st.scale, ref_st.scale),
                  (st.shift, ref_st.shift), (rm1, rm2), (rv1, rv2)):
         assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("n,h,wd", [(2, 57, 853), (3, 10, 40), (2, 9, 12)])
+def test_trunk_conv8_fwd_with_bn_stats(cuda, n, h, wd):
+    """Row-rolling conv4 kernel (32 -> 32, 8x8, BN+ReLU applied on staging) vs float64 conv2d of the
+    same bf16 operands, and its fused BN statistics == mia_bn_fwd_stats over its own output."""
+    g = torch.Generator(device=cuda).manual_seed(h * wd + n)
+    x = (torch.randn(n, h, wd, 32, generator=g, device=cuda) * 0.7 + 0.1).to(torch.bfloat16)
+    scale = torch.rand(32, generator=g, device=cuda) + 0.5
+    shift = torch.randn(32, generator=g, device=cuda) * 0.3
+    W = torch.randn(32, 32, 8, 8, generator=g, device=cuda) * 0.03
+    bias = torch.randn(32, generator=g, device=cuda) * 0.5
+    wp = K.pack_weight(W, L.BF16, 0)
+    oh, ow = h - 7, wd - 7
+    y = torch.full((n * oh * ow, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    part, nblk = K.trunk_conv8(x, wp, y, n, h, wd, scale=scale, shift=shift, bias=bias, stats=True)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda)
+    rm1, rv1 = torch.zeros(32, device=cuda), torch.ones(32, device=cuda)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    st = K.bn_finalize_shifted(part, nblk, n * oh * ow, 32, bias, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    ref_st = K.bn_fwd_stats(y, n * oh * ow, 32, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
+    torch.cuda.synchronize()
+    a = torch.relu(x.float() * scale + shift).to(torch.bfloat16).double().permute(0, 3, 1, 2)
+    ref = F.conv2d(a, W.to(torch.bfloat16).double(), bias.double())
+    got = y.double().view(n, oh, ow, 32).permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    assert rel(got, ref) < 1e-2
+    for u, v in ((st.mean, ref_st.mean), (st.invstd, ref_st.invstd), (st.scale, ref_st.scale),
+                 (st.shift, ref_st.shift), (rm1, rm2), (rv1, rv2)):
+        assert torch.allclose(u, v, rtol=2e-5, atol=2e-6), (u - v).abs().max()
+
+
+@pytest.mark.parametrize("n,h,wd", [(2, 50, 846), (3, 3, 30), (1, 1, 1)])
+def test_trunk_conv8_dgrad(cuda, n, h, wd):
+    """conv4 backward-data on the row-rolling kernel (dY zero-padded by 7, flipped weights) vs float64
+    conv_transpose2d; covers dY maps shorter than the kernel."""
+    g = torch.Generator(device=cuda).manual_seed(h + wd + n)
+    dy = torch.randn(n, h, wd, 32, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(32, 32, 8, 8, generator=g, device=cuda) * 0.03
+    wf = K.pack_weight(W, L.BF16, 1)
+    dx = torch.full((n * (h + 7) * (wd + 7), 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.trunk_conv8(dy, wf, dx, n, h, wd, ph=7, pw=7)
+    torch.cuda.synchronize()
+    ref = F.conv_transpose2d(dy.double().permute(0, 3, 1, 2), W.to(torch.bfloat16).double())
+    got = dx.double().view(n, h + 7, wd + 7, 32).permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    assert rel(got, ref) < 1e-2
