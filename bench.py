@@ -259,8 +259,9 @@ def main():
     roof = None
     if dom:
         ks = kstats[dom]
-        kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel"}.get(
-            dom, "igemm_kernel")
+        kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel",
+                 "t0b.fwd": "conv8_kernel<PRE,STATS>", "t0b.dgrad": "conv8_kernel"}.get(
+            dom, KERNEL_HINT.get(dom, "igemm_kernel"))
         traffic, tsrc = pmc_traffic(args.model, ks, dom)
         if tsrc and tsrc.get("kernel"):
             kname = tsrc["kernel"].replace("_ZN12_GLOBAL__N_1", "").replace("(anonymous namespace)::", "").split("(")[0]

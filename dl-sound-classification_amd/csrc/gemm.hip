@@ -1544,6 +1544,36 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
     __builtin_amdgcn_s_barrier();
   }
 
+  // plain f32 output of a full tile (the wide weight-gradient GEMMs, e.g. EnvNet FC1: 1.38 GB of f32
+  // per step): the whole 128x128 tile is staged in the (now idle) 64 KB of LDS and written as whole
+  // 512-B rows, two rows per wave store instruction, non-temporal (read next by the optimizer pass)
+  const bool plain = g.split == 1 && g.e.dtype == MIA_F32 && g.e.act == MIA_ACT_NONE && !g.e.bias &&
+                     !g.e.accumulate && !g.e.rm_inner && g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N &&
+                     (g.e.ldc & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0;
+  if (plain) {
+    float* tile = reinterpret_cast<float*>(smem);  // [128][128], 32-dword halves swapped on row bit 2
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int col = wn * 64 + j * 32 + (lane & 31);
+          tile[row * 128 + (col ^ (((row >> 2) & 1) << 5))] = acc[i][j][r];
+        }
+    __syncthreads();
+    float* out = reinterpret_cast<float*>(g.e.ptr);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = wave * 32 + it * 2 + (lane >> 5);
+      const int col = (lane & 31) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col));
+    }
+    return;
+  }
+
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
