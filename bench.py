@@ -118,8 +118,8 @@ def cpu_model() -> str:
 
 # probe tag -> substring of its kernel symbol (disambiguates launches with similar durations)
 KERNEL_HINT = {
-    "t0b.fwd": "conv8_kernelILb1ELb1E",
-    "t0b.dgrad": "conv8_kernelILb0ELb0E",
+    "t0b.fwd": "conv8_kernel<true, true, 2>",
+    "t0b.dgrad": "conv8_kernel<false, false, 2>",
     "t0b.wgrad": "wgrad8_kernel",
     "conv2.fwd": "feconv_kernel<32, 16, 2, true>",
     "conv2.dgrad": "feconv_kernel<64, 8, 1, false>",

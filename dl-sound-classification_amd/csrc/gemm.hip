@@ -18,6 +18,8 @@
 //  * split-K writes f32 partial slabs; a reduce kernel applies the epilogue.
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace mgemm;
@@ -1569,7 +1571,9 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       const int row = wave * 32 + it * 2 + (lane >> 5);
       const int col = (lane & 31) * 4;
       const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
-      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col));
+      f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
+      if (g.nt) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
     }
     return;
   }
@@ -1809,6 +1813,8 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     d.nfast = (d.split == 1 && d.nbn <= 32 && d.nbm >= 4 * d.nbn) ? 1 : 0;
     d.ws = reinterpret_cast<float*>(workspace);
     d.e = to_dev(*E);
+    static const int nt_env = [] { const char* v = getenv("MIA_EPI_NT"); return v ? atoi(v) : 1; }();
+    d.nt = nt_env;
     hipStream_t s = as_stream(stream);
     hipError_t err;
     const int la = A->layout, lb = B->layout;

@@ -24,6 +24,7 @@ struct DArgs {
               // block, so A streams from HBM once instead of once per column tile)
   float* ws;
   EpiDev e;
+  int nt;  // full-tile f32 epilogue with non-temporal stores
 };
 
 // -------------------------------------------------------------------------- epilogue
