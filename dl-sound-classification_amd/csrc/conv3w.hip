@@ -1,0 +1,182 @@
+// Weight gradient of the EnvNet-v2 trunk conv3 (Conv2d(1, 32, (8, 8)), reference
+// src/models/envnet_v2.py:31), bf16 MFMA, gfx950:
+//
+//   dW[co][ky*8 + kx] = sum_{b, oy, ox} dY[b][oy][ox][co] * x[b][oy+ky][ox+kx]
+//
+// Wave-persistent, no barriers (the mirror of fe_conv3_kernel): a wave owns (clip, output row,
+// 32 output columns) items.  Per item it stages the 8 input rows x 40 samples it needs into a
+// per-wave LDS strip as four copies shifted by 0..3 samples (so the 8 consecutive samples of any
+// tap are two aligned ds_read_b64) and the [32 px][32 co] dY tile (64-B rows, read transposed with
+// ds_read_b64_tr_b16 as the A operand dY^T).  K = the 32 pixels (2 k-steps), N = the 64 taps
+// (2 tiles): 4 MFMAs per item into 32 accumulator registers kept across all items; the next item's
+// loads are in flight while the current one computes.  dY is read from HBM exactly once; each wave
+// writes one f32 slab and a fixed-order reduce sums the slabs (bit-reproducible).
+#include "common.h"
+
+namespace {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+struct W3Args {
+  const bf16* x;   // (n, h, wd) 1-channel image
+  const bf16* dy;  // (n, h-7, wd-7, 32)
+  float* part;     // [waves][32][64]
+  int n, h, wd, oh, ow, nseg;
+};
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* p0, int stride) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * stride));
+  const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+__global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
+  constexpr int ROWB = 88, CPYB = 8 * ROWB;
+  __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
+  __shared__ __attribute__((aligned(16))) char dyt[4][32 * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
+  const int items = g.n * g.oh * g.nseg;
+  char* sg = strip[wv];
+  char* dt = dyt[wv];
+  f32x16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; }
+
+  // staging: lane l (l - 40 for l >= 40) loads input row l / 5, samples 8q .. 8q+11 (q = l % 5) as three 8-byte
+  // loads (past the row end -> 0); every lane loads two 16-B dY chunks (px = q >> 2, 8 channels)
+  struct Raw { u32x2 v[3]; u32x4 d[2]; };
+  auto load = [&](int it) __attribute__((always_inline)) {
+    Raw R;
+    it = it < items ? it : items - 1;
+    const int seg = it % g.nseg, rest = it / g.nseg;
+    const int oy = rest % g.oh, b = rest / g.oh;
+    const int l = lane < 40 ? lane : lane - 40;  // lanes 40..63 repeat lanes 0..23 (no divergent staging)
+    const int r = l / 5, q = l % 5;
+    const int col = seg * 32 + 8 * q;
+    const bf16* src = g.x + ((int64_t)b * g.h + oy + r) * g.wd;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int c = col + 4 * k;
+      R.v[k] = c + 4 <= g.wd ? *reinterpret_cast<const u32x2*>(src + c) : u32x2{0u, 0u};
+    }
+    const bf16* drow = g.dy + ((int64_t)b * g.oh + oy) * g.ow * 32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int qq = lane + 64 * s;
+      const int px = seg * 32 + (qq >> 2);
+      R.d[s] = px < g.ow ? *reinterpret_cast<const u32x4*>(drow + (int64_t)px * 32 + (qq & 3) * 8)
+                         : u32x4{0u, 0u, 0u, 0u};
+    }
+    return R;
+  };
+  const int i16 = lane & 15, gq = lane >> 4, h = lane >> 5;
+  const int n = lane & 31;  // tap within an N tile: ky = 4*nt + (n >> 3), kx = n & 7
+  auto run = [&](const Raw& R) __attribute__((always_inline)) {
+    {
+      // every lane writes (lanes 40..63 the same bytes as lanes 0..23): a branch on lane < 40 let the
+      // compiler sink the B-fragment reads below into the masked region (lanes >= 40 read nothing)
+      const int l = lane < 40 ? lane : lane - 40;
+      const int r = l / 5, q = l % 5;
+      const uint32_t d[6] = {R.v[0][0], R.v[0][1], R.v[1][0], R.v[1][1], R.v[2][0], R.v[2][1]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        // copy c dword i = samples (8q + c + 2i, +1)
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = c + 2 * i;
+          o[i] = (e & 1) ? ((d[e >> 1] >> 16) | (d[(e >> 1) + 1] << 16)) : d[e >> 1];
+        }
+        *reinterpret_cast<u32x4*>(sg + c * CPYB + r * ROWB + 16 * q) = u32x4{o[0], o[1], o[2], o[3]};
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int qq = lane + 64 * s;
+      *reinterpret_cast<u32x4*>(dt + (qq >> 2) * 64 + (qq & 3) * 16) = R.d[s];
+    }
+    const int kx = n & 7, cp = kx & 3;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
+      const int c4 = 16 * (gq & 1) + 4 * (i16 & 3);
+      const bf16x8 fa = tr_frag(dt + kr * 64 + c4 * 2, 64);  // dY^T[co][px = 16ks + 8h + j]
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int ky = 4 * nt + (n >> 3);
+        // x[oy+ky][16ks + 8h + kx + j], j = 0..7: copy kx&3 at sample 16ks + 8h + (kx&4)
+        const char* src = sg + cp * CPYB + ky * ROWB + 2 * (16 * ks + 8 * h + (kx & 4));
+        const u32x2 p0 = *reinterpret_cast<const u32x2*>(src);
+        const u32x2 p1 = *reinterpret_cast<const u32x2*>(src + 8);
+        const u32x4 f = {p0[0], p0[1], p1[0], p1[1]};
+        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, __builtin_bit_cast(bf16x8, f), acc[nt], 0, 0, 0);
+      }
+    }
+  };
+
+  int it = gw;
+  if (it < items) {
+    Raw ra = load(it), rb;
+    for (;;) {
+      rb = load(it + nw);
+      run(ra);
+      it += nw;
+      if (it >= items) break;
+      ra = load(it + nw);
+      run(rb);
+      it += nw;
+      if (it >= items) break;
+    }
+  }
+  // slab [co][tap]: accumulator row = co, column = tap
+  float* dst = g.part + (int64_t)gw * 2048;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      dst[co * 64 + nt * 32 + n] = acc[nt][r];
+    }
+}
+
+// dw[e] = sum of the slabs (double, fixed order), e = co*64 + tap: a block owns 32 elements, its 8
+// thread rows sum the slabs w = row (mod 8) in order, then the 8 row sums are added in row order
+__global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int nslab,
+                                                                 float* __restrict__ dw) {
+  __shared__ double red[8][32];
+  const int t = threadIdx.x, e = blockIdx.x * 32 + (t & 31), row = t >> 5;
+  double s = 0.0;
+  for (int w = row; w < nslab; w += 8) s += (double)part[(int64_t)w * 2048 + e];
+  red[row][t & 31] = s;
+  __syncthreads();
+  if (t < 32) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a += red[r][t];
+    dw[blockIdx.x * 32 + t] = (float)a;
+  }
+}
+
+}  // namespace
+
+extern "C" int mia_conv3_wgrad(const void* x, const void* dy, float* dw, float* part, int32_t nwaves, int32_t n,
+                               int32_t h, int32_t wd, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && dy && dw && part && n > 0 && h >= 8 && wd >= 8, "conv3_wgrad: bad arguments");
+  MIA_CHECK_ARG(nwaves > 0 && nwaves % 4 == 0, "conv3_wgrad: nwaves must be a positive multiple of 4");
+  MIA_CHECK_ARG(wd % 4 == 0, "conv3_wgrad: image width must be a multiple of 4 (8-byte row alignment)");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(dy) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0,
+                "conv3_wgrad: dy must be 16-byte and x 8-byte aligned");
+  W3Args a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(dy), part, n, h, wd, h - 7, wd - 7,
+           (int)cdiv(wd - 7, 32)};
+  MIA_CHECK_ARG((int64_t)n * a.oh * a.nseg < (1ll << 31), "conv3_wgrad: too many items");
+  hipStream_t s = as_stream(stream);
+  conv3_wgrad_kernel<<<nwaves / 4, 256, 0, s>>>(a);
+  MIA_LAUNCH_CHECK("conv3_wgrad");
+  conv3_wgrad_reduce_kernel<<<64, 256, 0, s>>>(part, nwaves, dw);
+  MIA_LAUNCH_CHECK("conv3_wgrad_reduce");
+  return 0;
+}

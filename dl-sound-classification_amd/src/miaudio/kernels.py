@@ -339,6 +339,21 @@ def trunk_conv8(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, n: int, h: in
     return (part, 4 * nblk) if stats else None
 
 
+def conv3_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, n: int, h: int, wd: int,
+                tag: str | None = None):
+    """Weight gradient of EnvNet trunk conv3 (1 -> 32, 8x8), bf16: x (n, h, wd), dy (n*(h-7)*(wd-7), 32)
+    -> dw f32 (32, 64) (taps ky*8 + kx)."""
+    oh, ow = h - 7, wd - 7
+    assert x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and dw.dtype == torch.float32
+    assert x.numel() == n * h * wd and dy.numel() == n * oh * ow * 32 and dw.numel() == 32 * 64
+    assert x.is_contiguous() and dy.is_contiguous() and dw.is_contiguous()
+    nw = 2048
+    part = workspace(nw * 2048 * 4, x.device, "conv3w")
+    with probe(tag or "", 2.0 * n * oh * ow * 32 * 64, x.numel() * 2 + dy.numel() * 2):
+        L.check(L.load().mia_conv3_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), part.data_ptr(), nw, n, h, wd,
+                                         _s()), "mia_conv3_wgrad")
+
+
 def bn_finalize_shifted(partial: torch.Tensor, nblk: int, P: int, C: int, kshift: torch.Tensor, gamma, beta,
                         running_mean, running_var, momentum: float, eps: float) -> BNState:
     """Training-mode BN statistics from shifted partial sums (mia_bn_finalize_shifted)."""

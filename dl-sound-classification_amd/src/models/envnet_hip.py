@@ -372,6 +372,10 @@ class EnvNetFunction(torch.autograd.Function):
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
                 K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, K.pack_weight(p[pa], cd, 0),
                                dWa, dinp, tag=f"t{blk}a")
+            elif (cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0
+                  and os.environ.get("MIA_CONV3W", "1") != "0"):
+                # conv3 weight gradient: wave-persistent, dY read once (csrc/conv3w.hip)
+                K.conv3_wgrad(ts["inp"], dya, dWa, B, H, W, tag=f"t{blk}a.wgrad")
             else:
                 if cin == 1:
                     Bop = K.conv(ts["inp"], L.RC, B, H, W, 1, ha, wa, kh, kw, row_kind=True)

@@ -306,3 +306,21 @@ def test_trunk_conv8_dgrad(cuda, n, h, wd):
     got = dx.double().view(n, h + 7, wd + 7, 32).permute(0, 3, 1, 2)
     assert torch.isfinite(got).all()
     assert rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("n,h,wd", [(2, 64, 860), (3, 9, 40), (1, 8, 12)])
+def test_conv3_wgrad(cuda, n, h, wd):
+    """Wave-persistent conv3 (1 -> 32, 8x8) weight gradient vs float64 torch on the same bf16 operands."""
+    g = torch.Generator(device=cuda).manual_seed(h * 7 + wd + n)
+    x = torch.randn(n, h, wd, generator=g, device=cuda).to(torch.bfloat16)
+    oh, ow = h - 7, wd - 7
+    dy = torch.randn(n, oh, ow, 32, generator=g, device=cuda).to(torch.bfloat16)
+    dw = torch.full((32, 64), float("nan"), device=cuda)
+    K.conv3_wgrad(x, dy, dw, n, h, wd)
+    torch.cuda.synchronize()
+    xd = x.double()[:, None].requires_grad_(True)
+    w = torch.zeros(32, 1, 8, 8, dtype=torch.float64, device=cuda, requires_grad=True)
+    F.conv2d(xd, w).backward(dy.double().permute(0, 3, 1, 2))
+    ref = w.grad.view(32, 64)
+    assert torch.isfinite(dw).all()
+    assert rel(dw, ref) < 1e-4
