@@ -143,22 +143,24 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
     }
 }
 
-// dw[e] = sum of the slabs (double, fixed order), e = co*64 + tap: a block owns 32 elements, its 8
-// thread rows sum the slabs w = row (mod 8) in order, then the 8 row sums are added in row order
-__global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int nslab,
-                                                                 float* __restrict__ dw) {
-  __shared__ double red[8][32];
-  const int t = threadIdx.x, e = blockIdx.x * 32 + (t & 31), row = t >> 5;
+// dw[e] = sum of the slabs (fixed order, bit-reproducible), e = co*64 + tap, in two coalesced stages:
+// stage 1: group g of C3_G sums its slabs in order into tmp[g][e] (double); stage 2: tmp summed in g order
+constexpr int C3_G = 64;
+__global__ __launch_bounds__(256) void conv3_wgrad_reduce1_kernel(const float* __restrict__ part, int nslab,
+                                                                  double* __restrict__ tmp) {
+  const int e = blockIdx.x * 256 + threadIdx.x, gi = blockIdx.y;
+  const int per = (nslab + C3_G - 1) / C3_G;
+  const int w0 = gi * per, w1 = min(nslab, w0 + per);
   double s = 0.0;
-  for (int w = row; w < nslab; w += 8) s += (double)part[(int64_t)w * 2048 + e];
-  red[row][t & 31] = s;
-  __syncthreads();
-  if (t < 32) {
-    double a = 0.0;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) a += red[r][t];
-    dw[blockIdx.x * 32 + t] = (float)a;
-  }
+  for (int w = w0; w < w1; ++w) s += (double)part[(int64_t)w * 2048 + e];
+  tmp[gi * 2048 + e] = s;
+}
+__global__ __launch_bounds__(256) void conv3_wgrad_reduce2_kernel(const double* __restrict__ tmp, float* __restrict__ dw) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+#pragma unroll 8
+  for (int g = 0; g < C3_G; ++g) s += tmp[g * 2048 + e];
+  dw[e] = (float)s;
 }
 
 }  // namespace
@@ -176,7 +178,9 @@ extern "C" int mia_conv3_wgrad(const void* x, const void* dy, float* dw, float* 
   hipStream_t s = as_stream(stream);
   conv3_wgrad_kernel<<<nwaves / 4, 256, 0, s>>>(a);
   MIA_LAUNCH_CHECK("conv3_wgrad");
-  conv3_wgrad_reduce_kernel<<<64, 256, 0, s>>>(part, nwaves, dw);
+  double* tmp = reinterpret_cast<double*>(part + (int64_t)nwaves * 2048);
+  conv3_wgrad_reduce1_kernel<<<dim3(8, C3_G), 256, 0, s>>>(part, nwaves, tmp);
+  conv3_wgrad_reduce2_kernel<<<8, 256, 0, s>>>(tmp, dw);
   MIA_LAUNCH_CHECK("conv3_wgrad_reduce");
   return 0;
 }

@@ -227,7 +227,7 @@ int mia_trunk_conv8(const void* x, const float* pre_scale, const float* pre_shif
 /* Weight gradient of the EnvNet-v2 trunk conv3 (Conv2d(1, 32, (8, 8)), replaces the cuDNN backward-weight
  * of src/models/envnet_v2.py:31): dw[co][ky*8+kx] = sum dy[b][oy][ox][co] * x[b][oy+ky][ox+kx].  x bf16
  * (n, h, wd) (wd % 4 == 0, 8-byte aligned), dy bf16 (n, h-7, wd-7, 32) 16-byte aligned, dw f32 (32, 64);
- * part: f32 workspace of nwaves*2048 floats (one slab per wave, summed in fixed order). */
+ * part: f32 workspace of nwaves*2048 + 64*4096 floats, 8-byte aligned (one slab per wave, summed in fixed order). */
 int mia_conv3_wgrad(const void* x, const void* dy, float* dw, float* part, int32_t nwaves, int32_t n, int32_t h,
                     int32_t wd, mia_stream_t stream);
 
