@@ -86,6 +86,118 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
   }
 }
 
+// maxpool(relu(bn(x))) before the BN statistics exist (bf16 x, training): relu(s*x + t) is monotone in
+// x with the sign of s = gamma*invstd, i.e. of gamma, so the window's winner is the raw maximum
+// (gamma > 0), the raw minimum (gamma < 0) or, gamma == 0, the first position (every z ties), always
+// the first occurrence -- torch's max_pool2d routing (when relu clamps the whole window the routed
+// position differs from torch's first-position pick, but its gradient relu'(z) * g is 0 at either).
+// One pass over x: the winner's raw value (bf16) + argmax, and the BN shifted sums about kshift[c]
+// (the conv bias) of every pixel -> partial[block][C][2] for mia_bn_finalize_shifted; the pooled
+// relu(s*x_win + t) is written by pool_apply_kernel once the statistics are final.
+__global__ __launch_bounds__(NT) void pool_raw_stats_kernel(const bf16* __restrict__ x, int n, int H, int W, int C,
+                                                            int kh, int kw, const float* __restrict__ gamma,
+                                                            const float* __restrict__ kshift, bf16* __restrict__ win,
+                                                            uint8_t* __restrict__ argmax, float* __restrict__ partial) {
+  const int OH = H / kh, OW = W / kw, G = C / 8;
+  const int total = n * OH * OW * G;
+  const int cg = threadIdx.x % G;  // constant per thread (G | NT, gridDim*NT a multiple of G)
+  float dir[8], ks[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float gv = gamma[cg * 8 + i];
+    dir[i] = gv > 0.f ? 1.f : (gv < 0.f ? -1.f : 0.f);
+    ks[i] = kshift[cg * 8 + i];
+    s1[i] = 0.f; s2[i] = 0.f;
+  }
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < total; idx += gridDim.x * NT) {
+    int p = idx / G;
+    const int ox = p % OW;
+    p /= OW;
+    const int oy = p % OH;
+    const int b = p / OH;
+    float best[8], bestraw[8];
+    int arg[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bestraw[i] = 0.f; arg[i] = 0; }
+    for (int dy = 0; dy < kh; ++dy) {
+      const int iy = oy * kh + dy;
+      const bf16* row = x + (((int64_t)b * H + iy) * W + (int64_t)ox * kw) * C + cg * 8;
+#pragma unroll 4
+      for (int dx = 0; dx < kw; ++dx) {
+        const uint4 u = *reinterpret_cast<const uint4*>(row + (int64_t)dx * C);
+        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+        float f[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w4[i] << 16); f[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u); }
+        const int pos = dy * kw + dx;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = f[i] - ks[i];
+          s1[i] += d;
+          s2[i] = fmaf(d, d, s2[i]);
+          const float key = dir[i] * f[i];  // gamma == 0: key 0 everywhere -> first position wins
+          if (key > best[i]) { best[i] = key; bestraw[i] = f[i]; arg[i] = pos; }
+        }
+      }
+    }
+    const int64_t aoff = (((int64_t)b * OH + oy) * OW + ox) * C + cg * 8;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a0 |= (uint32_t)arg[i] << (8 * i); a1 |= (uint32_t)arg[i + 4] << (8 * i); }
+    *reinterpret_cast<uint2*>(argmax + aoff) = make_uint2(a0, a1);
+    uint32_t o4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16 lo = (bf16)bestraw[2 * i], hi = (bf16)bestraw[2 * i + 1];  // exact: bf16 inputs
+      o4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(win + aoff) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+  }
+  // pixels right of the last full window (W % kw of them per row) enter the statistics only
+  const int tailw = W - OW * kw;
+  const int ttotal = n * H * tailw * G;
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < ttotal; idx += gridDim.x * NT) {
+    int p = idx / G;
+    const int tx = p % tailw;
+    const int r = p / tailw;  // b * H + iy
+    const uint4 u = *reinterpret_cast<const uint4*>(x + ((int64_t)r * W + OW * kw + tx) * C + cg * 8);
+    const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = __uint_as_float(w4[i] << 16) - ks[2 * i], hi = __uint_as_float(w4[i] & 0xffff0000u) - ks[2 * i + 1];
+      s1[2 * i] += lo; s2[2 * i] = fmaf(lo, lo, s2[2 * i]);
+      s1[2 * i + 1] += hi; s2[2 * i + 1] = fmaf(hi, hi, s2[2 * i + 1]);
+    }
+  }
+  // block reduction of the shifted sums per channel (threads with equal cg), fixed order
+  __shared__ float red[NT][17];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
+  __syncthreads();
+  if ((int)threadIdx.x < C * 2) {
+    const int c = threadIdx.x >> 1, which = threadIdx.x & 1, g = c >> 3, i = c & 7;
+    float a = 0.f;
+    for (int t = g; t < NT; t += G) a += red[t][which * 8 + i];
+    partial[((int64_t)blockIdx.x * C + c) * 2 + which] = a;
+  }
+}
+
+// pooled output relu(scale*x_win + shift) in the requested layout (see pool_fwd_kernel)
+__global__ __launch_bounds__(NT) void pool_apply_kernel(const bf16* __restrict__ win, int n, int OH, int OW, int C,
+                                                        const float* __restrict__ scale, const float* __restrict__ shift,
+                                                        void* out, int dtype, int layout) {
+  const int64_t total = (int64_t)n * OH * OW * C;
+  for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < total; e += (int64_t)gridDim.x * NT) {
+    const int c = (int)(e % C);
+    int64_t p = e / C;
+    const int ox = (int)(p % OW);
+    p /= OW;
+    const int oy = (int)(p % OH), b = (int)(p / OH);
+    const float v = fmaxf(fmaf((float)win[e], scale[c], shift[c]), 0.f);
+    st_elem(out, dtype, out_index(layout, b, oy, ox, c, OH, OW, C), v);
+  }
+}
+
 // one thread = one (input pixel, 8-channel group); block partial reductions like norm.hip
 __global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ dout, int layout,
                                                       const uint8_t* __restrict__ argmax, const void* __restrict__ x,
@@ -429,6 +541,33 @@ extern "C" int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, 
   const int nb = (int)std::min<int64_t>(cdiv(total, NT), 16384);
   pool_fwd_kernel<<<nb, NT, 0, as_stream(stream)>>>(x, dtype, n, h, w, c, kh, kw, scale, shift, out, out_layout, argmax);
   MIA_LAUNCH_CHECK("pool_fwd");
+  return 0;
+}
+
+extern "C" int mia_pool_raw_stats(const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                                  const float* gamma, const float* kshift, void* win, uint8_t* argmax, float* partial,
+                                  int32_t nblocks, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && gamma && kshift && win && argmax && partial && nblocks > 0, "pool_raw_stats: null pointer");
+  MIA_CHECK_ARG(c % 8 == 0 && c >= 8 && c * 2 <= NT && (NT % (c / 8)) == 0, "pool_raw_stats: channels");
+  MIA_CHECK_ARG(h % kh == 0 && w >= kw && kh * kw <= 256, "pool_raw_stats: window geometry");
+  MIA_CHECK_ARG((int64_t)n * h * w * (c / 8) < (1ll << 31), "pool_raw_stats: too many elements for 32-bit indexing");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(win)) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(argmax) % 8 == 0, "pool_raw_stats: alignment");
+  pool_raw_stats_kernel<<<nblocks, NT, 0, as_stream(stream)>>>(reinterpret_cast<const bf16*>(x), n, h, w, c, kh, kw,
+                                                               gamma, kshift, reinterpret_cast<bf16*>(win), argmax,
+                                                               partial);
+  MIA_LAUNCH_CHECK("pool_raw_stats");
+  return 0;
+}
+
+extern "C" int mia_pool_apply(const void* win, int32_t n, int32_t oh, int32_t ow, int32_t c, const float* scale,
+                              const float* shift, void* out, int32_t dtype, int32_t out_layout, mia_stream_t stream) {
+  MIA_CHECK_ARG(win && scale && shift && out && n > 0 && oh > 0 && ow > 0 && c > 0, "pool_apply: bad arguments");
+  const int64_t total = (int64_t)n * oh * ow * c;
+  const int nb = (int)std::min<int64_t>(cdiv(total, NT), 16384);
+  pool_apply_kernel<<<nb, NT, 0, as_stream(stream)>>>(reinterpret_cast<const bf16*>(win), n, oh, ow, c, scale, shift,
+                                                      out, dtype, out_layout);
+  MIA_LAUNCH_CHECK("pool_apply");
   return 0;
 }
 

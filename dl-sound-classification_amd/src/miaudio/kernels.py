@@ -256,6 +256,24 @@ def pool_fwd(x, n, h, w, c, kh, kw, bn: BNState, out, out_layout, argmax):
             "mia_pool_fwd")
 
 
+def pool_raw_stats(x, n, h, w, c, kh, kw, gamma, kshift, win, argmax):
+    """maxpool(relu(bn(x))) winners before the BN statistics exist (bf16, training): writes the raw
+    winner values `win` (n, h/kh, w/kw, c) bf16 and `argmax`, returns (partial, nblk) of the BN shifted
+    sums about kshift for bn_finalize_shifted; pool_apply then writes the pooled output."""
+    assert x.dtype == torch.bfloat16 and win.dtype == torch.bfloat16 and x.is_contiguous()
+    nblk = 2048
+    part = torch.empty(nblk, c, 2, dtype=torch.float32, device=x.device)
+    L.check(L.load().mia_pool_raw_stats(x.data_ptr(), n, h, w, c, kh, kw, gamma.data_ptr(), kshift.data_ptr(),
+                                        win.data_ptr(), argmax.data_ptr(), part.data_ptr(), nblk, _s()),
+            "mia_pool_raw_stats")
+    return part, nblk
+
+
+def pool_apply(win, n, oh, ow, c, bn: BNState, out, out_layout):
+    L.check(L.load().mia_pool_apply(win.data_ptr(), n, oh, ow, c, bn.scale.data_ptr(), bn.shift.data_ptr(),
+                                    out.data_ptr(), L.dtype_code(out), out_layout, _s()), "mia_pool_apply")
+
+
 def pool_bwd_bn_relu_reduce(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn: BNState, dz):
     g = torch.empty(2, c, dtype=torch.float32, device=x.device)
     lib = L.load()

@@ -155,11 +155,21 @@ class EnvNetFunction(torch.autograd.Function):
                        shift=bn1.shift)
             K.gemm(A, K.dense(w2, L.KC, 64, 512), K.epilogue(y2, 64, bias=p[5]), B * W2, 64, 512, cd,
                    tag="conv2.fwd")
-        bn2 = bn(1, y2, B * W2, 64)
         # ---- maxpool (1,64) of relu(bn2(y2)), written as the transposed trunk image (B, 64, Wp)
         X0 = torch.empty(B, 64, Wp, dtype=tdt, device=dev)
         am0 = torch.empty(B, Wp, 64, dtype=torch.uint8, device=dev)
-        K.pool_fwd(y2, B, 1, W2, 64, 1, 64, bn2, X0, 1, am0)
+        if cd == L.BF16 and training and os.environ.get("MIA_POOL_RAW", "1") != "0":
+            # one pass over y2: window winners on the raw values (monotone BN+ReLU) + BN2 statistics,
+            # then the pooled relu(bn2(winner)) once the statistics are final
+            win0 = torch.empty(B, Wp, 64, dtype=tdt, device=dev)
+            part2, nb2 = K.pool_raw_stats(y2, B, 1, W2, 64, 1, 64, p[6], p[5], win0, am0)
+            m1 = bns[1]
+            bn2 = K.bn_finalize_shifted(part2, nb2, B * W2, 64, p[5], m1.weight, m1.bias, m1.running_mean,
+                                        m1.running_var, m1.momentum if m1.momentum is not None else 0.1, m1.eps)
+            K.pool_apply(win0, B, 1, Wp, 64, bn2, X0, 1)
+        else:
+            bn2 = bn(1, y2, B * W2, 64)
+            K.pool_fwd(y2, B, 1, W2, 64, 1, 64, bn2, X0, 1, am0)
         fe.__exit__(None, None, None)
         saved.update(x=x, y1=y1, y2=y2, bn1=bn1, bn2=bn2, X0=X0, am0=am0)
 

@@ -150,6 +150,18 @@ int mia_bn_relu_bwd_apply(const void* dact, const void* x, void* dx, int32_t dty
 int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c,
                  int32_t kh, int32_t kw, const float* scale, const float* shift, void* out,
                  int32_t out_layout, uint8_t* argmax, mia_stream_t stream);
+/* Forward of maxpool(relu(bn(x))) split around the BN statistics (training, bf16 x (n, h, w, c) NHWC):
+ * mia_pool_raw_stats reads x once and writes each window's winner (raw bf16 value; raw max for gamma > 0,
+ * raw min for gamma < 0, first position for gamma == 0; first occurrence on ties), its argmax (u8, as
+ * mia_pool_fwd) and the BN shifted sums about kshift[c] of EVERY pixel (the w % kw right of the last window
+ * included): partial[nblocks][c][2] for mia_bn_finalize_shifted (h % kh == 0).
+ * mia_pool_apply then writes relu(scale*win + shift) in mia_pool_fwd's output layouts.  Replaces the
+ * BatchNorm2d statistics pass + MaxPool2d of src/models/envnet_v2.py:20-24. */
+int mia_pool_raw_stats(const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                       const float* gamma, const float* kshift, void* win, uint8_t* argmax, float* partial,
+                       int32_t nblocks, mia_stream_t stream);
+int mia_pool_apply(const void* win, int32_t n, int32_t oh, int32_t ow, int32_t c, const float* scale,
+                   const float* shift, void* out, int32_t dtype, int32_t out_layout, mia_stream_t stream);
 /* Backward of pool(relu(bn(x))) up to dz (the BN output grad) + BN reductions
  * (nn.MaxPool2d after BN+ReLU, envnet_v2.py:16-23,32-37). */
 int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint8_t* argmax,
