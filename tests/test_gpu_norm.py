@@ -326,14 +326,14 @@ def test_conv3_wgrad(cuda, n, h, wd):
     assert rel(dw, ref) < 1e-4
 
 
-@pytest.mark.parametrize("n,w,kw", [(3, 55102, 64), (2, 300, 64), (2, 70, 7)])
-def test_pool_raw_stats_matches_pool_fwd(cuda, n, w, kw):
+@pytest.mark.parametrize("n,h,w,kw,C", [(3, 1, 55102, 64, 64), (2, 1, 300, 64, 64), (2, 1, 70, 7, 64),
+                                        (2, 10, 279, 2, 64), (2, 10, 139, 2, 128)])
+def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     """One-pass maxpool-on-raw-winners + BN statistics (then relu(bn(winner))) == BN statistics pass +
     maxpool of relu(bn(x)); argmax equal wherever the pooled value is positive (elsewhere the routed
     gradient is 0 either way).  Negative and zero gammas exercise the min / first-position winners."""
-    C = 64
     g = torch.Generator(device=cuda).manual_seed(n * w + kw)
-    x = (torch.randn(n, 1, w, C, generator=g, device=cuda) * 2 + 0.3).to(torch.bfloat16)
+    x = (torch.randn(n, h, w, C, generator=g, device=cuda) * 2 + 0.3).to(torch.bfloat16)
     gamma = torch.randn(C, generator=g, device=cuda)
     gamma[5] = 0.0
     beta = torch.randn(C, generator=g, device=cuda) * 0.5
@@ -341,19 +341,19 @@ def test_pool_raw_stats_matches_pool_fwd(cuda, n, w, kw):
     ow = w // kw
     rm1, rv1 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
     rm2, rv2 = rm1.clone(), rv1.clone()
-    win = torch.empty(n, ow, C, dtype=torch.bfloat16, device=cuda)
-    am1 = torch.empty(n, ow, C, dtype=torch.uint8, device=cuda)
-    part, nb = K.pool_raw_stats(x, n, 1, w, C, 1, kw, gamma, kshift, win, am1)
-    st1 = K.bn_finalize_shifted(part, nb, n * w, C, kshift, gamma, beta, rm1, rv1, 0.1, 1e-5)
-    out1 = torch.empty(n, C, ow, dtype=torch.bfloat16, device=cuda)
-    K.pool_apply(win, n, 1, ow, C, st1, out1, 1)
-    st2 = K.bn_fwd_stats(x, n * w, C, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
-    out2 = torch.empty(n, C, ow, dtype=torch.bfloat16, device=cuda)
-    am2 = torch.empty(n, ow, C, dtype=torch.uint8, device=cuda)
-    K.pool_fwd(x, n, 1, w, C, 1, kw, st2, out2, 1, am2)
+    win = torch.empty(n, h, ow, C, dtype=torch.bfloat16, device=cuda)
+    am1 = torch.empty(n, h, ow, C, dtype=torch.uint8, device=cuda)
+    part, nb = K.pool_raw_stats(x, n, h, w, C, 1, kw, gamma, kshift, win, am1)
+    st1 = K.bn_finalize_shifted(part, nb, n * h * w, C, kshift, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    out1 = torch.empty(n, h, ow, C, dtype=torch.bfloat16, device=cuda)
+    K.pool_apply(win, n, h, ow, C, st1, out1, 0)
+    st2 = K.bn_fwd_stats(x, n * h * w, C, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
+    out2 = torch.empty(n, h, ow, C, dtype=torch.bfloat16, device=cuda)
+    am2 = torch.empty(n, h, ow, C, dtype=torch.uint8, device=cuda)
+    K.pool_fwd(x, n, h, w, C, 1, kw, st2, out2, 0, am2)
     torch.cuda.synchronize()
     for a, b in ((st1.mean, st2.mean), (st1.invstd, st2.invstd), (rm1, rm2), (rv1, rv2)):
         assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
     assert (out1.float() - out2.float()).abs().max() <= 2e-2 * out2.float().abs().max()
-    pos = out2.permute(0, 2, 1) > 0
+    pos = out2 > 0
     assert torch.equal(am1[pos], am2[pos])
