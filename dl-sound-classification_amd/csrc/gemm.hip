@@ -1577,6 +1577,50 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
     }
     return;
   }
+  // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
+  // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
+  const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
+                       (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU) && !g.e.accumulate && !g.e.rm_inner &&
+                       g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N && (g.e.ldc & 7) == 0 &&
+                       ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0;
+  if (plain16) {
+    float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int col = wn * 64 + j * 32 + (lane & 31);
+          tile[row * 128 + (col ^ (((row >> 2) & 1) << 5))] = acc[i][j][r];
+        }
+    __syncthreads();
+    const int col = (lane & 15) * 8;
+    float bv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bv[c] = g.e.bias ? g.e.bias[n0 + col + c] : 0.f;
+    const bool relu = g.e.act == MIA_ACT_RELU;
+    bf16* out = reinterpret_cast<bf16*>(g.e.ptr);
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int row = wave * 32 + it * 4 + (lane >> 4);
+      const int sw = ((row >> 2) & 1) << 5;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ sw));
+      const f32x4 b = *reinterpret_cast<const f32x4*>(tile + row * 128 + ((col + 4) ^ sw));
+      float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      uint32_t w4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float lo = v[2 * q] + bv[2 * q], hi = v[2 * q + 1] + bv[2 * q + 1];
+        if (relu) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+        const bf16 bl = (bf16)lo, bh = (bf16)hi;
+        w4[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+      }
+      *reinterpret_cast<uint4*>(out + (m0 + row) * g.e.ldc + n0 + col) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    return;
+  }
 
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
 #pragma unroll
