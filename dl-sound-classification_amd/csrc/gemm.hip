@@ -1579,8 +1579,12 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   }
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
   // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
+  const bool save = g.e.act == MIA_ACT_GELU_SAVE;
   const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
-                       (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU) && !g.e.accumulate && !g.e.rm_inner &&
+                       (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU || g.e.act == MIA_ACT_GELU ||
+                        (save && g.e.aux_dtype == MIA_BF16 && (g.e.ldaux & 7) == 0 &&
+                         ((reinterpret_cast<uintptr_t>(g.e.aux)) & 15) == 0)) &&
+                       !g.e.accumulate && !g.e.rm_inner &&
                        g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N && (g.e.ldc & 7) == 0 &&
                        ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0;
   if (plain16) {
@@ -1600,8 +1604,17 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
     float bv[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) bv[c] = g.e.bias ? g.e.bias[n0 + col + c] : 0.f;
-    const bool relu = g.e.act == MIA_ACT_RELU;
+    const bool relu = g.e.act == MIA_ACT_RELU, gelu = g.e.act == MIA_ACT_GELU || save;
     bf16* out = reinterpret_cast<bf16*>(g.e.ptr);
+    auto pack = [](const float* f) {
+      uint32_t w4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16 bl = (bf16)f[2 * q], bh = (bf16)f[2 * q + 1];
+        w4[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+      }
+      return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    };
 #pragma unroll 4
     for (int it = 0; it < 8; ++it) {
       const int row = wave * 32 + it * 4 + (lane >> 4);
@@ -1609,15 +1622,14 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ sw));
       const f32x4 b = *reinterpret_cast<const f32x4*>(tile + row * 128 + ((col + 4) ^ sw));
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-      uint32_t w4[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float lo = v[2 * q] + bv[2 * q], hi = v[2 * q + 1] + bv[2 * q + 1];
-        if (relu) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
-        const bf16 bl = (bf16)lo, bh = (bf16)hi;
-        w4[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
-      }
-      *reinterpret_cast<uint4*>(out + (m0 + row) * g.e.ldc + n0 + col) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      for (int c = 0; c < 8; ++c) v[c] += bv[c];
+      if (save)  // GELU_SAVE: the pre-activation goes to aux (MLP fc1, read back by the backward)
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<char*>(g.e.aux)) + (m0 + row) * g.e.ldaux +
+                                  n0 + col) = pack(v);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = relu ? fmaxf(v[c], 0.f) : (gelu ? gelu_erf(v[c]) : v[c]);
+      *reinterpret_cast<uint4*>(out + (m0 + row) * g.e.ldc + n0 + col) = pack(v);
     }
     return;
   }
