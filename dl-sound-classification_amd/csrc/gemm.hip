@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
   // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
   const bool save = g.e.act == MIA_ACT_GELU_SAVE;
-  const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
+  const bool plain16 = g.full16 && g.split == 1 && g.e.dtype == MIA_BF16 &&
                        (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU || g.e.act == MIA_ACT_GELU ||
                         (save && g.e.aux_dtype == MIA_BF16 && (g.e.ldaux & 7) == 0 &&
                          ((reinterpret_cast<uintptr_t>(g.e.aux)) & 15) == 0)) &&
@@ -1871,6 +1871,8 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     d.e = to_dev(*E);
     static const int nt_env = [] { const char* v = getenv("MIA_EPI_NT"); return v ? atoi(v) : 1; }();
     d.nt = nt_env;
+    static const int f16_env = [] { const char* v = getenv("MIA_EPI_FULL16"); return v ? atoi(v) : 1; }();
+    d.full16 = f16_env;
     hipStream_t s = as_stream(stream);
     hipError_t err;
     const int la = A->layout, lb = B->layout;

@@ -24,7 +24,8 @@ struct DArgs {
               // block, so A streams from HBM once instead of once per column tile)
   float* ws;
   EpiDev e;
-  int nt;  // full-tile f32 epilogue with non-temporal stores
+  int nt;      // full-tile f32 epilogue with non-temporal stores
+  int full16;  // full-tile bf16 epilogue allowed
 };
 
 // -------------------------------------------------------------------------- epilogue
