@@ -1,19 +1,23 @@
 #!/usr/bin/env python
-"""Training-throughput benchmark of the MI355X hot path (BASELINE.json `metric`).
+"""Training-throughput benchmark of the MI355X hot path (BASELINE.json `metric`: training clips/sec
+for EnvNet-v2 & AST).
 
-Workload (configs[1]): EnvNet-v2, bf16 compute (f32 master params / grads / Adam state),
-batch 256 per GPU, synthetic 5 s @ 44.1 kHz clips resident in HBM.  One step = on-GPU BC
-mixing -> EnvNet-v2 forward -> soft-label loss -> backward -> (N>1: RCCL gradient all-reduce)
--> global-norm clip 1.0 -> Adam(lr 1e-4, wd 1e-4).  `--model ast` times configs[2] instead
-(waveform -> on-GPU log-mel -> AST fwd+bwd -> clip + Adam).
+Default invocation (what the driver runs) times BOTH configs on the same GPUs, one after the other:
+  * configs[1] — EnvNet-v2, bf16 compute (f32 master params / grads / Adam state), batch 256 per GPU:
+    on-GPU BC mixing -> forward -> soft-label loss -> backward -> (N>1: RCCL gradient all-reduce)
+    -> global-norm clip 1.0 -> Adam(lr 1e-4, wd 1e-4).  This is the top-level JSON line.
+  * configs[2] — AST, bf16, batch 256 per GPU: on-GPU log-mel -> SpecAugment + Mixup -> forward ->
+    soft-label loss -> backward -> (all-reduce) -> clip + Adam.  Nested as the "ast" object with its
+    own value / ms_per_step / roofline (attention forward, the north-star MFMA kernel) / cpu_baseline.
+Synthetic 5 s @ 44.1 kHz clips resident in HBM.  `--model envnet|ast` times one leg only (profiling).
 
 python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch one process per GPU with
-torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env).
-Rank 0 prints ONE JSON line.
+torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env).  Rank 0 prints ONE line.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -34,21 +38,25 @@ F32_PEAK_TF = 157.3
 ENVNET_FLOP_PER_CLIP = 32.74e9
 AST_FLOP_PER_CLIP = 1139.7e9
 
+# probe tags whose roofline is HBM bandwidth (the rest are MFMA-bound contractions)
+HBM_TAGS = {"optim.step", "logmel.fwd", "conv1.fwd", "conv1.wgrad"}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=["envnet", "ast"], default="envnet")
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256 for both models)")
+    ap.add_argument("--model", choices=["both", "envnet", "ast"], default="both")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU EnvNet batch (default 256)")
+    ap.add_argument("--ast-batch", type=int, default=None, help="per-GPU AST batch (default 256)")
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default=None, help="comma list of GEMM tags to time live (default: auto)")
+    ap.add_argument("--probe", default=None, help="comma list of probe tags to time live (default: auto)")
     return ap.parse_args()
 
 
-def setup_dist(args):
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -56,15 +64,6 @@ def setup_dist(args):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
-
-
-def build_envnet(args, dev):
-    from src.models.envnet_v2 import EnvNetV2
-    from src.training.optim import FusedAdam
-    torch.manual_seed(42)
-    model = EnvNetV2(num_classes=50, dropout=0.5, compute_dtype=args.dtype).to(dev).train()
-    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
-    return model, opt
 
 
 def make_batch(B, T, dev, rank, num_classes=50):
@@ -75,9 +74,17 @@ def make_batch(B, T, dev, rank, num_classes=50):
     return wav, labels, g
 
 
-def envnet_step_fn(model, opt, wav, labels, g, world, ddp):
+def build_envnet_step(args, dev, rank, world, B):
     from src.datasets.augment import bc_mix
     from src.miaudio import kernels as K
+    from src.models.envnet_v2 import EnvNetV2
+    from src.training.ddp import GradAllReducer
+    from src.training.optim import FusedAdam
+    torch.manual_seed(42)
+    model = EnvNetV2(num_classes=50, dropout=0.5, compute_dtype=args.dtype).to(dev).train()
+    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
+    wav, labels, g = make_batch(B, 220_500, dev, rank)
+    ddp = GradAllReducer(model, world) if world > 1 else None
 
     def step():
         x, y, _ = bc_mix(wav, labels, 50, gen=g)
@@ -89,7 +96,11 @@ def envnet_step_fn(model, opt, wav, labels, g, world, ddp):
         opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
-    return step
+
+    tags = ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv1.fwd", "conv1.wgrad", "conv2.fwd", "conv2.dgrad",
+            "conv2.wgrad", "fc1.fwd", "fc1.wgrad", "fc1.dgrad", "optim.step", "frontend.fwd", "frontend.bwd"]
+    workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
+    return step, ENVNET_FLOP_PER_CLIP, tags, workload
 
 
 def frontend_summary(regions: dict, B: int):
@@ -116,31 +127,43 @@ def cpu_model() -> str:
     return "unknown"
 
 
-# probe tag -> substring of its kernel symbol (disambiguates launches with similar durations)
+# probe tag -> substrings of its kernel symbols in the rocprof / PMC tables
 KERNEL_HINT = {
-    "t0b.fwd": "conv8_kernel<true, true, 2>",
-    "t0b.dgrad": "conv8_kernel<false, false, 2>",
-    "t0b.wgrad": "wgrad8_kernel",
-    "conv2.fwd": "feconv_kernel<32, 16, 2, true>",
-    "conv2.dgrad": "feconv_kernel<64, 8, 1, false>",
-    "conv2.wgrad": "fe_wgrad_kernel",
-    "conv1.fwd": "fe_conv1_kernel",
-    "attn.fwd": "attn_fwd_kernel",
+    "t0b.fwd": ["conv8_kernel<true, true, 2>"],
+    "t0b.dgrad": ["conv8_kernel<false, false, 2>"],
+    "t0b.wgrad": ["wgrad8_kernel"],
+    "conv2.fwd": ["feconv_kernel<32, 16, 2, true>"],
+    "conv2.dgrad": ["feconv_kernel<64, 8, 1, false>"],
+    "conv2.wgrad": ["fe_wgrad_kernel"],
+    "conv1.fwd": ["fe_conv1_kernel"],
+    "attn.fwd": ["attn_fwd_kernel"],
+    "attn.bwd": ["attn_bwd"],
+    "optim.step": ["sqnorm_kernel", "norm_final_kernel", "adam_kernel"],
+    "logmel.fwd": ["fft_mel_db_kernel", "clip_stats_kernel", "clip_norm_kernel", "logmel"],
 }
 
 
 def pmc_traffic(model: str, ks: dict, tag: str | None = None):
-    """HBM bytes per launch of the probed kernel from the committed rocprofv3 PMC summary of the same
+    """HBM bytes per launch of the probed launch from the committed rocprofv3 PMC summary of the same
     bench command (profiles/<round>_pmc_<model>.json, written by tools/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes).  The probed launch is matched to a kernel symbol by launches per
-    step and by its rocprof average duration (must agree with the live HIP-event time within 10 %)."""
+    FETCH_SIZE / WRITE_SIZE passes).  A multi-kernel launch (optim.step, logmel.fwd) sums its kernels;
+    a single-kernel tag is matched by its symbol, launches per step and the rocprof average duration
+    (which must agree with the live HIP-event time within 10 %)."""
     files = sorted((REPO / "profiles").glob(f"r*_pmc_{model}.json"))
     if not files:
         return None, None
     table = json.loads(files[-1].read_text())["kernels"]
-    hint = KERNEL_HINT.get(tag or "")
-    if hint and any(hint in n for n in table):
-        table = {n: e for n, e in table.items() if hint in n}
+    hints = KERNEL_HINT.get(tag or "", [])
+    if len(hints) > 1:
+        sel = {n: e for n, e in table.items() if any(h in n for h in hints) and "hbm_bytes" in e}
+        if not sel:
+            return None, {"file": files[-1].name, "match": None}
+        per = sum(e["hbm_bytes"] * e["launches_per_step"] for e in sel.values()) / max(ks["launches_per_step"], 1)
+        avg = sum(e["avg_ms"] * e["launches_per_step"] for e in sel.values()) / max(ks["launches_per_step"], 1)
+        return per, {"file": files[-1].name, "kernels": sorted(sel), "rocprof_ms_per_launch": round(avg, 4),
+                     "live_vs_rocprof": round(abs(avg - ks["ms"]) / ks["ms"], 4)}
+    if hints and any(hints[0] in n for n in table):
+        table = {n: e for n, e in table.items() if hints[0] in n}
     best = None
     for name, e in table.items():
         if "hbm_bytes" not in e or e["launches_per_step"] != round(ks["launches_per_step"]):
@@ -155,9 +178,91 @@ def pmc_traffic(model: str, ks: dict, tag: str | None = None):
                             "live_vs_rocprof": round(rel, 4)}
 
 
-def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 10):
-    """Oracle (CPU restatement of the reference path) timed on this host: fwd+loss+bwd+clip+Adam."""
+def roofline(model: str, tag: str, ks: dict, peak_tf: float):
+    traffic, tsrc = pmc_traffic(model, ks, tag)
+    kname = "+".join(KERNEL_HINT.get(tag, ["igemm_kernel/dgemm_kernel"]))
+    if tsrc and tsrc.get("kernel"):
+        kname = tsrc["kernel"].replace("_ZN12_GLOBAL__N_1", "").replace("(anonymous namespace)::", "").split("(")[0]
+    if tag in HBM_TAGS:
+        ach, peak, unit = ks["gbs"], HBM_PEAK_GBS, "GB/s"
+    else:
+        ach, peak, unit = ks["tflops"], peak_tf, "TFLOP/s"
+    return {"bound": "hbm" if tag in HBM_TAGS else "mfma", "kernel": f"{kname} [{tag}]", "achieved": round(ach, 2),
+            "peak": peak, "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+            "algorithmic_per_launch": {"flop": ks["flop"], "bytes": ks["bytes"]},
+            "ms_per_launch": round(ks["ms"], 4), "launches_per_step": ks["launches_per_step"]}
+
+
+def time_leg(step, probe_tags, args, world, dev, warmup, steps):
+    """W untimed steps, then exactly K steps between barrier + synchronize; max over ranks."""
+    from src.miaudio import kernels as K
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    K.PROBE = {t: [] for t in probe_tags}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probes, K.PROBE = K.PROBE, None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    kstats = {}
+    for tag, recs in probes.items():
+        if not recs:
+            continue
+        dur = sum(e0.elapsed_time(e1) for e0, e1, _, _ in recs) / len(recs)  # ms per launch
+        flops, byts = recs[0][2], recs[0][3]
+        kstats[tag] = {"ms": dur, "tflops": flops / (dur * 1e-3) / 1e12, "gbs": byts / (dur * 1e-3) / 1e9,
+                       "launches_per_step": len(recs) / steps, "flop": flops, "bytes": byts}
+    return elapsed, float(loss), kstats
+
+
+def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_clip, args, workload,
+               roof_tag=None):
+    ms = elapsed / steps * 1e3
+    regions = {k: v for k, v in kstats.items() if k.startswith("frontend.")}
+    ks = {k: v for k, v in kstats.items() if k not in regions}
+    peak_tf = BF16_MFMA_PEAK_TF if args.dtype == "bf16" else F32_PEAK_TF
+    dom = max(ks, key=lambda k: ks[k]["ms"] * ks[k]["launches_per_step"]) if ks else None
+    name = "EnvNet-v2" if model == "envnet" else "AST"
+    out = {
+        "metric": f"training clips/sec ({name}, ESC-50 shape)",
+        "value": round(B * world * steps / elapsed, 2), "unit": "clips/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (peak-normalised 0.1*N(0,1) clips, uniform labels)",
+        "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B, "clip_samples": 220_500,
+                   "parallelism": f"dp{world}"},
+        "roofline": roofline(model, roof_tag or dom, ks[roof_tag or dom], peak_tf) if (roof_tag or dom) in ks else None,
+        "dominant_kernel": roofline(model, dom, ks[dom], peak_tf) if dom and roof_tag else None,
+        "step_tflops": round(flop_per_clip * B / (ms * 1e-3) / 1e12, 2),
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                    for k, v in ks.items()},
+        "loss": loss,
+    }
+    if model == "envnet":
+        out["frontend_path"] = frontend_summary(regions, B)
+    if out["dominant_kernel"] is None:
+        out.pop("dominant_kernel")
+    return out
+
+
+def cpu_baseline_envnet(threads: int, batch: int, steps: int):
+    """Oracle (CPU restatement of the reference path) timed on this host: BC-mix + fwd + loss + bwd +
+    clip + Adam (kind "port")."""
     sys.path.insert(0, str(REPO))
+    import random
+
+    from oracle import augment as oaug
     from oracle import envnet as oenv
     from oracle import train as otrain
     torch.set_num_threads(threads)
@@ -169,13 +274,18 @@ def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 10):
         params[name] = torch.zeros(shape) if name.endswith("mean") else torch.ones(shape)
     names = oenv.trainable_names(params)
     opt = torch.optim.Adam([params[n] for n in names], lr=1e-4, weight_decay=1e-4)
-    x = torch.randn(batch, 1, 220_500, generator=gen) * 0.1
-    y = torch.zeros(batch, 50)
-    y[torch.arange(batch), torch.randint(0, 50, (batch,), generator=gen)] = 1.0
+    pool = [torch.randn(1, 220_500, generator=gen) * 0.1 for _ in range(2 * batch)]
+    pool_labels = [int(v) for v in torch.randint(0, 50, (2 * batch,), generator=gen)]
+    rng = random.Random(0)
 
     def one():
-        z = oenv.forward(params, x, training=True)
-        loss = otrain.soft_ce(z, y)
+        xs, ys = [], []
+        for b in range(batch):  # per-sample BC mixing as in the reference's DataLoader workers
+            m, y, _, _, _ = oaug.apply_bc_mixing(pool[b], pool_labels[b], pool, pool_labels, 50, rng)
+            xs.append(m)
+            ys.append(y)
+        z = oenv.forward(params, torch.stack(xs), training=True)
+        loss = otrain.soft_ce(z, torch.stack(ys))
         loss.backward()
         torch.nn.utils.clip_grad_norm_([params[n] for n in names], 1.0)
         opt.step()
@@ -187,109 +297,106 @@ def cpu_baseline_envnet(threads: int, batch: int = 4, steps: int = 10):
         one()
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
-            "sample": f"oracle EnvNet-v2 f32 train step (fwd+loss+bwd+clip+Adam), batch {batch}, "
+            "sample": f"oracle EnvNet-v2 f32 train step (BC-mix, fwd, loss, bwd, clip, Adam), batch {batch}, "
                       f"{steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work on {threads} threads "
                       f"of {cpu_model()}"}
 
 
+def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 3):
+    """Oracle AST train step on this host with the feature path included: log-mel of the waveform
+    (ASTPreprocessor restatement), SpecAugment + Mixup per clip, fwd, loss, bwd, clip, Adam."""
+    sys.path.insert(0, str(REPO))
+    import random
+
+    from oracle import ast as oast
+    from oracle import augment as oaug
+    from oracle import logmel as olog
+    from oracle import train as otrain
+    torch.set_num_threads(threads)
+    hw, hb = oast.head_hash(900, 50)
+    params = {k: v.clone().requires_grad_(True) for k, v in oast.model_params(oast.deit_hash_state(300), hw, hb).items()}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-4, weight_decay=1e-4)
+    gen = torch.Generator().manual_seed(0)
+    wav = (torch.randn(batch, 220_500, generator=gen) * 0.1).numpy()
+    labels = [int(v) for v in torch.randint(0, 50, (batch,), generator=gen)]
+    rng = random.Random(0)
+
+    def one():
+        spec = olog.logmel(wav)                                    # (B, 128, 1379)
+        pool = [spec[b:b + 1] for b in range(batch)]
+        xs, ys = [], []
+        for b in range(batch):
+            s, _ = oaug.specaugment(pool[b], 192, 48, rng)
+            s, y, _, _ = oaug.apply_mixup(s, labels[b], pool, labels, 50, 0.5, rng)
+            xs.append(s)
+            ys.append(y)
+        probs = oast.forward(params, torch.cat(xs))
+        loss = otrain.soft_ce(probs, torch.stack(ys))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(list(params.values()), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"oracle AST f32 train step (log-mel, SpecAugment+Mixup, fwd, loss, bwd, clip, Adam), "
+                      f"batch {batch}, {steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work on {threads} "
+                      f"threads of {cpu_model()}"}
+
+
+def free_leg():
+    from src.miaudio import kernels as K
+    K._WS.clear()
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
+    world, rank, local = setup_dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    from src.miaudio import kernels as K
-    from src.training.ddp import GradAllReducer
-
-    if args.model == "envnet":
+    results = {}
+    if args.model in ("both", "envnet"):
         B = args.batch or 256
-        model, opt = build_envnet(args, dev)
-        wav, labels, g = make_batch(B, 220_500, dev, rank)
-        ddp = GradAllReducer(model, world) if world > 1 else None
-        step = envnet_step_fn(model, opt, wav, labels, g, world, ddp)
-        flop_per_clip = ENVNET_FLOP_PER_CLIP
-        probe_tags = (args.probe.split(",") if args.probe else ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv1.fwd", "conv1.wgrad", "conv2.fwd", "conv2.dgrad", "conv2.wgrad"])
-        probe_tags += ["frontend.fwd", "frontend.bwd"]
-        workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
-    else:
+        step, fpc, tags, workload = build_envnet_step(args, dev, rank, world, B)
+        tags = args.probe.split(",") if args.probe else tags
+        el, loss, ks = time_leg(step, tags, args, world, dev, args.warmup, args.steps)
+        results["envnet"] = leg_result("envnet", B, world, args.steps, args.warmup, el, loss, ks, fpc, args,
+                                       workload)
+        results["envnet"]["config"]["model"] = "envnet_v2"
+        del step
+        free_leg()
+    if args.model in ("both", "ast"):
         sys.path.insert(0, str(REPO))
-        from bench_ast import build_ast_step  # noqa: E402
-        B = args.batch or 256  # AST at batch 256 on one MI355X (~84 GB of activations)
-        step, flop_per_clip, probe_tags, workload = build_ast_step(args, dev, rank, world, B)
-
-    if world > 1:
-        model_sync = getattr(step, "broadcast", None)
-        if model_sync:
-            model_sync()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    K.PROBE = {t: [] for t in probe_tags}
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    probes = K.PROBE
-    K.PROBE = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    ms = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
-
-    # live per-kernel timing (HIP events on the launch stream) for the roofline
-    kstats = {}
-    for tag, recs in probes.items():
-        if not recs:
-            continue
-        dur = sum(e0.elapsed_time(e1) for e0, e1, _, _ in recs) / len(recs)  # ms per launch
-        flops, byts = recs[0][2], recs[0][3]
-        kstats[tag] = {"ms": dur, "tflops": flops / (dur * 1e-3) / 1e12, "gbs": byts / (dur * 1e-3) / 1e9,
-                       "launches_per_step": len(recs) / args.steps, "flop": flops, "bytes": byts}
-    regions = {k: v for k, v in kstats.items() if k.startswith("frontend.")}
-    kstats = {k: v for k, v in kstats.items() if k not in regions}
-    dom = max(kstats, key=lambda k: kstats[k]["ms"] * kstats[k]["launches_per_step"]) if kstats else None
-    peak_tf = BF16_MFMA_PEAK_TF if args.dtype == "bf16" else F32_PEAK_TF
-    roof = None
-    if dom:
-        ks = kstats[dom]
-        kname = {"attn.fwd": "attn_fwd_kernel", "attn.bwd": "attn_bwd_dkdv_kernel+attn_bwd_dq_kernel",
-                 "t0b.fwd": "conv8_kernel<PRE,STATS>", "t0b.dgrad": "conv8_kernel"}.get(
-            dom, KERNEL_HINT.get(dom, "igemm_kernel"))
-        traffic, tsrc = pmc_traffic(args.model, ks, dom)
-        if tsrc and tsrc.get("kernel"):
-            kname = tsrc["kernel"].replace("_ZN12_GLOBAL__N_1", "").replace("(anonymous namespace)::", "").split("(")[0]
-        roof = {"bound": "mfma", "kernel": f"{kname} [{dom}]", "achieved": round(ks["tflops"], 2),
-                "peak": peak_tf, "unit": "TFLOP/s", "frac": round(ks["tflops"] / peak_tf, 4), "traffic": traffic,
-                "traffic_source": tsrc,
-                "algorithmic_per_launch": {"flop": ks["flop"], "bytes": ks["bytes"]},
-                "ms_per_launch": round(ks["ms"], 4)}
-    step_tf = flop_per_clip * B / (ms * 1e-3) / 1e12
-    out = {
-        "metric": "training clips/sec (EnvNet-v2, ESC-50 shape)" if args.model == "envnet"
-        else "training clips/sec (AST, ESC-50 shape)",
-        "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (peak-normalised 0.1*N(0,1) clips, uniform labels)",
-        "config": {"workload": workload, "model": "envnet_v2" if args.model == "envnet" else "ast",
-                   "global_batch": B * world, "per_gpu_batch": B, "clip_samples": 220_500,
-                   "parallelism": f"dp{world}"},
-        "roofline": roof,
-        "step_tflops": round(step_tf, 2),
-        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                    for k, v in kstats.items()},
-        "frontend_path": frontend_summary(regions, B),
-        "loss": float(loss),
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "envnet":
-        threads = min(16, len(os.sched_getaffinity(0)))
-        out["cpu_baseline"] = cpu_baseline_envnet(threads)
+        from bench_ast import build_ast_step
+        B = args.ast_batch or 256  # SURVEY.md §8(d) config 3: AST at batch 256 on one MI355X
+        step, fpc, tags, workload = build_ast_step(args, dev, rank, world, B)
+        tags = args.probe.split(",") if args.probe else tags
+        el, loss, ks = time_leg(step, tags, args, world, dev, args.warmup, args.steps)
+        results["ast"] = leg_result("ast", B, world, args.steps, args.warmup, el, loss, ks, fpc, args, workload,
+                                    roof_tag="attn.fwd")
+        results["ast"]["config"]["model"] = "ast"
+        del step
+        free_leg()
+    out = results.get("envnet") or results["ast"]
+    if "envnet" in results and "ast" in results:
+        out = dict(results["envnet"])
+        out["ast"] = results["ast"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = len(os.sched_getaffinity(0))
+        if "envnet" in results:
+            b4 = cpu_baseline_envnet(threads, batch=4, steps=8)
+            b16 = cpu_baseline_envnet(threads, batch=16, steps=2)
+            out["cpu_baseline"] = dict(b4, samples=[b4, b16])
+        if "ast" in results:
+            target = out["ast"] if "envnet" in results else out
+            target["cpu_baseline"] = cpu_baseline_ast(threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1,6 +1,6 @@
 """AST leg of bench.py (`python bench.py --model ast`): BASELINE.json configs[2].
 
-One step = on-GPU log-mel of 5 s @ 44.1 kHz clips (1379 frames x 128 mels) -> SpecAugment + Mixup
+Timed by bench.py (the nested "ast" object of the default run).  One step = on-GPU log-mel of 5 s @ 44.1 kHz clips (1379 frames x 128 mels) -> SpecAugment + Mixup
 against the batch -> AST (DeiT-base/384 geometry, 12 blocks, 1645 tokens, random init: no
 checkpoint offline) forward -> soft-label loss (softmax on the sigmoid outputs, as reference
 engine.py:175-176 does with ast.py:64) -> backward -> (N>1: RCCL all-reduce) -> clip 1.0 + Adam.
@@ -45,8 +45,8 @@ def build_ast_step(args, dev, rank, world, B):
         opt.zero_grad(set_to_none=True)
         return loss
 
-    tags = (args.probe.split(",") if args.probe else ["attn.fwd", "attn.bwd", "fc1.fwd", "fc2.fwd", "qkv.fwd",
-                                                      "fc1.wgrad", "fc2.dgrad"])
+    tags = ["attn.fwd", "attn.bwd", "qkv.fwd", "proj.fwd", "fc1.fwd", "fc2.fwd", "qkv.wgrad", "qkv.dgrad",
+            "fc1.wgrad", "fc1.dgrad", "fc2.wgrad", "fc2.dgrad", "logmel.fwd", "optim.step"]
     workload = ("AST train step (log-mel, SpecAugment+Mixup, fwd, soft-CE, bwd, clip, Adam), "
                 "5 s @ 44.1 kHz -> 128x1379 log-mel -> 1645 tokens, DeiT-base/384 geometry")
     return step, AST_FLOP_PER_CLIP, tags, workload

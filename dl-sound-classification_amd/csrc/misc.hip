@@ -342,8 +342,8 @@ __global__ __launch_bounds__(MS_NT) void clip_ms_kernel(const float* __restrict_
 }
 
 __device__ __forceinline__ float spl_db(float ms) {  // BCMixingUtils.a_weighted_spl (preprocessing.py:395-415)
-  const float rms = sqrtf(ms);
-  return rms > 0.f ? 20.f * log10f(rms) + 94.f : -80.f;
+  const float rms = __fsqrt_rn(ms);
+  return rms > 0.f ? __fadd_rn(__fmul_rn(20.f, log10f(rms)), 94.f) : -80.f;
 }
 
 // one thread per clip: ms[b] (own clip) and msq[b] (partner) -> p, soft labels
@@ -357,14 +357,15 @@ __global__ void bc_coef_kernel(const float* __restrict__ ms, const float* __rest
   const float rr = r[b];
   float p = 1.f;
   if (q >= 0) {
-    // perceptual_mixing_coefficient (preprocessing.py:418-446)
-    const float d = spl_db(ms[b]) - spl_db(msq[b]);
-    p = rr;
-    if (fabsf(d) > 10.f) {
-      const float adj = fminf(fabsf(d) / 40.f, 0.3f);
-      p = d > 0.f ? rr * (1.f - adj) : rr * (1.f + adj);
+    // perceptual_mixing_coefficient (preprocessing.py:421-447): f32 SPLs, Python-double arithmetic,
+    // f32 clamp
+    const double d = (double)spl_db(ms[b]) - (double)spl_db(msq[b]);
+    double pd = (double)rr;
+    if (fabs(d) > 10.0) {
+      const double adj = fmin(fabs(d) / 40.0, 0.3);
+      pd = d > 0.0 ? pd * (1.0 - adj) : pd * (1.0 + adj);
     }
-    p = fminf(fmaxf(p, 0.f), 1.f);
+    p = fminf(fmaxf((float)pd, 0.f), 1.f);
   }
   p_out[b] = p;
   if (yout) {
@@ -383,12 +384,89 @@ __global__ void bc_mix_kernel(const float* __restrict__ x, const float* __restri
   const int b = blockIdx.y;
   const int q = partner[b];
   const float p = p_in[b];
-  const float norm = sqrtf(p * p + (1.f - p) * (1.f - p));
+  // mix_waveforms (preprocessing.py:468-471) rounded op by op like the reference: p*x1 and (1-p)*x2
+  // in f32, their sum, then / f32(sqrt(f32(p^2 + (1-p)^2))) with the sum of squares in double
+  const double pd = (double)p;
+  const float norm = __fsqrt_rn((float)(pd * pd + (1.0 - pd) * (1.0 - pd)));
+  const float q1 = 1.f - p;
   const float* xa = x + (int64_t)b * T;
   const float* xb = pool + (int64_t)(q >= 0 ? q : 0) * T;
   float* o = out + (int64_t)b * T;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x)
-    o[i] = q >= 0 ? (p * xa[i] + (1.f - p) * xb[i]) / norm : xa[i];
+    o[i] = q >= 0 ? __fdiv_rn(__fadd_rn(__fmul_rn(p, xa[i]), __fmul_rn(q1, xb[i])), norm) : xa[i];
+}
+
+// Partner draw of apply_bc_mixing (preprocessing.py:584-591): uniform among the pool clips of a
+// different class.  One workgroup per clip: pass 1 counts the n_diff candidates, k = min(floor(u *
+// n_diff), n_diff - 1), pass 2 finds the k-th candidate in pool order with a chunked block scan
+// (ballot + popcount).  Exact (no rejection rounds); -1 when the pool holds no other class.
+constexpr int PT_NT = 256;
+__global__ __launch_bounds__(PT_NT) void bc_partner_kernel(const int64_t* __restrict__ labels,
+                                                           const int64_t* __restrict__ pool_labels, int N,
+                                                           const float* __restrict__ u, int* __restrict__ partner) {
+  __shared__ int wcnt[PT_NT / 64];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t l = labels[b];
+  int ndiff = 0;
+  for (int c = 0; c < N; c += PT_NT) {
+    const int i = c + threadIdx.x;
+    ndiff += __syncthreads_count(i < N && pool_labels[i] != l);
+  }
+  if (ndiff == 0) {
+    if (threadIdx.x == 0) partner[b] = -1;
+    return;
+  }
+  const int k = min((int)floorf(u[b] * (float)ndiff), ndiff - 1);
+  int base = 0;  // candidates before this chunk (uniform across the block)
+  for (int c = 0; c < N; c += PT_NT) {
+    const int i = c + threadIdx.x;
+    const bool f = i < N && pool_labels[i] != l;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int before = base;
+    for (int w = 0; w < wave; ++w) before += wcnt[w];
+    const int rank = before + __popcll(m & ((1ull << lane) - 1ull));
+    if (f && rank == k) partner[b] = i;
+    int tot = 0;
+    for (int w = 0; w < PT_NT / 64; ++w) tot += wcnt[w];
+    base += tot;
+    __syncthreads();
+    if (base > k) break;
+  }
+}
+
+// Time stretch + gain of EnvNetPreprocessor.apply_augmentation (preprocessing.py:886-925): clip b is
+// resampled to m = int(T / factor[b]) samples with torch's linear, align_corners=False rule
+// (src = (T/m)(i + 0.5) - 0.5 clamped at 0, i0 = floor(src), i1 = min(i0 + 1, T - 1)) and scaled by
+// gain[b]; factor <= 0 means no stretch.  The result is written into the T-sample window (stretched
+// clips cropped to T, shortened clips zero-filled past m), so the batch keeps one shape.
+__global__ void stretch_gain_kernel(const float* __restrict__ x, int64_t T, const double* __restrict__ factor,
+                                    const float* __restrict__ gain, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const double fac = factor ? factor[b] : 0.0;
+  const int64_t m = fac > 0.0 ? (int64_t)((double)T / fac) : T;
+  const float g = gain ? gain[b] : 1.f;
+  const float scale = (float)T / (float)m;
+  const float* xr = x + (int64_t)b * T;
+  float* o = out + (int64_t)b * T;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x) {
+    float v;
+    if (i >= m) {
+      v = 0.f;
+    } else if (m == T) {
+      v = xr[i];
+    } else {
+      float src = __fsub_rn(__fmul_rn(scale, (float)i + 0.5f), 0.5f);
+      src = src < 0.f ? 0.f : src;
+      const int64_t i0 = min((int64_t)floorf(src), T - 1);
+      const float l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+      const float l0 = 1.f - l1;
+      const int64_t i1 = i0 + (i0 < T - 1 ? 1 : 0);
+      v = __fadd_rn(__fmul_rn(xr[i0], l0), __fmul_rn(xr[i1], l1));
+    }
+    o[i] = gain ? __fmul_rn(v, g) : v;
+  }
 }
 
 // ------------------------------------------------------------------ SpecAugment + Mixup
@@ -405,7 +483,7 @@ __global__ void specaug_mixup_kernel(const float* __restrict__ spec, const float
     const int t = (int)(i % T), f = (int)(i / T);
     float v = spec[(int64_t)b * per + i];
     if ((t >= ts && t < te) || (f >= fs && f < fe)) v = 0.f;
-    if (q >= 0) v = l * v + (1.f - l) * pool[(int64_t)q * per + i];
+    if (q >= 0) v = __fadd_rn(__fmul_rn(l, v), __fmul_rn(1.f - l, pool[(int64_t)q * per + i]));  // preprocessing.py:961, op by op
     out[(int64_t)b * per + i] = v;
   }
 }
@@ -525,6 +603,23 @@ extern "C" int mia_bc_mix(const float* x, const float* pool, int64_t T, int32_t 
   bc_mix_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 512), B), 256, 0, s>>>(x, pool, T, B, partner, p_out,
                                                                                       out);
   MIA_LAUNCH_CHECK("bc_mix");
+  return 0;
+}
+
+extern "C" int mia_bc_partner(const int64_t* labels, int32_t B, const int64_t* pool_labels, int32_t N, const float* u,
+                              int32_t* partner, mia_stream_t stream) {
+  MIA_CHECK_ARG(labels && pool_labels && u && partner && B > 0 && N > 0, "bc_partner: args");
+  bc_partner_kernel<<<B, PT_NT, 0, as_stream(stream)>>>(labels, pool_labels, N, u, partner);
+  MIA_LAUNCH_CHECK("bc_partner");
+  return 0;
+}
+
+extern "C" int mia_stretch_gain(const float* x, int64_t T, int32_t B, const double* factor, const float* gain,
+                                float* out, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && out && B > 0 && T > 0 && out != x, "stretch_gain: args");
+  stretch_gain_kernel<<<dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 512), B), 256, 0, as_stream(stream)>>>(
+      x, T, factor, gain, out);
+  MIA_LAUNCH_CHECK("stretch_gain");
   return 0;
 }
 

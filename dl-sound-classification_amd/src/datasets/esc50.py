@@ -192,11 +192,20 @@ class ESC50DataModule:
             self._gen = torch.Generator(device=x.device).manual_seed(1234 + self.rank)
         C = self.num_classes
         if not self.is_spectrogram:
+            wav_aug = self.preprocessing_config.get("augment") or {}
+            if training and x.is_cuda and (wav_aug.get("time_stretch") or wav_aug.get("gain_shift")):
+                # EnvNetPreprocessor.apply_augmentation after the crop, before BC mixing (esc50.py:235-245)
+                from .augment import stretch_gain
+                x = stretch_gain(x.reshape(x.shape[0], -1), wav_aug.get("time_stretch"), wav_aug.get("gain_shift"),
+                                 gen=self._gen).view(x.shape[0], 1, -1)
             if training and self.enable_bc_mixing:
-                from .augment import bc_mix
+                from .augment import bc_mix, bc_mix_cpu
                 self._pools()
-                out, ys, _ = bc_mix(x.reshape(x.shape[0], -1), y, C, gen=self._gen, pool=self._pool,
-                                    pool_labels=self._pool_labels)
+                if x.is_cuda:
+                    out, ys, _ = bc_mix(x.reshape(x.shape[0], -1), y, C, gen=self._gen, pool=self._pool,
+                                        pool_labels=self._pool_labels)
+                else:  # trainer.accelerator=cpu (config 1 plumbing) only
+                    out, ys, _ = bc_mix_cpu(x, y, C, self._pool, self._pool_labels)
                 return out.view(x.shape[0], 1, -1), ys
             return x, _one_hot(y, C)
         spec = self.logmel()(x.reshape(x.shape[0], -1))

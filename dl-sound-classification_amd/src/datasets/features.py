@@ -84,8 +84,10 @@ class GpuLogMel:
         t = self.tables(wav.device)
         lib = L.load()
         ws = K.workspace(lib.mia_logmel_workspace_bytes(B, frames), wav.device, "logmel")
-        L.check(lib.mia_logmel_fwd(wav.data_ptr(), B, T, T, self.cfg, t["window"].data_ptr(), t["tw512"].data_ptr(),
-                                   t["tw1024"].data_ptr(), t["band_start"].data_ptr(), t["band_len"].data_ptr(),
-                                   t["band_off"].data_ptr(), t["band_w"].data_ptr(), out.data_ptr(), ws.data_ptr(),
-                                   L.stream_ptr()), "mia_logmel_fwd")
+        # algorithmic HBM bytes: waveform read once + log-mel written once, f32
+        with K.probe("logmel.fwd", 0.0, B * T * 4 + out.numel() * 4):
+            L.check(lib.mia_logmel_fwd(wav.data_ptr(), B, T, T, self.cfg, t["window"].data_ptr(),
+                                       t["tw512"].data_ptr(), t["tw1024"].data_ptr(), t["band_start"].data_ptr(),
+                                       t["band_len"].data_ptr(), t["band_off"].data_ptr(), t["band_w"].data_ptr(),
+                                       out.data_ptr(), ws.data_ptr(), L.stream_ptr()), "mia_logmel_fwd")
         return out

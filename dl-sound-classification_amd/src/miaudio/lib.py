@@ -103,7 +103,9 @@ SIGNATURES = {
     "mia_cast": (C.c_int, [vp, i32, vp, i32, i64, vp]),
     "mia_add_inplace": (C.c_int, [vp, vp, i32, i64, vp]),
     "mia_bc_mix": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
-    "mia_spec_augment_mixup": (C.c_int, [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mia_bc_partner": (C.c_int, [vp, i32, vp, i32, vp, vp, vp]),
+    "mia_stretch_gain": (C.c_int, [vp, i64, i32, vp, vp, vp, vp]),
+    "mia_spec_augment_mixup":(C.c_int, [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mia_last_error_string": (C.c_char_p, []),
     "mia_device_arch": (C.c_int, [C.c_char_p, i32]),
 }

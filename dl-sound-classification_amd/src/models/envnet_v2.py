@@ -4,8 +4,13 @@ Same Hydra target (configs/model/envnet_v2.yaml:10), same constructor kwargs
 (num_classes, dropout), same module tree and parameter names (so state_dicts interchange),
 same default-init -> ``_init_weights`` -> ``replace_head`` order (reference
 src/models/envnet_v2.py:10-90), same forward contract (B,1,T) or (B,1,1,T) -> (B, C) logits.
-The computation runs through the MI355X kernels in ``envnet_hip`` as one autograd node; there
-is no CPU path (inputs on the CPU raise).
+The computation runs through the MI355X kernels in ``envnet_hip`` as one autograd node.
+
+CPU tensors raise, with one explicit exception: BASELINE config 1 ("EnvNet-v2, batch 4,
+Lightning accelerator=cpu", a plumbing run without a GPU) is served by ``_cpu_forward`` — the
+reference's own torch module sequence — which runs ONLY when the Trainer was built with
+``accelerator="cpu"`` (it sets ``cpu_accelerator`` on the model).  It is never a fallback for a GPU
+run, never the oracle, and never what bench.py or the GPU tests measure.
 """
 from __future__ import annotations
 
@@ -44,6 +49,7 @@ class EnvNetV2(nn.Module):
             nn.Linear(4096, num_classes),
         )
         self.compute_dtype = compute_dtype  # None: follow autocast (bf16) else f32
+        self.cpu_accelerator = False        # set by lite.Trainer(accelerator="cpu") only (config 1)
         self._init_weights()
 
     def _init_weights(self):
@@ -71,8 +77,14 @@ class EnvNetV2(nn.Module):
             x = x.unsqueeze(2)
         if x.ndim != 4 or x.shape[1] != 1 or x.shape[2] != 1:
             raise ValueError(f"EnvNetV2 expects (B,1,T) or (B,1,1,T), got {tuple(x.shape)}")
+        if not x.is_cuda and self.cpu_accelerator:
+            return self._cpu_forward(x)
         with torch.autocast("cuda", enabled=False):
             return envnet_forward(self, x, self._compute_code())
+
+    def _cpu_forward(self, x: torch.Tensor) -> torch.Tensor:
+        """accelerator=cpu (config 1 plumbing): envnet_v2.py:80-84 on torch's CPU ops."""
+        return self.classifier(self.trunk(self.frontend(x).transpose(1, 2)))
 
     def replace_head(self, num_classes: int) -> None:
         in_feat = self.classifier[-1].in_features

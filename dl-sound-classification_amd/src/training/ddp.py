@@ -6,9 +6,13 @@ time, per-step fp32 gradient all-reduce averaged over ranks, and ``broadcast_buf
 BatchNorm running statistics (BN itself stays per-rank: no SyncBN, as in the reference).
 
 Gradients are exchanged in buckets on a dedicated communication stream.  Models whose backward
-reports gradients as they become ready (EnvNetV2 does, through ``model._grad_ready``) get their
-buckets launched during the backward, so the transfer of the FC-head gradients (1.4 GB for
-EnvNet) overlaps the convolution backward; everything else is flushed in ``finish()``.
+reports gradients as they become ready (the EnvNetV2 and AST autograd nodes do, through
+``module._grad_ready``) get their buckets launched during the backward, so the transfer of the
+FC-head gradients (1.4 GB for EnvNet) overlaps the convolution backward; everything else is flushed
+in ``finish()``.  The hook is installed on the wrapped module AND every submodule, because the
+drop-in path wraps the LitClassifier while the autograd nodes look for it on the inner model.
+The per-step BatchNorm buffer broadcast (DDP ``broadcast_buffers``) is one coalesced collective per
+dtype.
 """
 from __future__ import annotations
 
@@ -37,7 +41,9 @@ class GradAllReducer:
                 p._mia_bf16_ver = None  # a collective writes behind autograd's version counter: recast
             for b in model.buffers():
                 dist.broadcast(b.data, 0)
-        model._grad_ready = self.grad_ready
+        for m in model.modules():
+            m._grad_ready = self.grad_ready
+        self.fired = self.last_fired = 0  # gradients received through _grad_ready per step (tests)
 
     # ------------------------------------------------------------------ async launches
     def _launch(self, tensors):
@@ -71,6 +77,7 @@ class GradAllReducer:
                 continue
             p.grad = g
             self.done.add(id(p))
+            self.fired += 1
             (big if g.numel() * g.element_size() >= self.bucket_bytes // 4 else small).append(g)
         for g in big:
             self._launch([g])
@@ -100,8 +107,22 @@ class GradAllReducer:
                     off += n
         self.pending.clear()
         self.done.clear()
+        self.last_fired, self.fired = self.fired, 0
         if self.broadcast_buffers:
-            with torch.no_grad():
-                for b in self.model.buffers():
-                    if b.dtype.is_floating_point:
-                        dist.broadcast(b.data, 0)
+            self._broadcast_buffers()
+
+    @torch.no_grad()
+    def _broadcast_buffers(self):
+        """Rank 0's BatchNorm running statistics (+ counters) to every rank: one flat broadcast per
+        dtype instead of one collective per buffer."""
+        groups = {}
+        for b in self.model.buffers():
+            groups.setdefault((b.dtype, b.device), []).append(b)
+        for bufs in groups.values():
+            flat = torch.cat([b.reshape(-1) for b in bufs])
+            dist.broadcast(flat, 0)
+            off = 0
+            for b in bufs:
+                n = b.numel()
+                b.copy_(flat[off:off + n].view_as(b))
+                off += n

@@ -133,13 +133,19 @@ class LitClassifier(LightningModule):
     def configure_optimizers(self):
         params = list(self.parameters())
         target = str(self._optim_cfg.get("_target_", "")) if self._optim_cfg is not None else ""
+        optim = None
         if params and params[0].is_cuda and target in ("torch.optim.Adam", "src.training.optim.FusedAdam"):
             from .optim import FusedAdam
             kw = {k: v for k, v in self._optim_cfg.items() if k != "_target_"}
             clip = getattr(getattr(self, "trainer", None), "gradient_clip_val", 0.0) or 0.0
-            optim = FusedAdam(params, clip=clip, **kw)
-            optim.handles_clipping = True
-        else:
+            try:
+                optim = FusedAdam(params, clip=clip, **kw)
+                optim.handles_clipping = True
+            except ValueError as e:  # an Adam option the fused kernel does not implement
+                if target != "torch.optim.Adam":
+                    raise
+                print(f"[engine] {e}; running torch.optim.Adam", flush=True)
+        if optim is None:
             optim = instantiate(self._optim_cfg, params=params)
         if self._sched_cfg is None:
             return optim

@@ -77,33 +77,55 @@ class ModelCheckpoint:
         self.monitor, self.mode, self.dirpath, self.filename = monitor, mode, dirpath, filename
         self.best_score, self.best_model_path = None, ""
 
+    def state_dict(self):
+        return {"best_score": self.best_score, "best_model_path": self.best_model_path}
+
+    def load_state_dict(self, st):
+        self.best_score, self.best_model_path = st.get("best_score"), st.get("best_model_path", "")
+
     def _better(self, v):
         return self.best_score is None or (v > self.best_score if self.mode == "max" else v < self.best_score)
 
     def on_epoch_end(self, trainer, module, metrics):
-        if self.monitor not in metrics or not trainer.is_global_zero:
+        """Rank 0 writes the checkpoint; every rank learns the new best path (Lightning keeps the
+        callback state in sync the same way), so test(ckpt_path="best") loads it everywhere."""
+        if self.monitor not in metrics:
             return
         v = metrics[self.monitor]
-        if self._better(v):
+        if trainer.world > 1:
+            v = trainer.broadcast_object(v)  # rank 0's metrics decide, as in Lightning
+        if not self._better(v):
+            return
+        if not trainer.is_global_zero:
             self.best_score = v
-            fmt = {k.replace("/", "_"): val for k, val in metrics.items()}
-            fmt["epoch"] = module.current_epoch
-            name = self.filename
-            for k in metrics:
-                name = name.replace("{" + k, "{" + k.replace("/", "_"))
-            name = name.format(**fmt)
-            Path(self.dirpath).mkdir(parents=True, exist_ok=True)
-            path = str(Path(self.dirpath) / f"{name}.ckpt")
-            if self.best_model_path and os.path.exists(self.best_model_path):
-                os.remove(self.best_model_path)
-            trainer.save_checkpoint(path)
-            self.best_model_path = path
+            self.best_model_path = trainer.broadcast_object(None)
+            return
+        fmt = {k.replace("/", "_"): val for k, val in metrics.items()}
+        fmt["epoch"] = module.current_epoch
+        name = self.filename
+        for k in metrics:
+            name = name.replace("{" + k, "{" + k.replace("/", "_"))
+        name = name.format(**fmt)
+        Path(self.dirpath).mkdir(parents=True, exist_ok=True)
+        path = str(Path(self.dirpath) / f"{name}.ckpt")
+        if self.best_model_path and os.path.exists(self.best_model_path):
+            os.remove(self.best_model_path)
+        self.best_score, self.best_model_path = v, path
+        trainer.save_checkpoint(path)
+        if trainer.world > 1:
+            trainer.broadcast_object(path)
 
 
 class EarlyStopping:
     def __init__(self, monitor="val/acc", mode="max", patience=40, min_delta=0.0, **kw):
         self.monitor, self.mode, self.patience, self.min_delta = monitor, mode, patience, min_delta
         self.best, self.wait = None, 0
+
+    def state_dict(self):
+        return {"best": self.best, "wait": self.wait}
+
+    def load_state_dict(self, st):
+        self.best, self.wait = st.get("best"), st.get("wait", 0)
 
     def on_epoch_end(self, trainer, module, metrics):
         if self.monitor not in metrics:
@@ -136,6 +158,7 @@ class Trainer:
         self.max_epochs = int(max_epochs)
         self.gradient_clip_val = float(gradient_clip_val or 0.0)
         self.precision = str(precision)
+        self.compute_dtype = self._compute_dtype(self.precision)
         self.devices = devices
         self.log_every_n_steps = log_every_n_steps
         self.logger = logger
@@ -163,6 +186,28 @@ class Trainer:
         self.datamodule = None
 
     # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _compute_dtype(precision: str) -> str:
+        """Lightning precision string -> kernel compute dtype.  fp16 ("16-mixed", the reference's AST
+        suggestion) maps to bf16: same MFMA rate on MI355X, f32 exponent range, no loss scaling."""
+        p = precision.lower()
+        if p in ("32", "32-true", "highest", "high", "medium"):
+            return "f32"
+        if p in ("bf16", "bf16-mixed", "bf16-true"):
+            return "bf16"
+        if p in ("16", "16-mixed", "16-true"):
+            print(f"[lite] precision={precision!r}: fp16 runs as bf16 compute (f32 master weights, no loss "
+                  "scaling needed) on the MI355X kernels", flush=True)
+            return "bf16"
+        raise ValueError(f"unsupported trainer.precision {precision!r} (use 32, bf16-mixed or 16-mixed)")
+
+    def broadcast_object(self, obj):
+        if self.world <= 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
     def _prepare(self, module, datamodule):
         self.datamodule = datamodule
         module.trainer = self
@@ -171,10 +216,12 @@ class Trainer:
         if hasattr(datamodule, "attach"):
             datamodule.attach(self.device, self.world, self.rank)
         module.to(self.device)
-        cd = "bf16" if "bf16" in self.precision else "f32"
+        cd = self.compute_dtype
         for m in module.modules():
             if hasattr(m, "compute_dtype"):
                 m.compute_dtype = cd
+            if hasattr(m, "cpu_accelerator"):  # EnvNetV2: accelerator=cpu plumbing runs (config 1)
+                m.cpu_accelerator = self.device.type == "cpu"
 
     def _limit(self, stage, n):
         lim = self.limits[stage]
@@ -186,6 +233,9 @@ class Trainer:
         m = self._module
         torch.save({"state_dict": m.state_dict(), "epoch": m.current_epoch, "global_step": m.global_step,
                     "optimizer_states": [self.optimizer.state_dict()] if self.optimizer else [],
+                    "lr_schedulers": [self.scheduler.state_dict()] if self.scheduler is not None else [],
+                    "callbacks": {type(cb).__name__: cb.state_dict() for cb in self.callbacks
+                                  if hasattr(cb, "state_dict")},
                     "hyper_parameters": m.hparams}, path)
 
     def _load(self, module, path):
@@ -219,9 +269,18 @@ class Trainer:
             self.optimizer = opt_cfg
         start_epoch = 0
         if ckpt_path:
+            # full resume (Lightning fit(ckpt_path=...)): weights, optimizer, LR scheduler, callback
+            # state (best score / patience) and the step / epoch counters
             ck = self._load(module, ckpt_path)
             if ck.get("optimizer_states"):
                 self.optimizer.load_state_dict(ck["optimizer_states"][0])
+            if ck.get("lr_schedulers") and self.scheduler is not None:
+                self.scheduler.load_state_dict(ck["lr_schedulers"][0])
+            for cb in self.callbacks:
+                st = ck.get("callbacks", {}).get(type(cb).__name__)
+                if st is not None and hasattr(cb, "load_state_dict"):
+                    cb.load_state_dict(st)
+            module.global_step = int(ck.get("global_step", 0))
             start_epoch = ck.get("epoch", -1) + 1
         if self.world > 1:
             from .ddp import GradAllReducer
@@ -235,6 +294,9 @@ class Trainer:
             loader = datamodule.train_dataloader()
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(epoch)
+            sampler = getattr(loader, "sampler", None)
+            if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new shard order every epoch
+                sampler.set_epoch(epoch)
             n = self._limit("train", len(loader))
             for i, batch in enumerate(loader):
                 if i >= n:
@@ -282,6 +344,9 @@ class Trainer:
         self._prepare(module, datamodule)
         if ckpt_path == "best":
             best = next((cb.best_model_path for cb in self.callbacks if isinstance(cb, ModelCheckpoint)), "")
+            best = self.broadcast_object(best)
+            if self.world > 1:
+                dist.barrier()  # rank 0 finished writing it
             if best and os.path.exists(best):
                 self._load(module, best)
         elif ckpt_path:

@@ -1,7 +1,9 @@
-"""Epoch metrics used by LitClassifier (the torchmetrics MulticlassAccuracy / F1 / AUROC /
+"""Epoch metrics used by LitClassifier (the torchmetrics 1.7 MulticlassAccuracy / F1 / AUROC /
 ConfusionMatrix / per-class accuracy of reference engine.py:104-111; torchmetrics is not installed).
-States are small device tensors; ``compute()`` all-reduces them across data-parallel ranks
-(torchmetrics syncs at compute the same way)."""
+States are small device tensors; ``compute()`` all-reduces (AUROC: all-gathers) them across
+data-parallel ranks, as torchmetrics syncs at compute.  Macro averages weight a class in when
+tp + fp + fn > 0 (torchmetrics ``_adjust_weights_safe_divide``): a class never present but predicted
+counts with score 0, a class neither present nor predicted is left out."""
 from __future__ import annotations
 
 import torch
@@ -35,15 +37,18 @@ class _Confusion:
         return _sync(self.cm)
 
 
+def _macro(score: torch.Tensor, cm: torch.Tensor) -> torch.Tensor:
+    tp = cm.diag()
+    w = ((cm.sum(0) + cm.sum(1) - tp) > 0).double()  # tp + fp + fn > 0
+    return ((score * w).sum() / w.sum()).float() if w.sum() > 0 else score.sum().float() * 0
+
+
 class Accuracy(_Confusion):
-    """MulticlassAccuracy with torchmetrics' default average='macro' over classes present."""
+    """MulticlassAccuracy, average='macro' (per-class recall, torchmetrics class weighting)."""
 
     def compute(self):
         cm = self.confusion().double()
-        support = cm.sum(1)
-        per = torch.where(support > 0, cm.diag() / support.clamp_min(1), torch.zeros_like(support))
-        present = support > 0
-        return (per[present].mean() if present.any() else per.sum() * 0).float()
+        return _macro(cm.diag() / cm.sum(1).clamp_min(1), cm)
 
 
 class ClassAccuracy(_Confusion):
@@ -61,14 +66,27 @@ class F1Macro(_Confusion):
     def compute(self):
         cm = self.confusion().double()
         tp = cm.diag()
-        prec = tp / cm.sum(0).clamp_min(1)
-        rec = tp / cm.sum(1).clamp_min(1)
-        f1 = torch.where(prec + rec > 0, 2 * prec * rec / (prec + rec), torch.zeros_like(tp))
-        return f1.mean().float()
+        denom = 2 * tp + (cm.sum(0) - tp) + (cm.sum(1) - tp)  # 2tp + fp + fn
+        return _macro(torch.where(denom > 0, 2 * tp / denom.clamp_min(1), torch.zeros_like(tp)), cm)
+
+
+def _avg_ranks(v: torch.Tensor) -> torch.Tensor:
+    """1-based ranks with ties sharing their average rank (Mann-Whitney form of the ROC area)."""
+    order = v.argsort()
+    sv = v[order]
+    _, inv, counts = torch.unique_consecutive(sv, return_inverse=True, return_counts=True)
+    ends = counts.cumsum(0).double()
+    avg = ends - (counts.double() - 1) / 2
+    ranks = torch.empty(v.numel(), dtype=torch.float64)
+    ranks[order] = avg[inv]
+    return ranks
 
 
 class AUROC:
-    """Macro one-vs-rest AUROC from softmax scores (rank statistic), accumulated on the host."""
+    """MulticlassAUROC, average='macro', one-vs-rest.  Scores are softmaxed per update unless already in
+    [0, 1] (torchmetrics' rule: AST's sigmoid outputs are used as they are); classes without positives
+    are left out; ties get average ranks (= the trapezoidal ROC area).  Scores are gathered from every
+    rank at compute()."""
 
     def __init__(self, num_classes: int):
         self.C = num_classes
@@ -78,21 +96,26 @@ class AUROC:
         self.scores, self.targets = [], []
 
     def update(self, logits, target):
-        self.scores.append(torch.softmax(logits.detach().float(), dim=1).cpu())
+        s = logits.detach().float()
+        if not bool(((s >= 0) & (s <= 1)).all()):
+            s = torch.softmax(s, dim=1)
+        self.scores.append(s.cpu())
         self.targets.append(target.detach().long().cpu())
 
     def compute(self):
-        if not self.scores:
-            return torch.tensor(0.0)
-        s = torch.cat(self.scores)
-        t = torch.cat(self.targets)
+        s = torch.cat(self.scores) if self.scores else torch.zeros(0, self.C)
+        t = torch.cat(self.targets) if self.targets else torch.zeros(0, dtype=torch.long)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            parts = [None] * dist.get_world_size()
+            dist.all_gather_object(parts, (s, t))
+            s = torch.cat([p[0] for p in parts])
+            t = torch.cat([p[1] for p in parts])
         aucs = []
         for c in range(self.C):
             pos = t == c
             npos, nneg = int(pos.sum()), int((~pos).sum())
             if npos == 0 or nneg == 0:
                 continue
-            ranks = torch.empty_like(s[:, c])
-            ranks[s[:, c].argsort()] = torch.arange(1, len(t) + 1, dtype=ranks.dtype)
-            aucs.append((ranks[pos].sum() - npos * (npos + 1) / 2) / (npos * nneg))
-        return torch.stack(aucs).mean() if aucs else torch.tensor(0.0)
+            r = _avg_ranks(s[:, c].double())
+            aucs.append((r[pos].sum() - npos * (npos + 1) / 2) / (npos * nneg))
+        return torch.stack(aucs).mean().float() if aucs else torch.tensor(0.0)

@@ -16,8 +16,21 @@ from ..miaudio import lib as L
 
 
 class FusedAdam(torch.optim.Optimizer):
+    # torch.optim.Adam options the fused kernel implements only at their defaults
+    _DEFAULT_ONLY = {"amsgrad": False, "maximize": False, "capturable": False, "differentiable": False,
+                     "decoupled_weight_decay": False}
+    _IGNORED = ("foreach", "fused")  # implementation selectors of torch's Adam: this is the fused one
+
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, clip: float = 0.0, **unused):
+                 weight_decay: float = 0.0, clip: float = 0.0, **kw):
+        for k, v in kw.items():
+            if k in self._IGNORED:
+                continue
+            if k not in self._DEFAULT_ONLY:
+                raise TypeError(f"FusedAdam got an unexpected keyword argument {k!r}")
+            if bool(v) != self._DEFAULT_ONLY[k]:
+                raise ValueError(f"FusedAdam implements torch.optim.Adam with {k}={self._DEFAULT_ONLY[k]} only "
+                                 f"(got {k}={v}); use torch.optim.Adam for this option")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.clip = float(clip or 0.0)
@@ -61,12 +74,17 @@ class FusedAdam(torch.optim.Optimizer):
         ws = K.workspace(lib.mia_adam_workspace_bytes(n), dev, "adam")
         tot = torch.empty(1, dtype=torch.float32, device=dev)
         b1, b2 = grp["betas"]
-        L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
-                                  table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
-                                  max(p.numel() for p in ps),
-                                  float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
-                                  float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
-                                  L.stream_ptr()), "mia_clip_adam")
+        # algorithmic HBM bytes: grad read by the norm pass (4 B/param) + Adam's p, g, m, v read and
+        # p, m, v written (28 B/param) + the bf16 operand copies rewritten (2 B/param where shadowed)
+        nel = sum(p.numel() for p in ps)
+        nbytes = 32 * nel + 2 * sum(p.numel() for p, sh in zip(ps, shadows) if sh is not None)
+        with K.probe("optim.step", 0.0, nbytes):
+            L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
+                                      table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
+                                      max(p.numel() for p in ps),
+                                      float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+                                      float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
+                                      L.stream_ptr()), "mia_clip_adam")
         self.last_total_norm = tot
         for p, sh in zip(ps, shadows):
             if sh is not None:

@@ -397,6 +397,18 @@ int mia_bc_mix(const float* x, const float* pool, int64_t T, int32_t B, const in
                const float* r, const int64_t* labels, const int64_t* pool_labels,
                int32_t num_classes, float* out, float* yout, float* p_out, void* workspace,
                mia_stream_t stream);
+/* BC-mixing partner draw (apply_bc_mixing's random.choice over different-class clips,
+ * preprocessing.py:584-591): partner[b] = the k-th pool clip (pool order) whose label differs
+ * from labels[b], k = min(floor(u[b] * n_diff), n_diff - 1); -1 when the pool has no other class
+ * (the reference then returns the clip unmixed with a one-hot label, :585-588). */
+int mia_bc_partner(const int64_t* labels, int32_t B, const int64_t* pool_labels, int32_t N,
+                   const float* u, int32_t* partner, mia_stream_t stream);
+/* Time stretch + gain (EnvNetPreprocessor.apply_augmentation, preprocessing.py:886-925) of a
+ * (B, T) batch: clip b resampled to int(T / factor[b]) samples with F.interpolate's linear,
+ * align_corners=False rule (factor <= 0: unchanged), times gain[b]; written into the T-sample
+ * window (cropped past T, zero past the stretched length).  factor (f64) / gain (f32) may be NULL. */
+int mia_stretch_gain(const float* x, int64_t T, int32_t B, const double* factor, const float* gain,
+                     float* out, mia_stream_t stream);
 /* SpecAugment zero masks then Mixup with an un-augmented partner from `pool`
  * (preprocessing.py:1075-1104, esc50.py:52-76) on (B, F, T) spectrograms; masks and partners
  * (partner < 0: no mixup) drawn by the caller. */

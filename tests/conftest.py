@@ -30,6 +30,12 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_aug():
+    import numpy as np
+    return dict(np.load(REPO / "tests" / "golden" / "golden_aug.npz", allow_pickle=False))
+
+
+@pytest.fixture(scope="session")
 def cuda():
     import torch
     if not torch.cuda.is_available():

@@ -2,7 +2,8 @@
 """Generate the golden parity fixtures by running the REFERENCE's own Python here.
 
 Run in this container only (the reference is not present on the GPU box):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py        # golden.npz
+    python tests/golden/make_golden.py aug    # golden_aug.npz (augmentations + pad/crop)
 
 What runs from /root/reference (imported as-is, never copied):
   * src/models/envnet_v2.py::EnvNetV2                    (needs only torch)
@@ -10,6 +11,9 @@ What runs from /root/reference (imported as-is, never copied):
         through tests/golden/_stubs/torchaudio (restates torchaudio 2.7.1)
   * src/models/ast.py::ASTModel through tests/golden/_stubs/timm (restates timm 1.0.16,
         synthetic weights because the pretrained DeiT checkpoint needs the network)
+  * src/datasets/preprocessing.py::BCMixingDataset, ASTPreprocessor.apply_specaugment,
+        EnvNetPreprocessor.apply_augmentation, and src/datasets/esc50.py::MixupDataset /
+        ESC50Dataset (through a two-line lightning stub), with Python's `random` seeded per case
 Inputs/weights come from oracle/synth.py (splitmix64 counters) so the GPU tests can
 regenerate them bit-identically; only outputs and checksums are committed.
 The script also cross-checks oracle/ against these outputs and prints the errors.
@@ -197,7 +201,108 @@ def golden_bcmix(out):
     out["bcmix_soft_label"] = lab
 
 
+# --------------------------------------------------------------------------- augmentations + batch source
+def golden_aug(out):
+    """BC mixing, SpecAugment, Mixup, time-stretch/gain and the EnvNet pad + crop, each run through
+    the reference's own classes with Python's `random` (and torch's generator for Beta) seeded per
+    case; the oracle (oracle/augment.py) replays the same draws and must reproduce every output."""
+    import tempfile
+
+    from src.datasets.esc50 import ESC50Dataset, MixupDataset
+    from src.datasets.preprocessing import (ASTPreprocessor, BCMixingDataset, EnvNetPreprocessor,
+                                            PreprocessingConfig)
+    from oracle import augment as oaug
+    from tests._aug_inputs import (AUG_BC_LABELS, AUG_MIX_LABELS, AUG_SPEC_CASES, AUG_STRETCH_CFG,
+                                   aug_bc_pool, aug_crop_clip, aug_mix_pool, aug_spec_input,
+                                   aug_stretch_input)
+    # BC mixing through BCMixingDataset.apply_bc_mixing (preprocessing.py:564-609)
+    pool = [torch.from_numpy(w) for w in aug_bc_pool()]
+    data = list(zip(pool, AUG_BC_LABELS))
+    bc = BCMixingDataset(enable_bc_mixing=True, num_classes=4)
+    for s in range(8):
+        i = s % len(pool)
+        random.seed(1000 + s)
+        mixed, y = bc.apply_bc_mixing(pool[i], AUG_BC_LABELS[i], data)
+        pack(f"aug_bc{s}", checksum(mixed.numpy(), 64), out)
+        out[f"aug_bc{s}__y"] = y.numpy()
+        m2, y2, q, r, p = oaug.apply_bc_mixing(pool[i], AUG_BC_LABELS[i], pool, list(AUG_BC_LABELS), 4,
+                                               random.Random(1000 + s))
+        print(f"[aug] bc{s}: partner {q} r {r:.4f} p {p:.4f} oracle err {np.abs(m2.numpy() - mixed.numpy()).max():.3g}")
+        assert torch.equal(y, y2)
+    random.seed(1099)
+    mixed, y = bc.apply_bc_mixing(pool[0], 0, [(pool[1], 0), (pool[0], 0)])  # no other class: unchanged, one-hot
+    out["aug_bc_sameclass__y"] = y.numpy()
+    out["aug_bc_sameclass__equal"] = np.array(torch.equal(mixed, pool[0]))
+    # SpecAugment (preprocessing.py:1075-1104)
+    pre = ASTPreprocessor(PreprocessingConfig(sample_rate=44100, n_mels=128))
+    for s, (shape, tm, fm) in enumerate(AUG_SPEC_CASES):
+        spec = torch.from_numpy(aug_spec_input(s))
+        random.seed(2000 + s)
+        o = pre.apply_specaugment(spec, time_mask=tm, freq_mask=fm).numpy()
+        pack(f"aug_spec{s}", checksum(o, 64), out)
+        out[f"aug_spec{s}__zeros"] = np.array((o == 0).sum())
+        o2, prm = oaug.specaugment(spec, tm, fm, random.Random(2000 + s))
+        print(f"[aug] spec{s}: {prm} oracle equal {np.array_equal(o2.numpy(), o)}")
+        assert np.array_equal(o2.numpy(), o)
+    # Mixup: MixupDataset.apply_mixup (esc50.py:52-76) -> MixupAugmentation (preprocessing.py:935-968)
+    mpool = [torch.from_numpy(x) for x in aug_mix_pool()]
+    mdata = list(zip(mpool, AUG_MIX_LABELS))
+    md = MixupDataset(enable_mixup=True, mixup_alpha=0.5, num_classes=10)
+    for s in range(12):
+        i = s % len(mpool)
+        random.seed(3000 + s)
+        torch.manual_seed(3000 + s)
+        o, y = md.apply_mixup(mpool[i], AUG_MIX_LABELS[i], mdata)
+        pack(f"aug_mix{s}", checksum(o.numpy(), 64), out)
+        out[f"aug_mix{s}__y"] = y.numpy()
+        torch.manual_seed(3000 + s)
+        o2, y2, q, lam = oaug.apply_mixup(mpool[i], AUG_MIX_LABELS[i], mpool, list(AUG_MIX_LABELS), 10, 0.5,
+                                          random.Random(3000 + s))
+        print(f"[aug] mix{s}: partner {q} lam {lam} oracle equal {torch.equal(o, o2) and torch.equal(y, y2)}")
+        assert torch.equal(o, o2) and torch.equal(y, y2)
+    # time stretch + gain (EnvNetPreprocessor.apply_augmentation, preprocessing.py:886-925)
+    ep = EnvNetPreprocessor(PreprocessingConfig(sample_rate=44100, window_length=0.5, augment=AUG_STRETCH_CFG))
+    w = torch.from_numpy(aug_stretch_input())
+    for s in range(10):
+        random.seed(4000 + s)
+        o = ep.apply_augmentation(w).numpy()
+        out[f"aug_tsg{s}__len"] = np.array(o.shape[-1])
+        pack(f"aug_tsg{s}", checksum(o, 64), out)
+        o2, fac, gain = oaug.apply_augmentation(w, AUG_STRETCH_CFG, random.Random(4000 + s))
+        print(f"[aug] tsg{s}: factor {fac} gain {gain} len {o.shape[-1]} oracle err "
+              f"{np.abs(o2.numpy() - o).max() if o2.shape == o.shape else 'shape'}")
+        assert o2.shape == o.shape and np.abs(o2.numpy() - o).max() == 0
+    # ESC50Dataset pad + crop (esc50.py:198-249, preprocessing.py:814-855), envnet_v2 mode, no BC mixing
+    with tempfile.TemporaryDirectory() as td:
+        root = Path(td) / "esc50"
+        (root / "fold_0").mkdir(parents=True)
+        files = []
+        for i in range(3):
+            f = root / "fold_0" / f"clip{i}.pt"
+            torch.save({"waveform": torch.from_numpy(aug_crop_clip(i)), "label": i}, f)
+            files.append(f)
+        pc = {"window_length": 0.5, "padding_ratio": 0.5}
+        for training in (True, False):
+            ds = ESC50Dataset(root=root, files=files, preprocessing_mode="envnet_v2", preprocessing_config=pc,
+                              enable_bc_mixing=False, num_classes=3, training=training)
+            for s in range(6 if training else 3):
+                random.seed(5000 + s)
+                x, y = ds[s % 3]
+                tag = f"aug_crop{'T' if training else 'E'}{s}"
+                pack(tag, checksum(x.numpy(), 64), out)
+                out[f"{tag}__shape"] = np.array(x.shape)
+                out[f"{tag}__y"] = y.numpy()
+
+
 def main():
+    only = sys.argv[1:]
+    if only == ["aug"]:
+        out = {}
+        golden_aug(out)
+        dst = HERE / "golden_aug.npz"
+        np.savez_compressed(dst, **out)
+        print(f"wrote {dst} ({dst.stat().st_size / 1e6:.2f} MB, {len(out)} arrays)")
+        return
     random.seed(0)
     out = {}
     golden_logmel(out)
