@@ -42,6 +42,14 @@ AST_FLOP_PER_CLIP = 1139.7e9
 HBM_TAGS = {"optim.step", "logmel.fwd", "conv1.fwd", "conv1.wgrad"}
 
 
+T_START = time.time()
+
+
+def log(msg):
+    """Progress on stderr (a long silent run looks hung to the GPU harness)."""
+    print(f"[bench {time.time() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +123,26 @@ def frontend_summary(regions: dict, B: int):
     return {"bytes_per_clip": byts // B, "ms_fwd": round(f["ms"], 4), "ms_bwd": round(b["ms"], 4),
             "achieved_gbs": round(byts / (ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
             "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def cpu_threads() -> tuple[int, str]:
+    """Threads for the CPU baseline: every core this process may run on — the affinity set, capped by
+    the cgroup CPU quota (a GPU box's share of a large host: affinity shows all 256 host threads while
+    the quota grants 16, and 256 threads on 16 CPUs run 20x slower than 16)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None and quota < aff:
+        return quota, f"cgroup cpu.max quota {quota} of {aff} affinity CPUs"
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and 0 < int(env) < aff:
+        return int(env), f"OMP_NUM_THREADS={env} of {aff} affinity CPUs"
+    return aff, f"all {aff} affinity CPUs"
 
 
 def cpu_model() -> str:
@@ -199,6 +227,7 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    log("warm-up done, timing")
     K.PROBE = {t: [] for t in probe_tags}
     if world > 1:
         dist.barrier()
@@ -293,8 +322,9 @@ def cpu_baseline_envnet(threads: int, batch: int, steps: int):
 
     one()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         one()
+        log(f"  cpu EnvNet B={batch} step {i + 1}/{steps}")
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
             "sample": f"oracle EnvNet-v2 f32 train step (BC-mix, fwd, loss, bwd, clip, Adam), batch {batch}, "
@@ -339,8 +369,9 @@ def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 3):
 
     one()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         one()
+        log(f"  cpu AST B={batch} step {i + 1}/{steps}")
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
             "sample": f"oracle AST f32 train step (log-mel, SpecAugment+Mixup, fwd, loss, bwd, clip, Adam), "
@@ -363,6 +394,7 @@ def main():
     torch.cuda.set_device(dev)
     results = {}
     if args.model in ("both", "envnet"):
+        log("EnvNet-v2 leg: building")
         B = args.batch or 256
         step, fpc, tags, workload = build_envnet_step(args, dev, rank, world, B)
         tags = args.probe.split(",") if args.probe else tags
@@ -370,11 +402,13 @@ def main():
         results["envnet"] = leg_result("envnet", B, world, args.steps, args.warmup, el, loss, ks, fpc, args,
                                        workload)
         results["envnet"]["config"]["model"] = "envnet_v2"
+        log(f"EnvNet-v2: {results['envnet']['value']} clips/s")
         del step
         free_leg()
     if args.model in ("both", "ast"):
         sys.path.insert(0, str(REPO))
         from bench_ast import build_ast_step
+        log("AST leg: building")
         B = args.ast_batch or 256  # AST at batch 256 on one MI355X
         step, fpc, tags, workload = build_ast_step(args, dev, rank, world, B)
         tags = args.probe.split(",") if args.probe else tags
@@ -382,6 +416,7 @@ def main():
         results["ast"] = leg_result("ast", B, world, args.steps, args.warmup, el, loss, ks, fpc, args, workload,
                                     roof_tag="attn.fwd")
         results["ast"]["config"]["model"] = "ast"
+        log(f"AST: {results['ast']['value']} clips/s")
         del step
         free_leg()
     out = results.get("envnet") or results["ast"]
@@ -389,14 +424,19 @@ def main():
         out = dict(results["envnet"])
         out["ast"] = results["ast"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = len(os.sched_getaffinity(0))
+        threads, why = cpu_threads()
+        log(f"CPU baseline threads: {threads} ({why})")
         if "envnet" in results:
+            log(f"CPU baseline EnvNet-v2 B=4 on {threads} threads")
             b4 = cpu_baseline_envnet(threads, batch=4, steps=8)
+            log(f"CPU baseline EnvNet-v2 B=16: B=4 gave {b4['value']} clips/s")
             b16 = cpu_baseline_envnet(threads, batch=16, steps=2)
-            out["cpu_baseline"] = dict(b4, samples=[b4, b16])
+            out["cpu_baseline"] = dict(b4, samples=[b4, b16], threads_rule=why)
         if "ast" in results:
             target = out["ast"] if "envnet" in results else out
-            target["cpu_baseline"] = cpu_baseline_ast(threads)
+            log("CPU baseline AST B=2")
+            target["cpu_baseline"] = dict(cpu_baseline_ast(threads), threads_rule=why)
+        log("CPU baselines done")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

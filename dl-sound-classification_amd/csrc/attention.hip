@@ -128,21 +128,41 @@ __device__ __forceinline__ float half_exchange_sum(float x) {
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 // ------------------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                       float* __restrict__ lse, int N, int H, float scale_log2) {
+// XCD-aware block order: consecutive work items (the query blocks of one (b, h), which stream the
+// same K/V) land on ONE XCD so K/V come from that XCD's L2, not from HBM once per XCD.  Blocks are
+// dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so slot s of XCD x
+// takes work item x * (total / 8) + s.  Pure speed mapping: any placement gives the same result.
+__device__ __forceinline__ int xcd_work_item(int L, int total) {
+  return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+}
+
+// Each wave owns 64 queries as two 32-query groups sharing every K / V fragment read from LDS (one
+// LDS fragment feeds 2 MFMAs); 4 waves = 256 queries per block; 64-key tiles double-buffered in LDS
+// with the next tile's global loads in flight under the current tile's MFMAs.
+constexpr int FWD_Q = 256;
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                       float* __restrict__ lse, int N, int H, int nqb,
+                                                       float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);
+  const int bh = w / nqb, qb = w - bh * nqb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const int q = blockIdx.x * 128 + wave * 32 + (lane & 31);
-  const bool qvalid = q < N;
-  bf16x8 qf[4];
+  const int q0 = qb * FWD_Q + wave * 64;
+  const bool active = q0 < N;  // wave-uniform: a wave past the last query only helps staging
+  bf16x8 qf[2][4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qvalid);
-  f32x16 o0 = zero16(), o1 = zero16();
-  float m = -INFINITY, l = 0.f;  // m: running max of the log2-scaled scores
+  for (int g = 0; g < 2; ++g) {
+    const int q = q0 + 32 * g + (lane & 31);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[g][ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
+  }
+  f32x16 o[2][2];  // [d half][query group]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { o[i][0] = zero16(); o[i][1] = zero16(); }
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};  // m: running max of the log2-scaled scores
   const int ntiles = (N + 63) / 64;
   Stage64 kreg, vreg;
   kreg.load(base + H * D, ldt, N, t);
@@ -152,84 +172,99 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * 64;
-    const bool more = kt + 1 < ntiles;
-    if (more) {
-      kreg.load(base + (int64_t)(k0 + 64) * ldt + H * D, ldt, N - k0 - 64, t);
-      vreg.load(base + (int64_t)(k0 + 64) * ldt + 2 * H * D, ldt, N - k0 - 64, t);
-    }
-    const bf16* K_ = Ks[kt & 1];
-    const bf16* V_ = Vs[kt & 1];
-    const bool tail = k0 + 64 > N;
-    // both 32-key halves of the tile first (8 MFMAs), then ONE max / rescale decision per 64 keys
-    f32x16 s0 = zero16(), s1 = zero16();
+    // next tile's loads in flight under this tile's MFMAs (the last iteration re-reads the last
+    // tile into the idle buffer: unconditional, so the staging registers stay in VGPRs)
+    const int kn = min(k0 + 64, (ntiles - 1) * 64);
+    kreg.load(base + (int64_t)kn * ldt + H * D, ldt, N - kn, t);
+    vreg.load(base + (int64_t)kn * ldt + 2 * H * D, ldt, N - kn, t);
+    if (active) {
+      const bf16* K_ = Ks[kt & 1];
+      const bf16* V_ = Vs[kt & 1];
+      const bool tail = k0 + 64 > N;
+      // S^T = K . Q^T for both key halves x both query groups: 16 MFMAs, 8 K fragments
+      f32x16 s[2][2];  // [key half][query group]
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      s0 = mfma(frag_row(K_, lane & 31, ks, lane), qf[ks], s0);
-      s1 = mfma(frag_row(K_, 32 + (lane & 31), ks, lane), qf[ks], s1);
-    }
-    if (tail) {
+      for (int kh = 0; kh < 2; ++kh) { s[kh][0] = zero16(); s[kh][1] = zero16(); }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (k0 + acc_row(r, lane) >= N) s0[r] = -INFINITY;
-        if (k0 + 32 + acc_row(r, lane) >= N) s1[r] = -INFINITY;
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const bf16x8 kf = frag_row(K_, 32 * kh + (lane & 31), ks, lane);
+          s[kh][0] = mfma(kf, qf[0][ks], s[kh][0]);
+          s[kh][1] = mfma(kf, qf[1][ks], s[kh][1]);
+        }
+      }
+      bf16x8 pf[2][4];  // [query group][16-key chunk]
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        if (tail) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (k0 + acc_row(r, lane) >= N) s[0][g][r] = -INFINITY;
+            if (k0 + 32 + acc_row(r, lane) >= N) s[1][g][r] = -INFINITY;
+          }
+        }
+        float mx = max3(s[0][g][0], s[1][g][0], s[0][g][1]);
+#pragma unroll
+        for (int r = 1; r < 15; ++r) mx = max3(mx, s[1][g][r], s[0][g][r + 1]);
+        mx = max3(mx, s[1][g][15], s[1][g][15]);
+        mx = half_exchange_max(mx) * scale_log2;
+        const float mn = fmaxf(m[g], mx);
+        // rescale O only when some lane's running max moved (wave-uniform branch)
+        if (__any(mn > m[g])) {
+          const float alpha = m[g] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[g] - mn);
+          l[g] *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) { o[0][g][r] *= alpha; o[1][g][r] *= alpha; }
+        }
+        m[g] = mn;
+        const float nm = mn == -INFINITY ? 0.f : -mn;
+        float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[0][g][r] = __builtin_amdgcn_exp2f(fmaf(s[0][g][r], scale_log2, nm));
+          s[1][g][r] = __builtin_amdgcn_exp2f(fmaf(s[1][g][r], scale_log2, nm));
+          l0 += s[0][g][r];
+          l1 += s[1][g][r];
+        }
+        l[g] += l0 + l1;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pf[g][c] = acc_frag(s[c >> 1][g], c & 1);
+      }
+      // O^T += V^T . P^T: 16 MFMAs, 8 transposed V fragments each feeding both query groups
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const bf16x8 vf = frag_tr(V_, 16 * c, 32 * dh, lane);
+          o[dh][0] = mfma(vf, pf[0][c], o[dh][0]);
+          o[dh][1] = mfma(vf, pf[1][c], o[dh][1]);
+        }
       }
     }
-    float mx = max3(s0[0], s1[0], s0[1]);
-#pragma unroll
-    for (int r = 1; r < 15; ++r) mx = max3(mx, s1[r], s0[r + 1]);
-    mx = max3(mx, s1[15], s1[15]);
-    mx = half_exchange_max(mx) * scale_log2;
-    const float mn = fmaxf(m, mx);
-    // rescale O only when some lane's running max moved (wave-uniform branch)
-    if (__any(mn > m)) {
-      const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mn);
-      l *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-    }
-    m = mn;
-    const float nm = mn == -INFINITY ? 0.f : -mn;
-    float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, nm));
-      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, nm));
-      l0 += s0[r];
-      l1 += s1[r];
-    }
-    l += l0 + l1;
-#pragma unroll
-    for (int sk = 0; sk < 2; ++sk) {
-      const bf16x8 pf = acc_frag(s0, sk);
-      o0 = mfma(frag_tr(V_, 16 * sk, 0, lane), pf, o0);
-      o1 = mfma(frag_tr(V_, 16 * sk, 32, lane), pf, o1);
-    }
-#pragma unroll
-    for (int sk = 0; sk < 2; ++sk) {
-      const bf16x8 pf = acc_frag(s1, sk);
-      o0 = mfma(frag_tr(V_, 32 + 16 * sk, 0, lane), pf, o0);
-      o1 = mfma(frag_tr(V_, 32 + 16 * sk, 32, lane), pf, o1);
-    }
-    if (more) {
-      kreg.store(Ks[(kt + 1) & 1], t);
-      vreg.store(Vs[(kt + 1) & 1], t);
-    }
+    kreg.store(Ks[(kt + 1) & 1], t);
+    vreg.store(Vs[(kt + 1) & 1], t);
     __syncthreads();
   }
-  const float lt = half_exchange_sum(l);
-  if (qvalid) {
-    const float inv = 1.f / lt;
-    bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
+  if (!active) return;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
-      const int d0 = 8 * g4 + 4 * (lane >> 5);
-      bf16x4 v0, v1;
+  for (int g = 0; g < 2; ++g) {
+    const int q = q0 + 32 * g + (lane & 31);
+    const float lt = half_exchange_sum(l[g]);
+    if (q < N) {
+      const float inv = 1.f / lt;
+      bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(o0[4 * g4 + i] * inv); v1[i] = (bf16)(o1[4 * g4 + i] * inv); }
-      *reinterpret_cast<bf16x4*>(orow + d0) = v0;
-      *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
+      for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
+        const int d0 = 8 * g4 + 4 * (lane >> 5);
+        bf16x4 v0, v1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(o[0][g][4 * g4 + i] * inv); v1[i] = (bf16)(o[1][g][4 * g4 + i] * inv); }
+        *reinterpret_cast<bf16x4*>(orow + d0) = v0;
+        *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
+      }
+      if (lane < 32) lse[(int64_t)bh * N + q] = (m[g] + log2f(lt)) / LOG2E;
     }
-    if (lane < 32) lse[(int64_t)bh * N + q] = (m + log2f(lt)) / LOG2E;
   }
 }
 
@@ -257,29 +292,47 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __re
   }
 }
 
-// key on the lane: each wave owns 32 keys (128 per block); sweeps query tiles of 64.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+// 4 consecutive accumulator rows r = 4j..4j+3 of a 32-row block are rows 8j + 4h + 0..3: one float4
+__device__ __forceinline__ float4 rows4(const float* v, int j, int lane) {
+  return *reinterpret_cast<const float4*>(v + 8 * j + 4 * (lane >> 5));
+}
+
+// Key-parallel dK / dV.  Each wave owns 64 keys as two 32-key groups (4 waves = 256 keys per block)
+// and sweeps 64-query tiles staged in LDS (Q, dO, lse, delta); with the key on the lane the S / dP
+// accumulators are query rows x key columns, and every Q / dO fragment read from LDS (row or
+// transposed) feeds both key groups.  dK, dV accumulate in registers; no atomics.
+constexpr int BWD_K = 256;
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                            int N, int H, float scale, float scale_log2) {
+                                                            int N, int H, int nkb, float scale, float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][64 * LROW];
   __shared__ __attribute__((aligned(16))) bf16 Gs[2][64 * LROW];
   __shared__ __attribute__((aligned(16))) float Ls[2][64];
   __shared__ __attribute__((aligned(16))) float Ds[2][64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);
+  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
   const bf16* gbase = dout + (int64_t)b * N * ldo + hd * D;
-  const int key = blockIdx.x * 128 + wave * 32 + (lane & 31);
-  const bool kvalid = key < N;
-  bf16x8 kf[4], vf[4];
+  const int k0w = kb * BWD_K + wave * 64;
+  const bool active = k0w < N;
+  bf16x8 kf[2][4], vf[2][4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    kf[ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, kvalid);
-    vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, kvalid);
+  for (int g = 0; g < 2; ++g) {
+    const int key = k0w + 32 * g + (lane & 31);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[g][ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, key < N);
+      vf[g][ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
+    }
   }
-  f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
+  f32x16 dv[2][2], dk[2][2];  // [d half][key group]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) { dv[i][g] = zero16(); dk[i][g] = zero16(); }
   const int ntiles = (N + 63) / 64;
   Stage64 qreg, greg;
   float lreg = 0.f, dreg = 0.f;
@@ -301,42 +354,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   store_rows(0);
   __syncthreads();
   for (int qt = 0; qt < ntiles; ++qt) {
-    const bool more = qt + 1 < ntiles;
-    if (more) load_rows((qt + 1) * 64);
-    const bf16* Q_ = Qs[qt & 1];
-    const bf16* G_ = Gs[qt & 1];
-    const float* L_ = Ls[qt & 1];
-    const float* D_ = Ds[qt & 1];
+    load_rows(min(qt + 1, ntiles - 1) * 64);  // the last iteration re-stages into the idle buffer
+    if (active) {
+      const bf16* Q_ = Qs[qt & 1];
+      const bf16* G_ = Gs[qt & 1];
+      const float* L_ = Ls[qt & 1];
+      const float* D_ = Ds[qt & 1];
 #pragma unroll
-    for (int sq = 0; sq < 2; ++sq) {
-      f32x16 s = zero16(), dp = zero16();
+      for (int sq = 0; sq < 2; ++sq) {
+        f32x16 sc[2], dp[2];
+        sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma(frag_row(Q_, sq * 32 + (lane & 31), ks, lane), kf[ks], s);
-        dp = mfma(frag_row(G_, sq * 32 + (lane & 31), ks, lane), vf[ks], dp);
-      }
-      // rows of the accumulators are queries sq*32 + acc_row(r)
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8 qa = frag_row(Q_, sq * 32 + (lane & 31), ks, lane);
+          const bf16x8 ga = frag_row(G_, sq * 32 + (lane & 31), ks, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = sq * 32 + acc_row(r, lane);
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -L_[qi]));
-        s[r] = p;
-        dp[r] = p * (dp[r] - D_[qi]);
-      }
+          for (int g = 0; g < 2; ++g) {
+            sc[g] = mfma(qa, kf[g][ks], sc[g]);
+            dp[g] = mfma(ga, vf[g][ks], dp[g]);
+          }
+        }
+        // accumulator rows are queries sq*32 + acc_row(r); their lse / delta as 4 float4 each
+        float lr[16], dr[16];
 #pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        const bf16x8 pf = acc_frag(s, sk);
-        const bf16x8 df = acc_frag(dp, sk);
-        dv0 = mfma(frag_tr(G_, sq * 32 + 16 * sk, 0, lane), pf, dv0);
-        dv1 = mfma(frag_tr(G_, sq * 32 + 16 * sk, 32, lane), pf, dv1);
-        dk0 = mfma(frag_tr(Q_, sq * 32 + 16 * sk, 0, lane), df, dk0);
-        dk1 = mfma(frag_tr(Q_, sq * 32 + 16 * sk, 32, lane), df, dk1);
+        for (int j = 0; j < 4; ++j) {
+          const float4 l4 = rows4(L_ + sq * 32, j, lane), d4 = rows4(D_ + sq * 32, j, lane);
+          lr[4 * j] = l4.x; lr[4 * j + 1] = l4.y; lr[4 * j + 2] = l4.z; lr[4 * j + 3] = l4.w;
+          dr[4 * j] = d4.x; dr[4 * j + 1] = d4.y; dr[4 * j + 2] = d4.z; dr[4 * j + 3] = d4.w;
+        }
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[g][r], scale_log2, -lr[r]));
+            sc[g][r] = p;
+            dp[g][r] = p * (dp[g][r] - dr[r]);
+          }
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+          bf16x8 tg[2], tq[2];
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            tg[dh] = frag_tr(G_, sq * 32 + 16 * sk, 32 * dh, lane);
+            tq[dh] = frag_tr(Q_, sq * 32 + 16 * sk, 32 * dh, lane);
+          }
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const bf16x8 pf = acc_frag(sc[g], sk);
+            const bf16x8 df = acc_frag(dp[g], sk);
+#pragma unroll
+            for (int dh = 0; dh < 2; ++dh) {
+              dv[dh][g] = mfma(tg[dh], pf, dv[dh][g]);
+              dk[dh][g] = mfma(tq[dh], df, dk[dh][g]);
+            }
+          }
+        }
       }
     }
-    if (more) store_rows((qt + 1) & 1);
+    store_rows((qt + 1) & 1);
     __syncthreads();
   }
-  if (kvalid) {
+  if (!active) return;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int key = k0w + 32 * g + (lane & 31);
+    if (key >= N) continue;
     bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
     bf16* vrow = krow + H * D;
 #pragma unroll
@@ -345,10 +427,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       bf16x4 a0, a1, c0, c1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        a0[i] = (bf16)(dk0[4 * g4 + i] * scale);
-        a1[i] = (bf16)(dk1[4 * g4 + i] * scale);
-        c0[i] = (bf16)dv0[4 * g4 + i];
-        c1[i] = (bf16)dv1[4 * g4 + i];
+        a0[i] = (bf16)(dk[0][g][4 * g4 + i] * scale);
+        a1[i] = (bf16)(dk[1][g][4 * g4 + i] * scale);
+        c0[i] = (bf16)dv[0][g][4 * g4 + i];
+        c1[i] = (bf16)dv[1][g][4 * g4 + i];
       }
       *reinterpret_cast<bf16x4*>(krow + d0) = a0;
       *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
@@ -358,28 +440,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
-// query on the lane: each wave owns 32 queries (128 per block); sweeps key tiles of 64.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+// Query-parallel dQ: each wave owns 64 queries as two 32-query groups (256 per block), sweeps 64-key
+// tiles (K, V in LDS), recomputes S^T and dP^T with the query on the lane and accumulates dQ^T; every
+// K / V fragment read feeds both query groups.
+constexpr int BWD_Q = 256;
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          bf16* __restrict__ dqkv, int N, int H, float scale,
+                                                          bf16* __restrict__ dqkv, int N, int H, int nqb, float scale,
                                                           float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);
+  const int bh = w / nqb, qb = w - bh * nqb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const int q = blockIdx.x * 128 + wave * 32 + (lane & 31);
-  const bool qvalid = q < N;
-  bf16x8 qf[4], gf[4];
+  const int q0w = qb * BWD_Q + wave * 64;
+  const bool active = q0w < N;
+  bf16x8 qf[2][4], gf[2][4];
+  float lq[2], dl[2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qf[ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qvalid);
-    gf[ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qvalid);
+  for (int g = 0; g < 2; ++g) {
+    const int q = q0w + 32 * g + (lane & 31);
+    const bool qv = q < N;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[g][ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qv);
+      gf[g][ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
+    }
+    lq[g] = qv ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
+    dl[g] = qv ? delta[(int64_t)bh * N + q] : 0.f;
   }
-  const float lq = qvalid ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
-  const float dq_delta = qvalid ? delta[(int64_t)bh * N + q] : 0.f;
-  f32x16 a0 = zero16(), a1 = zero16();
+  f32x16 acc[2][2];  // [d half][query group]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { acc[i][0] = zero16(); acc[i][1] = zero16(); }
   const int ntiles = (N + 63) / 64;
   Stage64 kreg, vreg;
   kreg.load(base + H * D, ldt, N, t);
@@ -389,48 +483,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * 64;
-    const bool more = kt + 1 < ntiles;
-    if (more) {
-      kreg.load(base + (int64_t)(k0 + 64) * ldt + H * D, ldt, N - k0 - 64, t);
-      vreg.load(base + (int64_t)(k0 + 64) * ldt + 2 * H * D, ldt, N - k0 - 64, t);
-    }
-    const bf16* K_ = Ks[kt & 1];
-    const bf16* V_ = Vs[kt & 1];
+    const int kn = min(k0 + 64, (ntiles - 1) * 64);
+    kreg.load(base + (int64_t)kn * ldt + H * D, ldt, N - kn, t);
+    vreg.load(base + (int64_t)kn * ldt + 2 * H * D, ldt, N - kn, t);
+    if (active) {
+      const bf16* K_ = Ks[kt & 1];
+      const bf16* V_ = Vs[kt & 1];
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      f32x16 s = zero16(), dp = zero16();
+      for (int st = 0; st < 2; ++st) {
+        f32x16 sc[2], dp[2];
+        sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma(frag_row(K_, st * 32 + (lane & 31), ks, lane), qf[ks], s);
-        dp = mfma(frag_row(V_, st * 32 + (lane & 31), ks, lane), gf[ks], dp);
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8 ka = frag_row(K_, st * 32 + (lane & 31), ks, lane);
+          const bf16x8 va = frag_row(V_, st * 32 + (lane & 31), ks, lane);
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            sc[g] = mfma(ka, qf[g][ks], sc[g]);
+            dp[g] = mfma(va, gf[g][ks], dp[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + st * 32 + acc_row(r, lane);
+            const float p = key < N ? __builtin_amdgcn_exp2f(fmaf(sc[g][r], scale_log2, -lq[g])) : 0.f;
+            dp[g][r] = p * (dp[g][r] - dl[g]);
+          }
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+          bf16x8 tk[2];
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) tk[dh] = frag_tr(K_, st * 32 + 16 * sk, 32 * dh, lane);
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const bf16x8 df = acc_frag(dp[g], sk);
+#pragma unroll
+            for (int dh = 0; dh < 2; ++dh) acc[dh][g] = mfma(tk[dh], df, acc[dh][g]);
+          }
+        }
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + st * 32 + acc_row(r, lane);
-        const float p = key < N ? __builtin_amdgcn_exp2f(fmaf(s[r], scale_log2, -lq)) : 0.f;
-        dp[r] = p * (dp[r] - dq_delta);
-      }
-#pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        const bf16x8 df = acc_frag(dp, sk);
-        a0 = mfma(frag_tr(K_, st * 32 + 16 * sk, 0, lane), df, a0);
-        a1 = mfma(frag_tr(K_, st * 32 + 16 * sk, 32, lane), df, a1);
-      }
     }
-    if (more) {
-      kreg.store(Ks[(kt + 1) & 1], t);
-      vreg.store(Vs[(kt + 1) & 1], t);
-    }
+    kreg.store(Ks[(kt + 1) & 1], t);
+    vreg.store(Vs[(kt + 1) & 1], t);
     __syncthreads();
   }
-  if (qvalid) {
+  if (!active) return;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int q = q0w + 32 * g + (lane & 31);
+    if (q >= N) continue;
     bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int d0 = 8 * g4 + 4 * (lane >> 5);
       bf16x4 v0, v1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(a0[4 * g4 + i] * scale); v1[i] = (bf16)(a1[4 * g4 + i] * scale); }
+      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(acc[0][g][4 * g4 + i] * scale); v1[i] = (bf16)(acc[1][g][4 * g4 + i] * scale); }
       *reinterpret_cast<bf16x4*>(qrow + d0) = v0;
       *reinterpret_cast<bf16x4*>(qrow + 32 + d0) = v1;
     }
@@ -581,8 +691,10 @@ extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtyp
     return 0;
   }
   MIA_CHECK_ARG(dtype == MIA_BF16, "attn_fwd: dtype");
-  dim3 grid((unsigned)cdiv(N, 128), (unsigned)(B * H));
-  attn_fwd_kernel<<<grid, 256, 0, as_stream(stream)>>>((const bf16*)qkv, (bf16*)out, lse, N, H, scale * LOG2E);
+  const int nqb = (int)cdiv(N, FWD_Q);
+  MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd: grid too large");
+  attn_fwd_kernel<<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>((const bf16*)qkv, (bf16*)out, lse, N, H, nqb,
+                                                                        scale * LOG2E);
   MIA_LAUNCH_CHECK("attn_fwd");
   return 0;
 }
@@ -613,12 +725,12 @@ extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, 
   attn_delta_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
       (const bf16*)out, (const bf16*)dout, delta, B, N, H);
   MIA_LAUNCH_CHECK("attn_delta");
-  dim3 grid((unsigned)cdiv(N, 128), (unsigned)(B * H));
-  attn_bwd_dkdv_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale,
-                                            scale * LOG2E);
+  const int nkb = (int)cdiv(N, BWD_K), nqb = (int)cdiv(N, BWD_Q);
+  attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                               (bf16*)dqkv, N, H, nkb, scale, scale * LOG2E);
   MIA_LAUNCH_CHECK("attn_bwd_dkdv");
-  attn_bwd_dq_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale,
-                                          scale * LOG2E);
+  attn_bwd_dq_kernel<<<(unsigned)(nqb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                             (bf16*)dqkv, N, H, nqb, scale, scale * LOG2E);
   MIA_LAUNCH_CHECK("attn_bwd_dq");
   return 0;
 }

@@ -3,24 +3,25 @@
 // Per frame f (hop 160): the 400 windowed samples x[f*160-200+u]*hann[u] (reflect padding at the
 // clip edges, = torch.stft center=True with the 400-tap window centred in n_fft=1024) are packed as
 // 200 complex points z[n] = x[2n] + i x[2n+1], transformed by a 512-point Stockham radix-8 FFT in
-// LDS (one wave per frame, 3 passes), split into the 513 real-FFT bins, squared, reduced into the
-// 128 htk mel bands (sparse band table: start/len/offset/weights), and converted to dB.
-// A block owns 32 consecutive frames of one clip: the 5,360-sample input segment is read from HBM
-// once with coalesced loads into LDS, and the 128 x 32 dB tile is written back as 128 rows of
-// 32 contiguous frames.  Per-clip top_db clamp + mean / unbiased-std normalisation need the clip
+// LDS (one wave per frame, 3 passes in one in-place buffer per wave; window taps and twiddles held in
+// registers), split into the 513 real-FFT bins, squared, reduced into the 128 htk mel bands (sparse
+// band table staged in LDS: start/len/offset/weights), and converted to dB (f32 log10).
+// A block owns 16 consecutive frames of one clip: the 2,800-sample input segment is read from HBM
+// once with coalesced loads into LDS, and the 128 x 16 dB tile is written back as 128 rows of
+// 16 contiguous frames.  Per-clip top_db clamp + mean / unbiased-std normalisation need the clip
 // max first, so two light passes follow (stats over the dB tensor, which stays in the 256 MB
 // Infinity Cache at batch 256, then an in-place normalise).
 #include "common.h"
 
 namespace {
 
-constexpr int FB = 32;          // frames per block
+constexpr int FB = 16;          // frames per block (3 blocks per CU by LDS)
 constexpr int NFFT = 1024;
 constexpr int NC = 512;         // complex FFT size
 constexpr int HOP = 160;
 constexpr int WIN = 400;
 constexpr int NMEL_MAX = 128;
-constexpr int SEG = (FB - 1) * HOP + WIN;  // 5360 samples
+constexpr int SEG = (FB - 1) * HOP + WIN;  // 2800 samples
 
 struct MelTables {
   const float* window;   // [WIN]
@@ -71,12 +72,16 @@ __device__ __forceinline__ int reflect_idx(int n, int T) {
   return n;
 }
 
+constexpr int MAX_NNZ = 1536;  // band weights staged in LDS (htk, 128 mels at n_fft 1024: 1,008)
+
 __global__ __launch_bounds__(256) void fft_mel_db_kernel(const float* __restrict__ wav, int64_t ld, int T,
                                                          int frames, int n_mels, MelTables tb,
                                                          float* __restrict__ out, float* __restrict__ blockmax) {
   __shared__ float seg[SEG];
-  __shared__ float2 buf[4][2][NC];
+  __shared__ float2 buf[4][NC];          // one in-place Stockham buffer per wave
   __shared__ float tile[NMEL_MAX][FB + 1];
+  __shared__ float bw[MAX_NNZ];
+  __shared__ int bs[NMEL_MAX], bl[NMEL_MAX], bo[NMEL_MAX];
   __shared__ float redmax[4];
 
   const int b = blockIdx.y;
@@ -84,6 +89,12 @@ __global__ __launch_bounds__(256) void fft_mel_db_kernel(const float* __restrict
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const float* x = wav + (int64_t)b * ld;
 
+  // mel band table into LDS (the per-band loops below then touch no global memory)
+  const int nnz = tb.band_off[n_mels - 1] + tb.band_len[n_mels - 1];
+  const bool w_lds = nnz <= MAX_NNZ;  // block-uniform
+  if (w_lds)
+    for (int i = t; i < nnz; i += 256) bw[i] = tb.band_w[i];
+  for (int m = t; m < n_mels; m += 256) { bs[m] = tb.band_start[m]; bl[m] = tb.band_len[m]; bo[m] = tb.band_off[m]; }
   // coalesced segment load with reflect padding
   const int s0 = f0 * HOP - WIN / 2;
   for (int i = t; i < SEG; i += 256) {
@@ -92,79 +103,99 @@ __global__ __launch_bounds__(256) void fft_mel_db_kernel(const float* __restrict
     if (n >= -(NFFT / 2) && n < T + NFFT / 2) v = x[reflect_idx(n, T)];  // valid reflect range (T > 512)
     seg[i] = v;
   }
+  // loop-invariant per-lane constants: window taps, stage twiddles, real-split twiddles
+  float2 win[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int u = 2 * (lane + 64 * r);
+    win[r] = u < WIN ? make_float2(tb.window[u], tb.window[u + 1]) : make_float2(0.f, 0.f);
+  }
+  float2 tw1[8], tw2[8], tws[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    tw1[r] = tb.tw512[((lane % 8) * (NC / 64) * r) & (NC - 1)];
+    tw2[r] = tb.tw512[(lane * (NC / 512) * r) & (NC - 1)];
+    tws[r] = tb.tw1024[lane + 64 * r];
+  }
   __syncthreads();
 
+  const float* bwp = w_lds ? bw : tb.band_w;
   float lmax = -INFINITY;
+  float2* d = buf[wave];
   for (int fi = wave; fi < FB; fi += 4) {
     const int f = f0 + fi;
     if (f >= frames) break;  // wave-uniform
-    float2* d0 = buf[wave][0];
-    float2* d1 = buf[wave][1];
     // stage 0 (Ns = 1) reads z[j + 64 r] straight from the segment, z[n] = 0 for n >= 200
     {
       float2 v[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const int n = lane + 64 * r;
-        if (n < WIN / 2) {
-          const int u = 2 * n;
-          v[r] = make_float2(seg[fi * HOP + u] * tb.window[u], seg[fi * HOP + u + 1] * tb.window[u + 1]);
+        if (r < 4 && n < WIN / 2) {
+          const float2 xv = *reinterpret_cast<const float2*>(&seg[fi * HOP + 2 * n]);
+          v[r] = make_float2(xv.x * win[r].x, xv.y * win[r].y);
         } else {
           v[r] = make_float2(0.f, 0.f);
         }
       }
       dft8(v);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) d0[lane * 8 + r] = v[r];
+      for (int r = 0; r < 8; ++r) d[lane * 8 + r] = v[r];
     }
     wave_sync();
-    // stage 1 (Ns = 8) and stage 2 (Ns = 64)
+    // stages 1 (Ns = 8) and 2 (Ns = 64), in place: every lane's reads land before any lane's writes
+    // (one wave, program order), so the single buffer needs no ping-pong
 #pragma unroll
     for (int st = 1; st < 3; ++st) {
       const int Ns = st == 1 ? 8 : 64;
-      const float2* src = st == 1 ? d0 : d1;
-      float2* dst = st == 1 ? d1 : d0;
       float2 v[8];
       const int jm = lane % Ns;
-      const int qstep = jm * (NC / (Ns * 8));
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        float2 a = src[lane + 64 * r];
-        if (r) a = cmul(a, tb.tw512[(qstep * r) & (NC - 1)]);
+        float2 a = d[lane + 64 * r];
+        if (r) a = cmul(a, st == 1 ? tw1[r] : tw2[r]);
         v[r] = a;
       }
       dft8(v);
+      wave_sync();
       const int idxD = (lane / Ns) * Ns * 8 + jm;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) dst[idxD + r * Ns] = v[r];
+      for (int r = 0; r < 8; ++r) d[idxD + r * Ns] = v[r];
       wave_sync();
     }
-    // Z in d0 (natural order). Real-FFT split -> power P[k] (k = 0..512) into d1 as floats.
-    float* P = reinterpret_cast<float*>(d1);
+    // Z in d (natural order). Real-FFT split -> power P[k] (k = 0..512), kept in registers, then
+    // written over the (consumed) spectrum as floats
+    float pk[8];
+    float pn = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = lane + 64 * q;
-      const float2 zk = d0[k];
-      const float2 zc = d0[(NC - k) & (NC - 1)];
+      const float2 zk = d[k];
+      const float2 zc = d[(NC - k) & (NC - 1)];
       const float2 zcj = make_float2(zc.x, -zc.y);
       const float2 e = cadd(zk, zcj);          // 2 * even part
       const float2 o = csub(zk, zcj);          // 2i * odd part (before twiddle)
       // X[k] = 0.5*(e - i W^k o)
-      const float2 wo = cmul(tb.tw1024[k], o);
+      const float2 wo = cmul(tws[q], o);
       const float2 X = make_float2(0.5f * (e.x + wo.y), 0.5f * (e.y - wo.x));
-      P[k] = X.x * X.x + X.y * X.y;
+      pk[q] = X.x * X.x + X.y * X.y;
     }
     if (lane == 0) {
-      const float2 z0 = d0[0];
+      const float2 z0 = d[0];
       const float xn = z0.x - z0.y;  // X[512]
-      P[NC] = xn * xn;
+      pn = xn * xn;
     }
     wave_sync();
+    float* P = reinterpret_cast<float*>(d);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) P[lane + 64 * q] = pk[q];
+    if (lane == 0) P[NC] = pn;
+    wave_sync();
     for (int m = lane; m < n_mels; m += 64) {
-      const int ks = tb.band_start[m], kl = tb.band_len[m], off = tb.band_off[m];
+      const int ks = bs[m], kl = bl[m], off = bo[m];
       float acc = 0.f;
-      for (int i = 0; i < kl; ++i) acc = fmaf(P[ks + i], tb.band_w[off + i], acc);
-      const float db = (float)(10.0 * log10((double)fmaxf(acc, 1e-10f)));  // correctly rounded like torch
+      for (int i = 0; i < kl; ++i) acc = fmaf(P[ks + i], bwp[off + i], acc);
+      const float db = 10.f * log10f(fmaxf(acc, 1e-10f));  // AmplitudeToDB (multiplier 10, amin 1e-10)
       tile[m][fi] = db;
       lmax = fmaxf(lmax, db);
     }
@@ -204,7 +235,22 @@ __global__ __launch_bounds__(256) void clip_stats_kernel(const float* __restrict
   const float floor_v = smax - top_db;
   const float* x = out + (int64_t)b * per_clip;
   double s = 0.0, ss = 0.0;  // sums of (v - amax): exact zero variance for a constant clip
-  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < per_clip; i += (int64_t)gridDim.x * 256) {
+  const bool vec = ((per_clip & 3) == 0);  // 16-B aligned clip rows (the B x 128 x 1379 case)
+  const int64_t n4 = vec ? per_clip >> 2 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 q = reinterpret_cast<const float4*>(x)[i];
+    const float e[4] = {q.x, q.y, q.z, q.w};
+    float fs = 0.f, fss = 0.f;  // 4 terms in f32 (|v - amax| <= top_db), flushed to double
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = fmaxf(e[j], floor_v) - smax;
+      fs += v;
+      fss = fmaf(v, v, fss);
+    }
+    s += (double)fs;
+    ss += (double)fss;
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + t; i < per_clip; i += (int64_t)gridDim.x * 256) {
     const double v = (double)fmaxf(x[i], floor_v) - (double)smax;
     s += v;
     ss += v * v;
@@ -255,7 +301,19 @@ __global__ __launch_bounds__(256) void clip_norm_kernel(float* __restrict__ out,
   const float fl = sp[0], mean = sp[1], sd = sp[2];
   const bool do_norm = normalize && sd > 0.f;
   float* x = out + (int64_t)b * per_clip;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < per_clip; i += (int64_t)gridDim.x * 256) {
+  const int64_t n4 = ((per_clip & 3) == 0) ? per_clip >> 2 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 q = reinterpret_cast<float4*>(x)[i];
+    float e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = fmaxf(e[j], fl);
+      if (do_norm) v = (v - mean) / sd * tstd + tmean;
+      e[j] = v;
+    }
+    reinterpret_cast<float4*>(x)[i] = make_float4(e[0], e[1], e[2], e[3]);
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + t; i < per_clip; i += (int64_t)gridDim.x * 256) {
     float v = fmaxf(x[i], fl);
     if (do_norm) v = (v - mean) / sd * tstd + tmean;
     x[i] = v;

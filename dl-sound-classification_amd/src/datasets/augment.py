@@ -80,7 +80,7 @@ def bc_mix(wav: torch.Tensor, labels: torch.Tensor, num_classes: int, gen: torch
     L.require_device(wav, "bc_mix")
     wav = wav.reshape(wav.shape[0], -1).contiguous().float()
     B, T = wav.shape
-    labels = labels.to(torch.int64).contiguous()
+    labels = labels.to(device=wav.device, dtype=torch.int64).contiguous()
     if pool is None:
         pool, pool_labels = wav, labels
     pool = pool.reshape(pool.shape[0], -1).contiguous().float()
@@ -89,10 +89,10 @@ def bc_mix(wav: torch.Tensor, labels: torch.Tensor, num_classes: int, gen: torch
         raise ValueError(f"pool clips have {pool.shape[1]} samples, batch {T}")
     if partner is None:
         partner = bc_partner(labels, pool_labels, torch.rand(B, generator=gen, device=wav.device))
-    partner = partner.to(torch.int32).contiguous()
+    partner = partner.to(device=wav.device, dtype=torch.int32).contiguous()
     if r is None:
         r = torch.rand(B, generator=gen, device=wav.device)
-    r = r.float().contiguous()
+    r = r.to(device=wav.device, dtype=torch.float32).contiguous()
     out = torch.empty_like(wav)
     y = torch.empty(B, num_classes, dtype=torch.float32, device=wav.device)
     p = torch.empty(B, dtype=torch.float32, device=wav.device)
@@ -181,8 +181,8 @@ def stretch_gain(wav: torch.Tensor, time_stretch=None, gain_shift=None, gen: tor
         gain = torch.where(on, torch.pow(10.0, db / 20.0), torch.ones_like(db)).float()
     if factor is None and gain is None:
         return wav
-    factor = None if factor is None else factor.to(torch.float64).contiguous()
-    gain = None if gain is None else gain.float().contiguous()
+    factor = None if factor is None else factor.to(device=dev, dtype=torch.float64).contiguous()
+    gain = None if gain is None else gain.to(device=dev, dtype=torch.float32).contiguous()
     out = torch.empty_like(wav)
     L.check(L.load().mia_stretch_gain(wav.data_ptr(), T, B, L.ptr(factor), L.ptr(gain), out.data_ptr(),
                                       L.stream_ptr()), "mia_stretch_gain")

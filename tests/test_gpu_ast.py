@@ -28,7 +28,7 @@ def _attn_ref(qkv, B, N, H):
 
 
 @pytest.mark.parametrize("dt", [L.BF16, L.F32])
-@pytest.mark.parametrize("B,N,H", [(2, 100, 2), (1, 257, 3), (2, 1645, 1)])
+@pytest.mark.parametrize("B,N,H", [(2, 100, 2), (1, 257, 3), (2, 1645, 1), (3, 37, 2), (4, 300, 2), (8, 1645, 1)])
 def test_attention_fwd_bwd(cuda, dt, B, N, H):
     g = torch.Generator().manual_seed(N + H)
     tdt = torch.bfloat16 if dt == L.BF16 else torch.float32
@@ -48,6 +48,8 @@ def test_attention_fwd_bwd(cuda, dt, B, N, H):
     torch.cuda.synchronize()
     tol = 2e-2 if dt == L.BF16 else 1e-5
     assert rel(out.view(B, N, H, 64).permute(0, 2, 1, 3), o) < tol
+    lse_ref = torch.logsumexp(q.detach() @ k.detach().transpose(-1, -2) / 8.0, -1)  # (B, H, N)
+    assert float((lse.cpu().double() - lse_ref).abs().max()) < (2e-2 if dt == L.BF16 else 1e-5)
     dqkv = dq.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     assert rel(dqkv[0], q.grad) < 3 * tol
     assert rel(dqkv[1], k.grad) < 3 * tol

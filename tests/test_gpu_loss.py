@@ -119,4 +119,5 @@ def test_envnet_dropout_backward_mask_is_forward_mask(cuda):
                            (m.classifier[1].weight.grad[rows], dW1, "fc1")):
         err = float((got.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 1e-4, (name, err)
-    torch.testing.assert_close(m.classifier[4].bias.grad.double(), d2.sum(0), rtol=1e-4, atol=1e-9)
+    db = d2.sum(0)
+    torch.testing.assert_close(m.classifier[4].bias.grad.double(), db, rtol=1e-4, atol=1e-5 * float(db.abs().max()))
