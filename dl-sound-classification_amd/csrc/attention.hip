@@ -18,6 +18,10 @@ namespace {
 
 constexpr int D = 64;
 constexpr int LROW = 72;  // LDS row stride in bf16 (144 B): conflict-free ds_read_b128 rows
+// Stride of a tile read ONLY transposed (forward V): 96 bf16 = 48 dwords puts the 4 rows of one
+// ds_read_b64_tr_b16 group on disjoint 16-bank windows (rows 0..3 -> banks 0, 48, 32, 16); at the
+// 36-dword LROW stride rows r and r + 2 overlap by 8 banks (2-way conflicts, SQ_LDS_BANK_CONFLICT).
+constexpr int VROW = 96;
 constexpr float LOG2E = 1.4426950408889634f;
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -58,11 +62,12 @@ struct Stage64 {
       v[s] = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
     }
   }
+  template <int ROW = LROW>
   __device__ __forceinline__ void store(bf16* lds, int t) const {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = t + 256 * s;
-      *reinterpret_cast<uint4*>(lds + (c >> 3) * LROW + (c & 7) * 8) = v[s];
+      *reinterpret_cast<uint4*>(lds + (c >> 3) * ROW + (c & 7) * 8) = v[s];
     }
   }
 };
@@ -74,12 +79,13 @@ __device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int ks, int
 
 // Transposed fragment in the accumulator k-order: element j = tile[k0 + 8(j>>2) + 4h + (j&3)][c0 + (lane&31)]
 // (two ds_read_b64_tr_b16: 4 consecutive tile rows x 16 columns per 16-lane group).
+template <int ROW = LROW>
 __device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int k0, int c0, int lane) {
   const int i16 = lane & 15, g = lane >> 4, h = lane >> 5;
   const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
   const int r = k0 + 4 * h + (i16 >> 2);
-  const bf16* p0 = lds + r * LROW + col;
-  const bf16* p1 = p0 + 8 * LROW;
+  const bf16* p0 = lds + r * ROW + col;
+  const bf16* p1 = p0 + 8 * ROW;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
   s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -136,15 +142,96 @@ __device__ __forceinline__ int xcd_work_item(int L, int total) {
   return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
 }
 
+constexpr int FWD_Q = 256;
+// Deferred max (T13 of the CDNA4 playbook): the running max moves only when a tile's scores exceed it
+// by more than FWD_THR log2 units, so P stays <= 2^8 (exact in f32, same relative precision in bf16)
+// and the O / l rescale pass runs on a handful of tiles instead of on almost every tile.
+constexpr float FWD_THR = 8.f;
+
+struct FwdState {
+  bf16x8 qf[2][4];
+  f32x16 o[2][2];  // [d half][query group]
+  float l[2];      // row sums (this lane's half of the keys)
+  float m[2];      // running max (log2 units); set from the first tile
+};
+
+// One 64-key tile of the forward; TAIL masks keys >= N (only the last tile, peeled off the loop).
+template <bool TAIL>
+__device__ __forceinline__ void fwd_tile(FwdState& st, const bf16* K_, const bf16* V_, int k0, int N, bool first,
+                                         int lane) {
+  // S^T = K . Q'^T (log2 units): 16 MFMAs, 8 K fragments each feeding both query groups
+  f32x16 s[2][2];  // [key half][query group]
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const bf16x8 kf = frag_row(K_, 32 * kh + (lane & 31), ks, lane);
+      s[kh][0] = mfma(kf, st.qf[0][ks], ks == 0 ? zero16() : s[kh][0]);
+      s[kh][1] = mfma(kf, st.qf[1][ks], ks == 0 ? zero16() : s[kh][1]);
+    }
+  }
+  bf16x8 pf[2][4];  // [query group][16-key chunk]
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (k0 + acc_row(r, lane) >= N) s[0][g][r] = -INFINITY;
+        if (k0 + 32 + acc_row(r, lane) >= N) s[1][g][r] = -INFINITY;
+      }
+    }
+    float mx = max3(s[0][g][0], s[1][g][0], s[0][g][1]);
+#pragma unroll
+    for (int r = 1; r < 15; ++r) mx = max3(mx, s[1][g][r], s[0][g][r + 1]);
+    mx = max3(mx, s[1][g][15], s[1][g][15]);
+    mx = half_exchange_max(mx);  // this tile's max for this lane's query
+    // move the running max (wave-uniform branch): always on the first tile, later only past FWD_THR
+    if (__builtin_expect(first || __any(mx > st.m[g] + FWD_THR), 0)) {
+      const float mn = first ? mx : fmaxf(mx, st.m[g]);
+      if (!first) {
+        const float alpha = __builtin_amdgcn_exp2f(st.m[g] - mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { st.o[0][g][r] *= alpha; st.o[1][g][r] *= alpha; }
+        st.l[g] *= alpha;
+      }
+      st.m[g] = mn;
+    }
+    const float nm = -st.m[g];
+    float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[0][g][r] = __builtin_amdgcn_exp2f(s[0][g][r] + nm);
+      s[1][g][r] = __builtin_amdgcn_exp2f(s[1][g][r] + nm);
+      l0 += s[0][g][r];
+      l1 += s[1][g][r];
+    }
+    st.l[g] += l0 + l1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pf[g][c] = acc_frag(s[c >> 1][g], c & 1);
+  }
+  // O^T += V^T . P^T: 16 MFMAs, 8 transposed V fragments each feeding both query groups
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const bf16x8 vf = frag_tr<VROW>(V_, 16 * c, 32 * dh, lane);
+      st.o[dh][0] = mfma(vf, pf[0][c], st.o[dh][0]);
+      st.o[dh][1] = mfma(vf, pf[1][c], st.o[dh][1]);
+    }
+  }
+}
+
 // Each wave owns 64 queries as two 32-query groups sharing every K / V fragment read from LDS (one
 // LDS fragment feeds 2 MFMAs); 4 waves = 256 queries per block; 64-key tiles double-buffered in LDS
 // with the next tile's global loads in flight under the current tile's MFMAs.
-constexpr int FWD_Q = 256;
+// VALU diet (the loop is vector-issue bound at head dim 64): Q is pre-scaled by scale*log2(e) once
+// (bf16) so p = exp2(s - m) is one add + one exp per score; the running max is deferred (FWD_THR);
+// the key mask exists only in the peeled last tile.
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                        float* __restrict__ lse, int N, int H, int nqb,
                                                        float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * VROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
   const int bh = w / nqb, qb = w - bh * nqb, b = bh / H, hd = bh % H;
@@ -152,105 +239,47 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
   const int q0 = qb * FWD_Q + wave * 64;
   const bool active = q0 < N;  // wave-uniform: a wave past the last query only helps staging
-  bf16x8 qf[2][4];
+  FwdState st;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int q = q0 + 32 * g + (lane & 31);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[g][ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
-  }
-  f32x16 o[2][2];  // [d half][query group]
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) { o[i][0] = zero16(); o[i][1] = zero16(); }
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};  // m: running max of the log2-scaled scores
+      for (int j = 0; j < 8; ++j) st.qf[g][ks][j] = (bf16)((float)r[j] * scale_log2);
+    }
+    st.o[0][g] = zero16(); st.o[1][g] = zero16();
+    st.m[g] = 0.f;
+    st.l[g] = 0.f;
+  }
   const int ntiles = (N + 63) / 64;
   Stage64 kreg, vreg;
   kreg.load(base + H * D, ldt, N, t);
   vreg.load(base + 2 * H * D, ldt, N, t);
   kreg.store(Ks[0], t);
-  vreg.store(Vs[0], t);
+  vreg.store<VROW>(Vs[0], t);
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int k0 = kt * 64;
-    // next tile's loads in flight under this tile's MFMAs (the last iteration re-reads the last
-    // tile into the idle buffer: unconditional, so the staging registers stay in VGPRs)
-    const int kn = min(k0 + 64, (ntiles - 1) * 64);
+  for (int kt = 0; kt < ntiles - 1; ++kt) {
+    // next tile's loads in flight under this tile's MFMAs
+    const int kn = (kt + 1) * 64;
     kreg.load(base + (int64_t)kn * ldt + H * D, ldt, N - kn, t);
     vreg.load(base + (int64_t)kn * ldt + 2 * H * D, ldt, N - kn, t);
-    if (active) {
-      const bf16* K_ = Ks[kt & 1];
-      const bf16* V_ = Vs[kt & 1];
-      const bool tail = k0 + 64 > N;
-      // S^T = K . Q^T for both key halves x both query groups: 16 MFMAs, 8 K fragments
-      f32x16 s[2][2];  // [key half][query group]
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) { s[kh][0] = zero16(); s[kh][1] = zero16(); }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-          const bf16x8 kf = frag_row(K_, 32 * kh + (lane & 31), ks, lane);
-          s[kh][0] = mfma(kf, qf[0][ks], s[kh][0]);
-          s[kh][1] = mfma(kf, qf[1][ks], s[kh][1]);
-        }
-      }
-      bf16x8 pf[2][4];  // [query group][16-key chunk]
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        if (tail) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            if (k0 + acc_row(r, lane) >= N) s[0][g][r] = -INFINITY;
-            if (k0 + 32 + acc_row(r, lane) >= N) s[1][g][r] = -INFINITY;
-          }
-        }
-        float mx = max3(s[0][g][0], s[1][g][0], s[0][g][1]);
-#pragma unroll
-        for (int r = 1; r < 15; ++r) mx = max3(mx, s[1][g][r], s[0][g][r + 1]);
-        mx = max3(mx, s[1][g][15], s[1][g][15]);
-        mx = half_exchange_max(mx) * scale_log2;
-        const float mn = fmaxf(m[g], mx);
-        // rescale O only when some lane's running max moved (wave-uniform branch)
-        if (__any(mn > m[g])) {
-          const float alpha = m[g] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[g] - mn);
-          l[g] *= alpha;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) { o[0][g][r] *= alpha; o[1][g][r] *= alpha; }
-        }
-        m[g] = mn;
-        const float nm = mn == -INFINITY ? 0.f : -mn;
-        float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s[0][g][r] = __builtin_amdgcn_exp2f(fmaf(s[0][g][r], scale_log2, nm));
-          s[1][g][r] = __builtin_amdgcn_exp2f(fmaf(s[1][g][r], scale_log2, nm));
-          l0 += s[0][g][r];
-          l1 += s[1][g][r];
-        }
-        l[g] += l0 + l1;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pf[g][c] = acc_frag(s[c >> 1][g], c & 1);
-      }
-      // O^T += V^T . P^T: 16 MFMAs, 8 transposed V fragments each feeding both query groups
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          const bf16x8 vf = frag_tr(V_, 16 * c, 32 * dh, lane);
-          o[dh][0] = mfma(vf, pf[0][c], o[dh][0]);
-          o[dh][1] = mfma(vf, pf[1][c], o[dh][1]);
-        }
-      }
-    }
+    if (active) fwd_tile<false>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
     kreg.store(Ks[(kt + 1) & 1], t);
-    vreg.store(Vs[(kt + 1) & 1], t);
+    vreg.store<VROW>(Vs[(kt + 1) & 1], t);
     __syncthreads();
   }
   if (!active) return;
+  {
+    const int kt = ntiles - 1;
+    if ((kt + 1) * 64 > N) fwd_tile<true>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
+    else fwd_tile<false>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
+  }
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int q = q0 + 32 * g + (lane & 31);
-    const float lt = half_exchange_sum(l[g]);
+    const float lt = half_exchange_sum(st.l[g]);
     if (q < N) {
       const float inv = 1.f / lt;
       bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
@@ -259,11 +288,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
         const int d0 = 8 * g4 + 4 * (lane >> 5);
         bf16x4 v0, v1;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(o[0][g][4 * g4 + i] * inv); v1[i] = (bf16)(o[1][g][4 * g4 + i] * inv); }
+        for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(st.o[0][g][4 * g4 + i] * inv); v1[i] = (bf16)(st.o[1][g][4 * g4 + i] * inv); }
         *reinterpret_cast<bf16x4*>(orow + d0) = v0;
         *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
       }
-      if (lane < 32) lse[(int64_t)bh * N + q] = (m[g] + log2f(lt)) / LOG2E;
+      if (lane < 32) lse[(int64_t)bh * N + q] = (st.m[g] + log2f(lt)) / LOG2E;
     }
   }
 }

@@ -1491,8 +1491,17 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int bm = g.nfast ? wgid / g.nbn : wgid % g.nbm;
-  const int bn = g.nfast ? wgid % g.nbn : wgid / g.nbm;
+  int bm, bn;
+  if (g.nfast) {  // grouped order: gm row blocks x all column tiles, M fastest inside a group
+    const int gsize = g.gm * g.nbn;
+    const int grp = wgid / gsize, rem = wgid - grp * gsize;
+    const int gme = min(g.gm, g.nbm - grp * g.gm);
+    bm = grp * g.gm + rem % gme;
+    bn = rem / gme;
+  } else {
+    bm = wgid % g.nbm;
+    bn = wgid / g.nbm;
+  }
   const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
   const int z = blockIdx.y;
   const int64_t kbeg = (int64_t)z * g.kper;
@@ -1572,15 +1581,14 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       const int col = (lane & 31) * 4;
       const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
       f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
-      if (g.nt) __builtin_nontemporal_store(v, dst);
-      else *dst = v;
+      __builtin_nontemporal_store(v, dst);
     }
     return;
   }
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
   // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
   const bool save = g.e.act == MIA_ACT_GELU_SAVE;
-  const bool plain16 = g.full16 && g.split == 1 && g.e.dtype == MIA_BF16 &&
+  const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
                        (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU || g.e.act == MIA_ACT_GELU ||
                         (save && g.e.aux_dtype == MIA_BF16 && (g.e.ldaux & 7) == 0 &&
                          ((reinterpret_cast<uintptr_t>(g.e.aux)) & 15) == 0)) &&
@@ -1863,21 +1871,18 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     d.split = split_k < 1 ? 1 : split_k;
     d.kper = cdiv(cdiv(K, d.split), 64) * 64;
     d.nbm = (int)cdiv(M, 128); d.nbn = (int)cdiv(N, 128);
-    // tall GEMMs (AST linears: M = tokens, N <= 3072): walk N fastest so each A row block is read
-    // from HBM once (at batch 256 the activations exceed the 256 MB Infinity Cache, and an
+    // tall GEMMs (AST linears: M = tokens, N <= 3072): grouped tile order (DArgs::gm) so each A row
+    // block is read from HBM once (at batch 256 the activations exceed the 256 MB Infinity Cache; an
     // M-fastest walk re-streamed them once per column tile: 12-15 GB per launch, rocprof FETCH_SIZE)
+    // and each B column tile once per group of gm row blocks
     d.nfast = (d.split == 1 && d.nbn <= 32 && d.nbm >= 4 * d.nbn) ? 1 : 0;
+    d.gm = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2ll << 20) / (128 * 2 * std::max<int64_t>(K, 64))));
     d.ws = reinterpret_cast<float*>(workspace);
     d.e = to_dev(*E);
-    static const int nt_env = [] { const char* v = getenv("MIA_EPI_NT"); return v ? atoi(v) : 1; }();
-    d.nt = nt_env;
-    static const int f16_env = [] { const char* v = getenv("MIA_EPI_FULL16"); return v ? atoi(v) : 1; }();
-    d.full16 = f16_env;
     hipStream_t s = as_stream(stream);
     hipError_t err;
     const int la = A->layout, lb = B->layout;
-    if (dgemm256_pays(M, N, d.split)) err = dgemm256_launch(d, la, lb, s);
-    else if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
+    if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
     else if (la == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_RC>(d, s);
     else if (lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_KC>(d, s);
     else err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC>(d, s);

@@ -1,4 +1,4 @@
-// Shared pieces of the GEMM kernels (gemm.hip, dgemm256.hip): the epilogue descriptor and its
+// Shared pieces of the GEMM kernels (gemm.hip and its callers): the epilogue descriptor and its
 // vectorised store path, and the dense bf16 GEMM argument block.
 #pragma once
 #include "common.h"
@@ -20,12 +20,14 @@ struct DArgs {
   const bf16* b;
   int64_t lda, ldb, M, N, K, kper;
   int split, nbm, nbn;
-  int nfast;  // 1: consecutive tiles walk N (the few column tiles of a tall GEMM share one A row
-              // block, so A streams from HBM once instead of once per column tile)
+  int nfast;  // 1: tall GEMM (AST linears: M = tokens, few column tiles): grouped tile order, see gm
+  int gm;     // row blocks per group in the grouped order: within a group the column tiles are walked
+              // slowest, so the group's A rows (gm x 128 x K) stay in the XCD's L2 across all column
+              // tiles while each B column tile serves gm consecutive blocks; sized so gm A row blocks
+              // fit ~2 MB.  (A pure N-fastest walk re-fetched all of B from the Infinity Cache once per
+              // row block per XCD: ~8-11 GB per AST launch.)
   float* ws;
   EpiDev e;
-  int nt;      // full-tile f32 epilogue with non-temporal stores
-  int full16;  // full-tile bf16 epilogue allowed
 };
 
 // -------------------------------------------------------------------------- epilogue
@@ -172,8 +174,6 @@ struct W8Args {
 };
 hipError_t wgrad8_launch(const W8Args& a, hipStream_t s);
 
-// 256x256-tile dense bf16 GEMM (dgemm256.hip); la/lb = MIA_LAYOUT_KC / MIA_LAYOUT_RC.
-hipError_t dgemm256_launch(const DArgs& d, int la, int lb, hipStream_t s);
-bool dgemm256_pays(int64_t M, int64_t N, int split);
+
 
 }  // namespace mgemm

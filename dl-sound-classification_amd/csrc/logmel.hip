@@ -195,7 +195,9 @@ __global__ __launch_bounds__(256) void fft_mel_db_kernel(const float* __restrict
       const int ks = bs[m], kl = bl[m], off = bo[m];
       float acc = 0.f;
       for (int i = 0; i < kl; ++i) acc = fmaf(P[ks + i], bwp[off + i], acc);
-      const float db = 10.f * log10f(fmaxf(acc, 1e-10f));  // AmplitudeToDB (multiplier 10, amin 1e-10)
+      // AmplitudeToDB (multiplier 10, amin 1e-10): the floor is the exact torch value (-100.0f; f32
+      // log10f is 1 ulp low there), so an all-silent clip stays constant (std 0: no normalisation)
+      const float db = acc <= 1e-10f ? -100.f : 10.f * log10f(acc);
       tile[m][fi] = db;
       lmax = fmaxf(lmax, db);
     }

@@ -5,8 +5,6 @@ workspaces).  Shapes are validated here, geometry is validated again in the libr
 """
 from __future__ import annotations
 
-import os
-
 import math
 from dataclasses import dataclass
 
@@ -367,7 +365,7 @@ def conv3_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, n: int, h: 
     assert x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and dw.dtype == torch.float32
     assert x.numel() == n * h * wd and dy.numel() == n * oh * ow * 32 and dw.numel() == 32 * 64
     assert x.is_contiguous() and dy.is_contiguous() and dw.is_contiguous()
-    nw = int(os.environ.get("MIA_CONV3W_WAVES", 4096))
+    nw = 4096
     part = workspace(nw * 2048 * 4 + 64 * 2048 * 8, x.device, "conv3w")
     with probe(tag or "", 2.0 * n * oh * ow * 32 * 64, x.numel() * 2 + dy.numel() * 2):
         L.check(L.load().mia_conv3_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), part.data_ptr(), nw, n, h, wd,

@@ -14,7 +14,6 @@ Reference op sequence: src/models/envnet_v2.py:14-85.
 from __future__ import annotations
 
 import itertools
-import os
 
 import torch
 
@@ -25,10 +24,9 @@ _SEED = itertools.count(0x5EED)
 
 
 def _use_conv8(cd: int, cin: int, cout: int, kh: int, kw: int) -> bool:
-    """conv4 (32 -> 32, 8x8) forward / backward-data on the row-rolling kernel (csrc/conv8.hip);
-    MIA_CONV8=0 selects the row-window implicit GEMM instead (both HIP)."""
-    return (cd == L.BF16 and cin == 32 and cout == 32 and kh == 8 and kw == 8
-            and os.environ.get("MIA_CONV8", "1") != "0")
+    """conv4 (32 -> 32, 8x8) forward / backward-data on the row-rolling kernel (csrc/conv8.hip) in
+    bf16; the f32 parity path runs the generic row-window implicit GEMM."""
+    return cd == L.BF16 and cin == 32 and cout == 32 and kh == 8 and kw == 8
 
 # (conv module path, bn module path, cin, cout, kh, kw)
 TRUNK = [
@@ -158,7 +156,7 @@ class EnvNetFunction(torch.autograd.Function):
         # ---- maxpool (1,64) of relu(bn2(y2)), written as the transposed trunk image (B, 64, Wp)
         X0 = torch.empty(B, 64, Wp, dtype=tdt, device=dev)
         am0 = torch.empty(B, Wp, 64, dtype=torch.uint8, device=dev)
-        if cd == L.BF16 and training and os.environ.get("MIA_POOL_RAW", "1") != "0":
+        if cd == L.BF16 and training:
             # one pass over y2: window winners on the raw values (monotone BN+ReLU) + BN2 statistics,
             # then the pooled relu(bn2(winner)) once the statistics are final
             win0 = torch.empty(B, Wp, 64, dtype=tdt, device=dev)
@@ -382,8 +380,7 @@ class EnvNetFunction(torch.autograd.Function):
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
                 K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, K.pack_weight(p[pa], cd, 0),
                                dWa, dinp, tag=f"t{blk}a")
-            elif (cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0
-                  and os.environ.get("MIA_CONV3W", "1") != "0"):
+            elif cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0:
                 # conv3 weight gradient: wave-persistent, dY read once (csrc/conv3w.hip)
                 K.conv3_wgrad(ts["inp"], dya, dWa, B, H, W, tag=f"t{blk}a.wgrad")
             else:

@@ -89,7 +89,7 @@ def test_envnet_bf16_train_step_vs_autocast_oracle(cuda):
 
     r16, r32 = ref(True), ref(False)
     _check("envnet", z.detach().float(), float(loss), float(opt.last_total_norm), deltas, grads, r16, r32,
-           tol={"logits": 0.25, "loss": 0.05, "gradnorm": 0.15, "sign": 0.90})
+           tol={"logits": 0.2, "loss": 0.03, "gradnorm": 0.03, "sign": 0.95})  # measured 0.134 / 0.010 / 0.009 / 0.973
 
 
 def test_ast_depth2_bf16_train_step_vs_autocast_oracle(cuda):
@@ -128,4 +128,4 @@ def test_ast_depth2_bf16_train_step_vs_autocast_oracle(cuda):
 
     r16, r32 = ref(True), ref(False)
     _check("ast", probs.detach().float(), float(loss), float(opt.last_total_norm), deltas, grads, r16, r32,
-           tol={"logits": 0.05, "loss": 0.01, "gradnorm": 0.1, "sign": 0.95})
+           tol={"logits": 0.015, "loss": 0.002, "gradnorm": 0.006, "sign": 0.99})  # measured 0.0037 / 0.0004 / 0.0015 / 1.0

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 from src.miaudio import lib as L  # noqa: E402
 
 B, N, H, D = int(os.environ.get("BATCH", 64)), 1645, 12, 64
+ITERS = int(os.environ.get("ITERS", 10))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 qkv = torch.randn(B * N, 3 * H * D, generator=g, device=dev).to(torch.bfloat16)
@@ -39,9 +40,9 @@ for name, fn, fl in (("fwd", fwd, flop_f), ("bwd", bwd, 2.5 * flop_f)):
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(10):
+    for _ in range(ITERS):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 10
+    ms = e0.elapsed_time(e1) / ITERS
     print(f"attn.{name} B={B} {ms:7.3f} ms {fl / ms / 1e9:7.1f} TF/s ({100 * fl / ms / 1e9 / 2500:.1f}% of 2.5 PF)", flush=True)
