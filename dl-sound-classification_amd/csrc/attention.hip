@@ -48,6 +48,9 @@ __device__ __forceinline__ void stage64(bf16* lds, const bf16* g, int64_t ld, in
   }
 }
 
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int sw_off(int r, int col) { return r * 64 + (((col >> 3) ^ swz(r)) << 3) + (col & 7); }
+
 // Register-staged tile copy, split so the global loads of tile t+1 fly under tile t's MFMAs
 // (issue early / write late): 64 rows x 64 bf16 = 2 x 16 B per thread.
 struct Stage64 {
@@ -60,6 +63,14 @@ struct Stage64 {
       const int c = t + 256 * s;
       const int row = min(c >> 3, nvalid - 1), c16 = c & 7;
       v[s] = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
+    }
+  }
+  __device__ __forceinline__ void store_sw(bf16* lds, int t) const {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = t + 256 * s;
+      const int r = c >> 3;
+      *reinterpret_cast<uint4*>(lds + r * 64 + (((c & 7) ^ swz(r)) << 3)) = v[s];
     }
   }
   template <int ROW = LROW>
@@ -88,6 +99,26 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int k0, int c0, int l
   const bf16* p1 = p0 + 8 * ROW;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
+  s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+// Swizzled [rows][64] bf16 tile for a tile read BOTH as rows (ds_read_b128) and transposed
+// (ds_read_b64_tr_b16): 16-B chunk c of row r sits at chunk c ^ swz(r).  Rows r, r + 1 use opposite
+// bank halves (128-B rows); over the 8 same-parity rows of a ds_read_b128 16-lane group swz takes 8
+// distinct values, and rows r, r + 2 of a transposed read differ in swz bit 2, so their 4-chunk
+// column blocks land in opposite 64-B halves: both kinds of read are conflict-free, no padding.
+
+__device__ __forceinline__ bf16x8 frag_row_sw(const bf16* lds, int row, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(lds + sw_off(row, ks * 16 + 8 * (lane >> 5)));
+}
+
+__device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* lds, int k0, int c0, int lane) {
+  const int i16 = lane & 15, g = lane >> 4, h = lane >> 5;
+  const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
+  const int r = k0 + 4 * h + (i16 >> 2);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(lds + sw_off(r, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(lds + sw_off(r + 8, col)));
   s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, c);
 }
@@ -335,8 +366,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                             int N, int H, int nkb, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Qs[2][64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Gs[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Qs[2][64 * 64];
+  __shared__ __attribute__((aligned(16))) bf16 Gs[2][64 * 64];
   __shared__ __attribute__((aligned(16))) float Ls[2][64];
   __shared__ __attribute__((aligned(16))) float Ds[2][64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -375,8 +406,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
     }
   };
   auto store_rows = [&](int buf) __attribute__((always_inline)) {
-    qreg.store(Qs[buf], t);
-    greg.store(Gs[buf], t);
+    qreg.store_sw(Qs[buf], t);
+    greg.store_sw(Gs[buf], t);
     if (t < 64) { Ls[buf][t] = lreg; Ds[buf][t] = dreg; }
   };
   load_rows(0);
@@ -395,8 +426,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
         sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8 qa = frag_row(Q_, sq * 32 + (lane & 31), ks, lane);
-          const bf16x8 ga = frag_row(G_, sq * 32 + (lane & 31), ks, lane);
+          const bf16x8 qa = frag_row_sw(Q_, sq * 32 + (lane & 31), ks, lane);
+          const bf16x8 ga = frag_row_sw(G_, sq * 32 + (lane & 31), ks, lane);
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
             sc[g] = mfma(qa, kf[g][ks], sc[g]);
@@ -424,8 +455,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
           bf16x8 tg[2], tq[2];
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) {
-            tg[dh] = frag_tr(G_, sq * 32 + 16 * sk, 32 * dh, lane);
-            tq[dh] = frag_tr(Q_, sq * 32 + 16 * sk, 32 * dh, lane);
+            tg[dh] = frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane);
+            tq[dh] = frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane);
           }
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
@@ -470,14 +501,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 }
 
 // Query-parallel dQ: each wave owns 64 queries as two 32-query groups (256 per block), sweeps 64-key
-// tiles (K, V in LDS), recomputes S^T and dP^T with the query on the lane and accumulates dQ^T; every
-// K / V fragment read feeds both query groups.
+// tiles (K swizzled for its row AND transposed reads, V row-read only), recomputes S^T and dP^T with
+// the query on the lane and accumulates dQ^T; every K / V fragment read feeds both query groups.
 constexpr int BWD_Q = 256;
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           bf16* __restrict__ dqkv, int N, int H, int nqb, float scale,
                                                           float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * 64];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
@@ -507,7 +538,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   Stage64 kreg, vreg;
   kreg.load(base + H * D, ldt, N, t);
   vreg.load(base + 2 * H * D, ldt, N, t);
-  kreg.store(Ks[0], t);
+  kreg.store_sw(Ks[0], t);
   vreg.store(Vs[0], t);
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
@@ -524,7 +555,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8 ka = frag_row(K_, st * 32 + (lane & 31), ks, lane);
+          const bf16x8 ka = frag_row_sw(K_, st * 32 + (lane & 31), ks, lane);
           const bf16x8 va = frag_row(V_, st * 32 + (lane & 31), ks, lane);
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
@@ -544,7 +575,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         for (int sk = 0; sk < 2; ++sk) {
           bf16x8 tk[2];
 #pragma unroll
-          for (int dh = 0; dh < 2; ++dh) tk[dh] = frag_tr(K_, st * 32 + 16 * sk, 32 * dh, lane);
+          for (int dh = 0; dh < 2; ++dh) tk[dh] = frag_tr_sw(K_, st * 32 + 16 * sk, 32 * dh, lane);
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
             const bf16x8 df = acc_frag(dp[g], sk);
@@ -554,7 +585,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         }
       }
     }
-    kreg.store(Ks[(kt + 1) & 1], t);
+    kreg.store_sw(Ks[(kt + 1) & 1], t);
     vreg.store(Vs[(kt + 1) & 1], t);
     __syncthreads();
   }
