@@ -33,7 +33,7 @@ __device__ __forceinline__ int64_t out_index(int layout, int b, int oy, int ox, 
 __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x, int dtype, int n, int H, int W,
                                                       int C, int kh, int kw, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, void* out, int layout,
-                                                      uint8_t* __restrict__ argmax) {
+                                                      uint8_t* __restrict__ argmax, void* __restrict__ win) {
   const int OH = H / kh, OW = W / kw, G = C / 8;
   const int total = n * OH * OW * G;  // < 2^31 (checked by the launcher): 32-bit index math
   for (int idx = blockIdx.x * NT + threadIdx.x; idx < total; idx += gridDim.x * NT) {
@@ -43,13 +43,14 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
     p /= OW;
     const int oy = p % OH;
     const int b = p / OH;
-    float sc[8], sh[8], best[8];
+    float sc[8], sh[8], best[8], raw[8];
     int arg[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       sc[i] = scale ? scale[cg * 8 + i] : 1.f;
       sh[i] = shift ? shift[cg * 8 + i] : 0.f;
       best[i] = -INFINITY;
+      raw[i] = 0.f;
       arg[i] = 0;
     }
     for (int dy = 0; dy < kh; ++dy) {
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float v = fmaxf(fmaf(f[i], sc[i], sh[i]), 0.f);
-          if (v > best[i]) { best[i] = v; arg[i] = pos; }
+          if (v > best[i]) { best[i] = v; raw[i] = f[i]; arg[i] = pos; }
         }
       }
     }
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
 #pragma unroll
     for (int i = 0; i < 4; ++i) { a0 |= (uint32_t)arg[i] << (8 * i); a1 |= (uint32_t)arg[i + 4] << (8 * i); }
     *reinterpret_cast<uint2*>(argmax + aoff) = make_uint2(a0, a1);
+    if (win) store8(win, dtype, aoff, raw);  // the winner's raw x (exact: x's own dtype) for the backward
 #pragma unroll
     for (int i = 0; i < 8; ++i) st_elem(out, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C), best[i]);
   }
@@ -269,9 +271,13 @@ __global__ __launch_bounds__(NT) void pool_bwd_kernel(const void* __restrict__ d
 // a gradient, so dbeta = sum g and dgamma = sum g * xhat are gathered per pooled cell (one thread =
 // one (pooled cell, 8-channel group)) without touching the other kh*kw - 1 pixels of the window.
 // gm[cell][c] (f32, NHWC cells) keeps the ReLU-masked gradient at the argmax for the dense pass.
+// win (optional, NHWC cells, x's dtype): the raw winner value of each cell saved by the forward
+// (pool_raw_stats); when given, x is not gathered at all -- a contiguous read replaces kh*kw-strided
+// 2-byte gathers that each touch a separate cache line.
 __global__ __launch_bounds__(NT) void pool_bwd_sparse_kernel(const void* __restrict__ dout, int layout,
                                                              const uint8_t* __restrict__ argmax,
-                                                             const void* __restrict__ x, int dtype, int n, int H,
+                                                             const void* __restrict__ x,
+                                                             const void* __restrict__ win, int dtype, int n, int H,
                                                              int W, int C, int kh, int kw,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift,
@@ -294,15 +300,22 @@ __global__ __launch_bounds__(NT) void pool_bwd_sparse_kernel(const void* __restr
     const int q = cell / OW;
     const int oy = q % OH;
     const int b = q / OH;
-    const uint2 am = *reinterpret_cast<const uint2*>(argmax + (int64_t)cell * C + cg * 8);
     float xv[8], dv[8];
+    if (win) {
+      const int64_t off = (int64_t)cell * C + cg * 8;
+      load8(win, dtype, off, xv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {  // all loads first, unconditionally
-      const uint32_t word = i < 4 ? am.x : am.y;
-      const int a = (int)((word >> (8 * (i & 3))) & 0xffu);
-      const int iy = oy * kh + a / kw, ix = ox * kw + a % kw;
-      xv[i] = ld_elem(x, dtype, (((int64_t)b * H + iy) * W + ix) * C + cg * 8 + i);
-      dv[i] = ld_elem(dout, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C));
+      for (int i = 0; i < 8; ++i) dv[i] = ld_elem(dout, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C));
+    } else {
+      const uint2 am = *reinterpret_cast<const uint2*>(argmax + (int64_t)cell * C + cg * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // all loads first, unconditionally
+        const uint32_t word = i < 4 ? am.x : am.y;
+        const int a = (int)((word >> (8 * (i & 3))) & 0xffu);
+        const int iy = oy * kh + a / kw, ix = ox * kw + a % kw;
+        xv[i] = ld_elem(x, dtype, (((int64_t)b * H + iy) * W + ix) * C + cg * 8 + i);
+        dv[i] = ld_elem(dout, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C));
+      }
     }
     float gv[8];
 #pragma unroll
@@ -532,14 +545,16 @@ __global__ void col2im_rows_kernel(const float* __restrict__ p, int n, int ph, i
 
 extern "C" int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh,
                             int32_t kw, const float* scale, const float* shift, void* out, int32_t out_layout,
-                            uint8_t* argmax, mia_stream_t stream) {
+                            uint8_t* argmax, void* win, mia_stream_t stream) {
   MIA_CHECK_ARG(x && out && argmax, "pool_fwd: null pointer");
+  MIA_CHECK_ARG(!win || (reinterpret_cast<uintptr_t>(win) & 15) == 0, "pool_fwd: win alignment");
   MIA_CHECK_ARG(c % 8 == 0 && kh > 0 && kw > 0 && kh * kw <= 256 && h >= kh && w >= kw, "pool_fwd: bad geometry");
   MIA_CHECK_ARG(out_layout >= 0 && out_layout <= 2 && (out_layout != 1 || h / kh == 1), "pool_fwd: bad layout");
   MIA_CHECK_ARG((int64_t)n * h * w * (c / 8) < (1ll << 31), "pool_fwd: too many elements for 32-bit indexing");
   const int64_t total = (int64_t)n * (h / kh) * (w / kw) * (c / 8);
   const int nb = (int)std::min<int64_t>(cdiv(total, NT), 16384);
-  pool_fwd_kernel<<<nb, NT, 0, as_stream(stream)>>>(x, dtype, n, h, w, c, kh, kw, scale, shift, out, out_layout, argmax);
+  pool_fwd_kernel<<<nb, NT, 0, as_stream(stream)>>>(x, dtype, n, h, w, c, kh, kw, scale, shift, out, out_layout, argmax,
+                                                    win);
   MIA_LAUNCH_CHECK("pool_fwd");
   return 0;
 }
@@ -593,7 +608,7 @@ extern "C" int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout,
 }
 
 extern "C" int mia_pool_bwd_gather(const void* dout, int32_t out_layout, const uint8_t* argmax, const void* x,
-                                   int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
+                                   const void* win, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
                                    const float* scale, const float* shift, const float* mean, const float* invstd,
                                    float* gm, float* dgamma, float* dbeta, void* partial, mia_stream_t stream) {
   MIA_CHECK_ARG(dout && argmax && x && scale && shift && mean && invstd && gm && dgamma && dbeta && partial,
@@ -606,7 +621,8 @@ extern "C" int mia_pool_bwd_gather(const void* dout, int32_t out_layout, const u
   const int64_t cells = (int64_t)n * (h / kh) * (w / kw);
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(cells, (int64_t)rslots * 2), 1024));
   hipStream_t s = as_stream(stream);
-  pool_bwd_sparse_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, dtype, n, h, w, c, kh, kw, scale, shift, mean,
+  MIA_CHECK_ARG(!win || (reinterpret_cast<uintptr_t>(win) & 15) == 0, "pool_bwd_gather: win alignment");
+  pool_bwd_sparse_kernel<<<nb, NT, 0, s>>>(dout, out_layout, argmax, x, win, dtype, n, h, w, c, kh, kw, scale, shift, mean,
                                            invstd, gm, (float*)partial);
   MIA_LAUNCH_CHECK("pool_bwd_gather");
   partial_final_kernel<<<(unsigned)c, 256, 0, s>>>((const float*)partial, nb, c, dgamma, dbeta);

@@ -223,16 +223,19 @@ def bn_relu_bwd_apply(dact, x, dx, P, C, gamma, bn: BNState, dgamma, dbeta, dbia
                                       ws.data_ptr(), _s()), "mia_bn_relu_bwd_apply")
 
 
-def pool_bwd_gather(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn: BNState):
+def pool_bwd_gather(dout, out_layout, argmax, x, n, h, w, c, kh, kw, bn: BNState, win=None):
     """Sparse half of the pooled backward: (gm, dgamma, dbeta); gm = ReLU-masked gradient at each
-    pooled cell's argmax, f32 (n, h//kh, w//kw, c)."""
+    pooled cell's argmax, f32 (n, h//kh, w//kw, c).  ``win``: the raw winner values the forward
+    saved (pool_raw_stats), read instead of gathering x at the argmax positions."""
+    if win is not None and (win.dtype != x.dtype or win.numel() != n * (h // kh) * (w // kw) * c):
+        raise ValueError("pool_bwd_gather: win must hold one x-typed value per pooled cell and channel")
     dev = x.device
     g = torch.empty(2, c, dtype=torch.float32, device=dev)
     gm = torch.empty(n * (h // kh) * (w // kw), c, dtype=torch.float32, device=dev)
     lib = L.load()
     ws = workspace(lib.mia_bn_partial_bytes(n * h * w, c), dev, "bn")
-    L.check(lib.mia_pool_bwd_gather(dout.data_ptr(), out_layout, argmax.data_ptr(), x.data_ptr(), L.dtype_code(x),
-                                    n, h, w, c, kh, kw, bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
+    L.check(lib.mia_pool_bwd_gather(dout.data_ptr(), out_layout, argmax.data_ptr(), x.data_ptr(), L.ptr(win),
+                                    L.dtype_code(x), n, h, w, c, kh, kw, bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
                                     bn.invstd.data_ptr(), gm.data_ptr(), g[0].data_ptr(), g[1].data_ptr(),
                                     ws.data_ptr(), _s()), "mia_pool_bwd_gather")
     return gm, g[0], g[1]
@@ -248,9 +251,14 @@ def pool_bn_relu_bwd_apply(gm, argmax, x, n, h, w, c, kh, kw, gamma, bn: BNState
                                            ws.data_ptr(), _s()), "mia_pool_bn_relu_bwd_apply")
 
 
-def pool_fwd(x, n, h, w, c, kh, kw, bn: BNState, out, out_layout, argmax):
+def pool_fwd(x, n, h, w, c, kh, kw, bn: BNState, out, out_layout, argmax, win=None):
+    """maxpool(relu(bn(x))) with the argmax per cell; ``win`` (optional, x's dtype, one value per cell and
+    channel) receives the winner's raw x for pool_bwd_gather."""
+    if win is not None and (win.dtype != x.dtype or win.numel() != n * (h // kh) * (w // kw) * c):
+        raise ValueError("pool_fwd: win must hold one x-typed value per pooled cell and channel")
     L.check(L.load().mia_pool_fwd(x.data_ptr(), L.dtype_code(x), n, h, w, c, kh, kw, bn.scale.data_ptr(),
-                                  bn.shift.data_ptr(), out.data_ptr(), out_layout, argmax.data_ptr(), _s()),
+                                  bn.shift.data_ptr(), out.data_ptr(), out_layout, argmax.data_ptr(), L.ptr(win),
+                                  _s()),
             "mia_pool_fwd")
 
 

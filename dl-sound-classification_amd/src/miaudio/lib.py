@@ -63,11 +63,11 @@ SIGNATURES = {
     "mia_bn_relu_bwd_reduce": (C.c_int, [vp, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mia_bn_bwd_apply": (C.c_int, [vp, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mia_bn_relu_bwd_apply": (C.c_int, [vp, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "mia_pool_bwd_gather": (C.c_int, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp,
+    "mia_pool_bwd_gather": (C.c_int, [vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp,
                                       vp, vp, vp]),
     "mia_pool_bn_relu_bwd_apply": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp,
                                              vp, vp, vp]),
-    "mia_pool_fwd": (C.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
+    "mia_pool_fwd": (C.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp]),
     "mia_pool_bwd_bn_relu_reduce": (C.c_int, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp,
                                               vp, vp, vp, vp, vp, vp]),
     "mia_colsum": (C.c_int, [vp, i32, i64, i32, i64, vp, vp, vp]),

@@ -169,7 +169,8 @@ class EnvNetFunction(torch.autograd.Function):
             bn2 = bn(1, y2, B * W2, 64)
             K.pool_fwd(y2, B, 1, W2, 64, 1, 64, bn2, X0, 1, am0)
         fe.__exit__(None, None, None)
-        saved.update(x=x, y1=y1, y2=y2, bn1=bn1, bn2=bn2, X0=X0, am0=am0)
+        saved.update(x=x, y1=y1, y2=y2, bn1=bn1, bn2=bn2, X0=X0, am0=am0,
+                     win0=win0 if cd == L.BF16 and training else None)
 
         # ---- trunk
         inp = X0
@@ -236,8 +237,9 @@ class EnvNetFunction(torch.autograd.Function):
             pooled = torch.empty(B, cout2, hp, wp, dtype=tdt, device=dev) if last else \
                 torch.empty(B * hp * wp + 1, cout2, dtype=tdt, device=dev)[: B * hp * wp].view(B, hp, wp, cout2)
             am = torch.empty(B, hp, wp, cout2, dtype=torch.uint8, device=dev)
-            K.pool_fwd(yb, B, hb, wb, cout2, ph, pw, bnb, pooled, 2 if last else 0, am)
-            trunk_saved.append(dict(inp=inp, ya=ya, yb=yb, bna=bna, bnb=bnb, am=am, act=act))
+            win = torch.empty(B, hp, wp, cout2, dtype=tdt, device=dev) if training else None
+            K.pool_fwd(yb, B, hb, wb, cout2, ph, pw, bnb, pooled, 2 if last else 0, am, win=win)
+            trunk_saved.append(dict(inp=inp, ya=ya, yb=yb, bna=bna, bnb=bnb, am=am, act=act, win=win))
             inp = pooled
         flat = inp.reshape(B, -1)
         saved["trunk"] = trunk_saved
@@ -333,7 +335,8 @@ class EnvNetFunction(torch.autograd.Function):
             Pb = B * hb * wb
             lay = 2 if blk == 3 else 0
             # reductions gathered at the argmax positions, then one dense pass x -> dy
-            gm, dgb, dbb = K.pool_bwd_gather(dpool, lay, ts["am"], ts["yb"], B, hb, wb, cout2, ph, pw, ts["bnb"])
+            gm, dgb, dbb = K.pool_bwd_gather(dpool, lay, ts["am"], ts["yb"], B, hb, wb, cout2, ph, pw, ts["bnb"],
+                                             win=ts["win"])
             grads[pa + 6], grads[pa + 7] = dgb, dbb
             dyb = torch.empty(Pb, cout2, dtype=tdt, device=dev)
             dbias_b = torch.empty(cout2, dtype=torch.float32, device=dev)
@@ -424,7 +427,7 @@ class EnvNetFunction(torch.autograd.Function):
         fe.__enter__()
         W1, W2, Wp = g["W1"], g["W2"], g["Wp"]
         P2, P1 = B * W2, B * W1
-        gm, dg2, db2 = K.pool_bwd_gather(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"])
+        gm, dg2, db2 = K.pool_bwd_gather(dpool, 1, s["am0"], s["y2"], B, 1, W2, 64, 1, 64, s["bn2"], win=s["win0"])
         grads[6], grads[7] = dg2, db2
         dy2 = torch.empty(P2, 64, dtype=tdt, device=dev)
         dbias2 = torch.empty(64, dtype=torch.float32, device=dev)

@@ -149,7 +149,8 @@ int mia_bn_relu_bwd_apply(const void* dact, const void* x, void* dx, int32_t dty
  * argmax: (n, oh, ow, c) u8 window offset of the max. */
 int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c,
                  int32_t kh, int32_t kw, const float* scale, const float* shift, void* out,
-                 int32_t out_layout, uint8_t* argmax, mia_stream_t stream);
+                 int32_t out_layout, uint8_t* argmax, void* win /* optional: raw winner x per cell, or NULL */,
+                 mia_stream_t stream);
 /* Forward of maxpool(relu(bn(x))) split around the BN statistics (training, bf16 x (n, h, w, c) NHWC):
  * mia_pool_raw_stats reads x once and writes each window's winner (raw bf16 value; raw max for gamma > 0,
  * raw min for gamma < 0, first position for gamma == 0; first occurrence on ties), its argmax (u8, as
@@ -175,6 +176,7 @@ int mia_pool_bwd_bn_relu_reduce(const void* dout, int32_t out_layout, const uint
  * reductions dgamma = sum gm*xhat, dbeta = sum gm (the other kh*kw-1 window pixels carry no
  * gradient and are never read).  Replaces autograd of nn.MaxPool2d + nn.ReLU (envnet_v2.py:16-23). */
 int mia_pool_bwd_gather(const void* dout, int32_t out_layout, const uint8_t* argmax, const void* x,
+                        const void* win /* optional raw winners (n, h/kh, w/kw, c), x's dtype, or NULL */,
                         int32_t dtype, int32_t n, int32_t h, int32_t w, int32_t c, int32_t kh, int32_t kw,
                         const float* scale, const float* shift, const float* mean, const float* invstd,
                         float* gm, float* dgamma, float* dbeta, void* partial, mia_stream_t stream);

@@ -357,3 +357,56 @@ def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     assert (out1.float() - out2.float()).abs().max() <= 2e-2 * out2.float().abs().max()
     pos = out2 > 0
     assert torch.equal(am1[pos], am2[pos])
+
+
+@pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64), (3, 1, 1001, 64, 1, 64)])
+def test_pool_bwd_gather_raw_winners_bit_identical(cuda, geom):
+    """The frontend backward reads the forward's raw winners (pool_raw_stats `win`) instead of
+    gathering y2 at the argmax: gm, dgamma, dbeta must be bit-identical to the gathered version."""
+    n, h, w, c, kh, kw = geom
+    g = torch.Generator().manual_seed(w + 7)
+    y = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(cuda)
+    gamma = (torch.rand(c, generator=g) - 0.3).to(cuda)  # mixed signs: min- and max-winners
+    kshift = (torch.randn(c, generator=g) * 0.1).to(cuda)
+    oh, ow = h // kh, w // kw
+    win = torch.empty(n, oh, ow, c, dtype=torch.bfloat16, device=cuda)
+    am = torch.empty(n, oh, ow, c, dtype=torch.uint8, device=cuda)
+    K.pool_raw_stats(y, n, h, w, c, kh, kw, gamma, kshift, win, am)
+    st = K.BNState((torch.randn(c, generator=g) * 0.1).to(cuda), (torch.rand(c, generator=g) + 0.5).to(cuda),
+                   gamma.clone(), (torch.randn(c, generator=g) * 0.3).to(cuda))
+    dout = torch.randn(n, c, oh * ow, generator=g).to(torch.bfloat16).to(cuda)
+    ref = K.pool_bwd_gather(dout, 1, am, y, n, h, w, c, kh, kw, st)
+    ref = [t.clone() for t in ref]
+    got = K.pool_bwd_gather(dout, 1, am, y, n, h, w, c, kh, kw, st, win=win)
+    torch.cuda.synchronize()
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("geom", [(2, 10, 33, 32, 5, 3), (3, 2, 41, 64, 1, 2)])
+def test_pool_fwd_raw_winners_feed_gather_bit_identical(cuda, geom, dtype):
+    """pool_fwd's optional raw-winner output (trunk pools) == x at the argmax, and the gather reading
+    it is bit-identical to the gather over x."""
+    n, h, w, c, kh, kw = geom
+    g = torch.Generator().manual_seed(h * w)
+    y = torch.randn(n, h, w, c, generator=g).to(dtype).to(cuda)
+    st = K.BNState((torch.randn(c, generator=g) * 0.1).to(cuda), (torch.rand(c, generator=g) + 0.5).to(cuda),
+                   (torch.rand(c, generator=g) - 0.3).to(cuda), (torch.randn(c, generator=g) * 0.3).to(cuda))
+    oh, ow = h // kh, w // kw
+    out = torch.empty(n, oh, ow, c, dtype=dtype, device=cuda)
+    am = torch.empty(n, oh, ow, c, dtype=torch.uint8, device=cuda)
+    win = torch.empty(n, oh, ow, c, dtype=dtype, device=cuda)
+    K.pool_fwd(y, n, h, w, c, kh, kw, st, out, 0, am, win=win)
+    a = am.long().cpu()
+    iy = torch.arange(oh)[None, :, None, None] * kh + a // kw
+    ix = torch.arange(ow)[None, None, :, None] * kw + a % kw
+    yc = y.cpu()
+    exp = yc[torch.arange(n)[:, None, None, None], iy, ix, torch.arange(c)[None, None, None, :]]
+    assert torch.equal(win.cpu(), exp)
+    dout = torch.randn(n, oh, ow, c, generator=g).to(dtype).to(cuda)
+    ref = [t.clone() for t in K.pool_bwd_gather(dout, 0, am, y, n, h, w, c, kh, kw, st)]
+    got = K.pool_bwd_gather(dout, 0, am, y, n, h, w, c, kh, kw, st, win=win)
+    torch.cuda.synchronize()
+    for u, v in zip(got, ref):
+        assert torch.equal(u, v)

@@ -18,3 +18,7 @@ T = sum(tot.values())
 print(f"step kernel time {T / 1e3:.2f} ms, {e - s} launches")
 for n, v in sorted(tot.items(), key=lambda x: -x[1])[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
     print(f"{v / 1e3:8.2f} ms {cnt[n]:4d}x {100 * v / T:5.1f}%  {n}")
+if len(sys.argv) > 4:  # individual launches of the kernels whose name contains argv[4]
+    for r in rows[s:e]:
+        if sys.argv[4] in r["Kernel_Name"]:
+            print(f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.1f} us  {r['Kernel_Name'][:60]}")
