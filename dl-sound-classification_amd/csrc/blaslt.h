@@ -1,0 +1,25 @@
+// Library path of mia_gemm: plain dense bf16 GEMMs (no fused pre-op, epilogue = bias / ReLU /
+// residual add / f32 output) may run on hipBLASLt instead of the hand-written tile kernels.  The
+// fused GEMMs (GELU_SAVE, dGELU, ReLU-mask backward, row maps, implicit convolutions) never do.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/miaudio.h"
+
+namespace mblas {
+
+// operands/epilogue expressible as one hipBLASLt matmul with identical semantics
+bool eligible(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+              int compute);
+// run it (plan + heuristic algorithm cached per shape/layout/epilogue key and device)
+int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+        hipStream_t s);
+// MIA_GEMM_POLICY_* (mia_gemm_set_policy)
+int policy();
+// auto policy: the measured winner for this key on this device, -1 = not measured yet, 0 = tile
+// kernel, 1 = library
+int choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K);
+void set_choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+                int v);
+
+}  // namespace mblas

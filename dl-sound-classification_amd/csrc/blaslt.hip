@@ -1,0 +1,263 @@
+// hipBLASLt path of mia_gemm (see blaslt.h): plain dense bf16 GEMMs of the AST linears and the
+// EnvNet-v2 FC layers (reference: timm Block qkv/proj/fc1/fc2 under ast.py:38,60-61 and
+// envnet_v2.py:51,55,59 -- nn.Linear forward, and the dgrad / wgrad GEMMs autograd runs for them).
+//
+// mia_gemm computes C[M][N] = act(alpha * A.B^T + bias) (+ aux) in ROW-major storage; hipBLASLt is
+// column-major, so the call is issued transposed: D' = C^T (N x M, ld = ldc) = op(B') op(A') with
+//   A' = the B operand: KC (N x K rows, ld) read as the column-major K x N matrix -> op T,
+//                       RC (K x N rows, ld) read as the column-major N x K matrix -> op N;
+//   B' = the A operand: KC (M x K) -> column-major K x M, op N;  RC (K x M) -> M x K, op T.
+// bias[n] is per row of D' (hipBLASLt's bias vector: length = rows of D); the residual add
+// (MIA_ACT_ADD_AUX) is beta = 1 with C = aux (same dtype and shape as the output).
+// The two GELU epilogues of the AST MLP keep the exact erf GELU of nn.GELU (hipBLASLt's GELU
+// epilogues are not used): GELU_SAVE (fc1 forward) = GEMM + bias into aux (the saved
+// pre-activation u), then one pass out = gelu(u); DACT_GELU (fc2 backward-data) = GEMM into out,
+// then one pass out *= gelu'(aux).  Both passes read/write 8 bf16 per lane (16-B accesses).
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
+#include "blaslt.h"
+#include "common.h"
+
+namespace mblas {
+namespace {
+
+constexpr size_t WS_BYTES = 64ull << 20;  // hipBLASLt workspace per device
+constexpr int MAX_DEV = 16;
+
+struct Key {
+  int64_t m, n, k, lda, ldb, ldc, ldaux;
+  int la, lb, odt, act, bias, adt;
+  bool operator==(const Key& o) const {
+    return m == o.m && n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldc == o.ldc && ldaux == o.ldaux &&
+           la == o.la && lb == o.lb && odt == o.odt && act == o.act && bias == o.bias && adt == o.adt;
+  }
+};
+struct KeyHash {
+  size_t operator()(const Key& k) const {
+    uint64_t h = 1469598103934665603ull;
+    const int64_t v[13] = {k.m, k.n, k.k, k.lda, k.ldb, k.ldc, k.ldaux, k.la, k.lb, k.odt, k.act, k.bias, k.adt};
+    for (int64_t x : v) h = (h ^ (uint64_t)x) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+};
+
+struct Dev {
+  hipblasLtHandle_t handle = nullptr;
+  void* ws = nullptr;
+  std::unordered_map<Key, Plan, KeyHash> plans;
+  std::unordered_map<Key, int, KeyHash> choice;
+};
+
+std::mutex g_mu;
+Dev g_dev[MAX_DEV];
+
+Key make_key(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K) {
+  Key k;
+  k.m = M; k.n = N; k.k = K; k.lda = A.ld; k.ldb = B.ld; k.ldc = E.ldc;
+  const bool has_aux = E.act == MIA_ACT_ADD_AUX || E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU;
+  k.ldaux = has_aux ? E.ldaux : 0;
+  k.la = A.layout; k.lb = B.layout; k.odt = E.dtype; k.act = E.act; k.bias = E.bias != nullptr;
+  k.adt = has_aux ? E.aux_dtype : -1;
+  return k;
+}
+
+hipDataType dt(int d) { return d == MIA_F32 ? HIP_R_32F : HIP_R_16BF; }
+
+#define LT_CHECK(call)                                                                   \
+  do {                                                                                   \
+    hipblasStatus_t st__ = (call);                                                       \
+    if (st__ != HIPBLAS_STATUS_SUCCESS) return mia::fail(-5, "hipBLASLt %s: status %d", #call, (int)st__); \
+  } while (0)
+
+int device_state(Dev** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return mia::fail(-(int)e, "hipGetDevice: %s", hipGetErrorString(e));
+  if (dev < 0 || dev >= MAX_DEV) return mia::fail(-22, "gemm library path: device %d out of range", dev);
+  Dev& d = g_dev[dev];
+  if (!d.handle) {
+    LT_CHECK(hipblasLtCreate(&d.handle));
+    e = hipMalloc(&d.ws, WS_BYTES);
+    if (e != hipSuccess) return mia::fail(-(int)e, "hipBLASLt workspace: %s", hipGetErrorString(e));
+  }
+  *out = &d;
+  return 0;
+}
+
+int make_plan(Dev& d, const Key& k, Plan& p) {
+  // D' = op(A') op(B'): m' = N, n' = M
+  const hipblasOperation_t opa = k.lb == MIA_LAYOUT_KC ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  const hipblasOperation_t opb = k.la == MIA_LAYOUT_KC ? HIPBLAS_OP_N : HIPBLAS_OP_T;
+  LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opb, sizeof(opb)));
+  hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_DEFAULT;
+  if (k.act == MIA_ACT_RELU) epi = k.bias ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_RELU;
+  else if (k.bias) epi = HIPBLASLT_EPILOGUE_BIAS;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+  if (k.bias) {
+    const hipDataType bt = HIP_R_32F;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
+  if (opa == HIPBLAS_OP_T) LT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k.k, k.n, k.ldb));
+  else LT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k.n, k.k, k.ldb));
+  if (opb == HIPBLAS_OP_N) LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k.k, k.m, k.lda));
+  else LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k.m, k.k, k.lda));
+  // GELU_SAVE: the GEMM writes the pre-activation into aux (ld = ldaux); C is unused (beta = 0)
+  const int64_t ldd = k.act == MIA_ACT_GELU_SAVE ? k.ldaux : k.ldc;
+  const int64_t ldcc = k.act == MIA_ACT_ADD_AUX ? k.ldaux : ldd;
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.ld, dt(k.odt), k.n, k.m, ldd));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lc, dt(k.odt), k.n, k.m, ldcc));
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  const uint64_t wsb = WS_BYTES;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int got = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d.handle, p.desc, p.la, p.lb, p.lc, p.ld, pref, 1, res,
+                                                              &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || got < 1)
+    return mia::fail(-5, "hipBLASLt: no algorithm for M=%lld N=%lld K=%lld (status %d)", (long long)k.m,
+                     (long long)k.n, (long long)k.k, (int)st);
+  p.algo = res[0].algo;
+  p.ws = res[0].workspaceSize;
+  return 0;
+}
+
+// rows x cols bf16 elementwise pass behind the GEMM: GELU_SAVE: out = gelu(src);
+// DACT_GELU: out = out * gelu'(src).  One thread per 8 contiguous columns.
+template <bool DACT>
+__global__ __launch_bounds__(256) void gelu_rows_kernel(const bf16* __restrict__ src, int64_t lds,
+                                                        bf16* __restrict__ out, int64_t ldo, int64_t rows,
+                                                        int64_t cols8) {
+  const int64_t total = rows * cols8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols8, c = (i - r * cols8) * 8;
+    const uint4 u = *reinterpret_cast<const uint4*>(src + r * lds + c);
+    bf16* o = out + r * ldo + c;
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (DACT) d = *reinterpret_cast<const uint4*>(o);
+    const uint32_t uw[4] = {u.x, u.y, u.z, u.w}, dw[4] = {d.x, d.y, d.z, d.w};
+    uint32_t ow[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float x = __uint_as_float(h ? (uw[q] & 0xffff0000u) : (uw[q] << 16));
+        if (DACT) v[h] = __uint_as_float(h ? (dw[q] & 0xffff0000u) : (dw[q] << 16)) * gelu_erf_grad(x);
+        else v[h] = gelu_erf(x);
+      }
+      const bf16 lo = (bf16)v[0], hi = (bf16)v[1];
+      ow[q] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(o) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
+}  // namespace
+
+int g_policy = MIA_GEMM_POLICY_AUTO;
+
+int policy() { return g_policy; }
+
+bool eligible(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+              int compute) {
+  if (compute != MIA_BF16 || M < 256 || N < 256 || K < 256) return false;
+  if (2.0 * (double)M * (double)N * (double)K < 1e10) return false;  // small GEMMs: the tile kernel
+  if (A.kind != MIA_OP_DENSE || B.kind != MIA_OP_DENSE || A.dtype != MIA_BF16 || B.dtype != MIA_BF16) return false;
+  if (A.pre != MIA_PRE_NONE || B.pre != MIA_PRE_NONE) return false;
+  if (A.layout == MIA_LAYOUT_KC) { if (A.rows != M || A.cols < K) return false; }
+  else { if (A.rows < K || A.cols != M) return false; }
+  if (B.layout == MIA_LAYOUT_KC) { if (B.rows != N || B.cols < K) return false; }
+  else { if (B.rows < K || B.cols != N) return false; }
+  if (E.dtype != MIA_F32 && E.dtype != MIA_BF16) return false;
+  if (E.accumulate || E.rm_inner || E.alpha != 1.f) return false;
+  if (E.act != MIA_ACT_NONE && E.act != MIA_ACT_RELU && E.act != MIA_ACT_ADD_AUX && E.act != MIA_ACT_GELU_SAVE &&
+      E.act != MIA_DACT_GELU)
+    return false;
+  if (E.act == MIA_ACT_ADD_AUX && (!E.aux || E.aux_dtype != E.dtype || E.aux == E.ptr)) return false;
+  if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
+    // bf16 activations, 16-B aligned rows for the elementwise pass; dGELU has no bias in the tile
+    // kernel's order either (v = acc * gelu'(u)), so a bias there is left to the tile kernel
+    if (!E.aux || E.aux == E.ptr || E.dtype != MIA_BF16 || E.aux_dtype != MIA_BF16 || (N & 7) || (E.ldc & 7) ||
+        (E.ldaux & 7) || (reinterpret_cast<uintptr_t>(E.ptr) & 15) || (reinterpret_cast<uintptr_t>(E.aux) & 15))
+      return false;
+    if (E.act == MIA_DACT_GELU && E.bias) return false;
+  }
+  // the auto policy runs both paths on the caller's buffers: the output must not alias an input
+  if (E.ptr == A.ptr || E.ptr == B.ptr) return false;
+  return true;
+}
+
+int choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_dev[dev].choice.find(make_key(A, B, E, M, N, K));
+  return it == g_dev[dev].choice.end() ? -1 : it->second;
+}
+
+void set_choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+                int v) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_dev[dev].choice[make_key(A, B, E, M, N, K)] = v;
+}
+
+int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+        hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Dev* d = nullptr;
+  if (int r = device_state(&d)) return r;
+  const Key k = make_key(A, B, E, M, N, K);
+  auto it = d->plans.find(k);
+  if (it == d->plans.end()) {
+    Plan p;
+    if (int r = make_plan(*d, k, p)) return r;
+    it = d->plans.emplace(k, p).first;
+  }
+  Plan& p = it->second;
+  if (k.bias) {
+    const void* bp = E.bias;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
+  }
+  const float alpha = 1.f, beta = E.act == MIA_ACT_ADD_AUX ? 1.f : 0.f;
+  void* dptr = E.act == MIA_ACT_GELU_SAVE ? const_cast<void*>(E.aux) : E.ptr;
+  const void* cptr = E.act == MIA_ACT_ADD_AUX ? E.aux : dptr;
+  LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
+                           &p.algo, d->ws, p.ws, s));
+  if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
+    const int64_t total = M * (N / 8);
+    const unsigned nb = (unsigned)std::min<int64_t>(cdiv(total, 256), 8192);
+    const bf16* src = reinterpret_cast<const bf16*>(E.aux);
+    bf16* out = reinterpret_cast<bf16*>(E.ptr);
+    if (E.act == MIA_ACT_GELU_SAVE) gelu_rows_kernel<false><<<nb, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, N / 8);
+    else gelu_rows_kernel<true><<<nb, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, N / 8);
+    MIA_LAUNCH_CHECK("gemm gelu pass");
+  }
+  return 0;
+}
+
+}  // namespace mblas
+
+extern "C" int mia_gemm_set_policy(int32_t policy) {
+  MIA_CHECK_ARG(policy >= MIA_GEMM_POLICY_TILE && policy <= MIA_GEMM_POLICY_AUTO, "gemm policy %d", (int)policy);
+  std::lock_guard<std::mutex> lk(mblas::g_mu);
+  mblas::g_policy = policy;
+  for (auto& d : mblas::g_dev) d.choice.clear();
+  return 0;
+}

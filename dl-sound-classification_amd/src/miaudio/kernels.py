@@ -99,6 +99,12 @@ def _tiles(M, N):
     return math.ceil(M / bm) * math.ceil(N / bn)
 
 
+def gemm_policy(policy: int) -> None:
+    """Which kernel runs the plain dense bf16 GEMMs: L.GEMM_POLICY_TILE (hand-written tile kernel),
+    L.GEMM_POLICY_LIB (hipBLASLt) or L.GEMM_POLICY_AUTO (default: timed once per shape, faster kept)."""
+    L.check(L.load().mia_gemm_set_policy(int(policy)), "mia_gemm_set_policy")
+
+
 def auto_split(M: int, N: int, K: int, target_blocks: int = 1024, min_k: int = 1024) -> int:
     tiles = _tiles(M, N)
     if tiles >= target_blocks:

@@ -93,6 +93,15 @@ int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int
  * 5 = dense bf16 GEMM with LDS-DMA staging (bf16 DENSE operands, K % 64 == 0, M, N >= 64). */
 int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                   int32_t compute_dtype, int32_t split_k);
+/* Dense bf16 GEMMs (DENSE bf16 operands, no pre-op, >= 10 GFLOP) whose epilogue is an optional f32
+ * bias + ReLU, a residual add, GELU_SAVE or dGELU (bf16), with bf16/f32 output, may run on hipBLASLt
+ * (path 6 above) instead of the tile kernel -- the GELU forms as the library GEMM plus one exact-erf
+ * elementwise pass: TILE = always the hand-written kernel, LIB = always hipBLASLt, AUTO (default) =
+ * the first call per (shape, layouts, epilogue) times both on the stream and keeps the faster.
+ * The other fused epilogues (GELU, ReLU-mask, row maps, accumulate) and the implicit convolutions
+ * always run on the tile kernels. */
+enum { MIA_GEMM_POLICY_TILE = 0, MIA_GEMM_POLICY_LIB = 1, MIA_GEMM_POLICY_AUTO = 2 };
+int mia_gemm_set_policy(int32_t policy);
 
 /* Fused log-mel: frame gather + 1024-pt real FFT (LDS) + |X|^2 + htk mel (sparse bands)
  * + 10log10 + per-clip top_db clamp + per-clip mean/unbiased-std normalisation.

@@ -418,25 +418,89 @@ def test_conv1ch_dgrad_bf16(cuda, n, oh, ow):
     assert rel(out.float().cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
-@pytest.mark.parametrize("M,N,Kd,split", [(4096, 3072, 256, 1), (4000, 3000, 192, 1), (3840, 3584, 1024, 3)])
-def test_dense256_layouts(cuda, monkeypatch, la, lb, M, N, Kd, split):
-    """The 256x256-tile LDS-DMA GEMM (opt-in: MIA_DGEMM256=1) vs a PyTorch fp32 matmul of the same
-    bf16 operands: every layout pair, ragged M/N edges, split-K slabs."""
-    monkeypatch.setenv("MIA_DGEMM256", "1")
-    g = torch.Generator(device=cuda).manual_seed(M + N + Kd)
+@pytest.fixture
+def policy():
+    """Set the plain-GEMM policy for one test and restore the default (auto) afterwards."""
+    yield K.gemm_policy
+    K.gemm_policy(L.GEMM_POLICY_AUTO)
+
+
+def _big_operands(cuda, la, lb, M, N, Kd, seed):
+    g = torch.Generator(device=cuda).manual_seed(seed)
     a = torch.randn(M, Kd, generator=g, device=cuda).to(torch.bfloat16)
     b = torch.randn(N, Kd, generator=g, device=cuda).to(torch.bfloat16)
     ta = a.contiguous() if la == L.KC else a.t().contiguous()
     tb = b.contiguous() if lb == L.KC else b.t().contiguous()
     A = K.dense(ta, L.KC, M, Kd) if la == L.KC else K.dense(ta, L.RC, Kd, M)
     Bo = K.dense(tb, L.KC, N, Kd) if lb == L.KC else K.dense(tb, L.RC, Kd, N)
+    return a, b, A, Bo, g
+
+
+@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB, L.GEMM_POLICY_AUTO])
+@pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
+@pytest.mark.parametrize("M,N,Kd,split", [(4096, 3072, 512, 1), (4000, 3000, 512, 1), (3840, 3584, 1024, 3)])
+def test_plain_gemm_policies(cuda, policy, pol, la, lb, M, N, Kd, split):
+    """Plain dense bf16 GEMM (bias + ReLU, bf16 out) on the tile kernel, on hipBLASLt and under the
+    timed auto choice vs a PyTorch fp32 matmul of the same bf16 operands: every layout pair, ragged
+    M/N edges, split-K slabs (tile path)."""
+    policy(pol)
+    a, b, A, Bo, g = _big_operands(cuda, la, lb, M, N, Kd, M + N + Kd)
+    path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, split)
+    assert path == (6 if pol == L.GEMM_POLICY_LIB else 5)
     bias = torch.randn(N, generator=g, device=cuda)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
-    K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_RELU, bias=bias), M, N, Kd, L.BF16, split_k=split)
     ref = torch.relu(a.float() @ b.float().t() + bias)
+    for _ in range(2):  # auto: the first call measures both paths, the second runs the cached winner
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_RELU, bias=bias), M, N, Kd, L.BF16, split_k=split)
+        torch.cuda.synchronize()
+        assert rel(out.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB])
+@pytest.mark.parametrize("case", ["wgrad_f32", "residual_f32", "bias_bf16", "gelu_save", "dact_gelu"])
+def test_plain_gemm_epilogues_both_paths(cuda, policy, pol, case):
+    """The epilogues the library path takes over, identical semantics on either path: f32 output of a
+    weight gradient (RC x RC), residual add into f32 with bias (AST proj/fc2 forward), bias only (qkv
+    forward), GELU_SAVE with bias (fc1 forward: erf GELU + saved pre-activation) and dGELU (fc2
+    backward-data: times gelu'(u), u = the saved pre-activation)."""
+    policy(pol)
+    if case == "wgrad_f32":
+        M, N, Kd, la, lb = 768, 2304, 8192, L.RC, L.RC
+    else:
+        M, N, Kd, la, lb = 8192, 768, 1024, L.KC, L.KC
+    a, b, A, Bo, g = _big_operands(cuda, la, lb, M, N, Kd, 11)
+    z = a.float() @ b.float().t()
+    bias = torch.randn(N, generator=g, device=cuda)
+    if case == "wgrad_f32":
+        out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N), M, N, Kd, L.BF16)
+        ref = z
+    elif case == "residual_f32":
+        res = torch.randn(M, N, generator=g, device=cuda)
+        out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_ADD_AUX, bias=bias, aux=res, ldaux=N), M, N, Kd, L.BF16)
+        ref = z + bias + res
+    elif case == "bias_bf16":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, bias=bias), M, N, Kd, L.BF16)
+        ref = z + bias
+    elif case == "gelu_save":
+        u = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_GELU_SAVE, bias=bias, aux=u, ldaux=N), M, N, Kd, L.BF16)
+        ref = F.gelu(z + bias)
+        torch.cuda.synchronize()
+        assert rel(u.float(), z + bias) < 1e-2
+    else:
+        u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N), M, N, Kd, L.BF16)
+        x = u.double().requires_grad_(True)
+        F.gelu(x).backward(torch.ones_like(x))
+        ref = z.double() * x.grad
     torch.cuda.synchronize()
-    assert rel(out.float(), ref) < 1e-2
+    tol = 1e-4 if out.dtype == torch.float32 else 1e-2
+    assert rel(out.float(), ref) < tol
 
 
 def test_wgrad8_many_items(cuda):

@@ -7,7 +7,11 @@ import torch
 T = int(os.environ.get("TOKENS", 105280))
 SHAPES = [("qkv.fwd", T, 2304, 768, 0, 0), ("fc1.fwd", T, 3072, 768, 0, 0), ("fc2.fwd", T, 768, 3072, 0, 0),
           ("proj.fwd", T, 768, 768, 0, 0), ("fc2.dgrad", T, 3072, 768, 0, 1), ("qkv.dgrad", T, 768, 2304, 0, 1),
-          ("fc1.wgrad", 3072, 768, T, 1, 1), ("qkv.wgrad", 2304, 768, T, 1, 1)]
+          ("fc1.wgrad", 3072, 768, T, 1, 1), ("qkv.wgrad", 2304, 768, T, 1, 1),
+          ("proj.dgrad", T, 768, 768, 0, 1), ("fc1.dgrad", T, 768, 3072, 0, 1), ("proj.wgrad", 768, 768, T, 1, 1),
+          ("fc2.wgrad", 768, 3072, T, 1, 1),
+          ("envfc1.fwd", 256, 4096, 84480, 0, 0), ("envfc1.dgrad", 256, 84480, 4096, 0, 1),
+          ("envfc1.wgrad", 4096, 84480, 256, 1, 1)]
 dev = torch.device("cuda:0")
 for name, M, N, Kd, la, lb in SHAPES:
     a = torch.randn(Kd, M, device=dev).to(torch.bfloat16).t() if la else torch.randn(M, Kd, device=dev).to(torch.bfloat16)
