@@ -137,33 +137,46 @@ int make_plan(Dev& d, const Key& k, Plan& p) {
 }
 
 // rows x cols bf16 elementwise pass behind the GEMM: GELU_SAVE: out = gelu(src);
-// DACT_GELU: out = out * gelu'(src).  One thread per 8 contiguous columns.
+// DACT_GELU: out = out * gelu'(src).  One thread per 8 contiguous columns; each block walks
+// GELU_ROWS rows (grid x) of one 2048-column slab (grid y) with all of a thread's 16-B loads issued before the math
+// (4 rows in flight per thread), no 64-bit index division.
+constexpr int GELU_ROWS = 4;
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
 template <bool DACT>
 __global__ __launch_bounds__(256) void gelu_rows_kernel(const bf16* __restrict__ src, int64_t lds,
                                                         bf16* __restrict__ out, int64_t ldo, int64_t rows,
-                                                        int64_t cols8) {
-  const int64_t total = rows * cols8;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / cols8, c = (i - r * cols8) * 8;
-    const uint4 u = *reinterpret_cast<const uint4*>(src + r * lds + c);
-    bf16* o = out + r * ldo + c;
-    uint4 d = make_uint4(0, 0, 0, 0);
-    if (DACT) d = *reinterpret_cast<const uint4*>(o);
-    const uint32_t uw[4] = {u.x, u.y, u.z, u.w}, dw[4] = {d.x, d.y, d.z, d.w};
+                                                        int cols8) {
+  const int c8 = blockIdx.y * 256 + threadIdx.x;
+  if (c8 >= cols8) return;
+  const int64_t r0 = (int64_t)blockIdx.x * GELU_ROWS;
+  uint4 u[GELU_ROWS], d[GELU_ROWS];
+#pragma unroll
+  for (int j = 0; j < GELU_ROWS; ++j) {
+    const int64_t r = r0 + j < rows ? r0 + j : rows - 1;  // clamped: the tail rows are not stored
+    u[j] = *reinterpret_cast<const uint4*>(src + r * lds + c8 * 8);
+    d[j] = DACT ? *reinterpret_cast<const uint4*>(out + r * ldo + c8 * 8) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < GELU_ROWS; ++j) {
+    if (r0 + j >= rows) break;
+    const uint32_t uw[4] = {u[j].x, u[j].y, u[j].z, u[j].w}, dw[4] = {d[j].x, d[j].y, d[j].z, d[j].w};
     uint32_t ow[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float x = __uint_as_float(h ? (uw[q] & 0xffff0000u) : (uw[q] << 16));
-        if (DACT) v[h] = __uint_as_float(h ? (dw[q] & 0xffff0000u) : (dw[q] << 16)) * gelu_erf_grad(x);
-        else v[h] = gelu_erf(x);
+      float lo, hi;
+      if (DACT) {
+        lo = bf_lo(dw[q]) * gelu_erf_grad(bf_lo(uw[q]));
+        hi = bf_hi(dw[q]) * gelu_erf_grad(bf_hi(uw[q]));
+      } else {
+        lo = gelu_erf(bf_lo(uw[q]));
+        hi = gelu_erf(bf_hi(uw[q]));
       }
-      const bf16 lo = (bf16)v[0], hi = (bf16)v[1];
-      ow[q] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      const bf16 bl = (bf16)lo, bh = (bf16)hi;
+      ow[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
     }
-    *reinterpret_cast<uint4*>(o) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    *reinterpret_cast<uint4*>(out + (r0 + j) * ldo + c8 * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
 }
 
@@ -241,12 +254,12 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
   LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
                            &p.algo, d->ws, p.ws, s));
   if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
-    const int64_t total = M * (N / 8);
-    const unsigned nb = (unsigned)std::min<int64_t>(cdiv(total, 256), 8192);
+    const dim3 grid((unsigned)cdiv(M, GELU_ROWS), (unsigned)cdiv(N / 8, 256));  // rows on x (< 2^31)
+    MIA_CHECK_ARG(cdiv(M, GELU_ROWS) < (1ll << 31), "gemm gelu pass: too many rows");
     const bf16* src = reinterpret_cast<const bf16*>(E.aux);
     bf16* out = reinterpret_cast<bf16*>(E.ptr);
-    if (E.act == MIA_ACT_GELU_SAVE) gelu_rows_kernel<false><<<nb, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, N / 8);
-    else gelu_rows_kernel<true><<<nb, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, N / 8);
+    if (E.act == MIA_ACT_GELU_SAVE) gelu_rows_kernel<false><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+    else gelu_rows_kernel<true><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
     MIA_LAUNCH_CHECK("gemm gelu pass");
   }
   return 0;
