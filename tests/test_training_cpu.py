@@ -366,3 +366,39 @@ def test_config1_envnet_cpu_plumbing(tmp_path, monkeypatch):
     del cfg["checkpoint"]  # a 4.4 GB checkpoint (weights + Adam state) is not what this test is about
     out = ts.train(cfg)
     assert set(out) >= {"test/acc", "test/loss"} and all(v == v for v in out.values())
+
+
+def test_multi_crop_test_through_engine_step(tmp_path):
+    """Multi-crop test evaluation (preprocessing_config multi_crop_test / test_crops; reference
+    esc50.py:208-214 + EnvNetPreprocessor.multi_crop_test, preprocessing.py:857-884): the test set
+    yields test_crops evenly spaced windows of the T/2-padded clip, collated as a list of batches,
+    and LitClassifier._step averages the model's logits over the crops before the loss
+    (reference engine.py:156-159).  Intended semantics: pad, then crop (the reference crops the raw
+    5 s clip -- one crop -- and pads it afterwards to 2x the window, which EnvNet's FC1 cannot take)."""
+    import torch.nn.functional as F
+    from src.training.engine import LitClassifier
+    torch.manual_seed(0)
+    waves = {}
+    for f in range(5):
+        d = tmp_path / f"fold_{f}"
+        d.mkdir()
+        for i in range(10):
+            w = torch.randn(1, 4410)
+            waves[(f, i)] = w
+            torch.save({"waveform": w, "label": i % 4}, d / f"{i}.pt")
+    dm = ESC50DataModule(root=str(tmp_path), fold=2, batch_size=3, num_workers=0, num_classes=4,
+                         preprocessing_config={"window_length": 0.1, "multi_crop_test": True, "test_crops": 3})
+    dm.setup("test")
+    xs, y = next(iter(dm.test_dataloader()))
+    assert isinstance(xs, list) and len(xs) == 3 and all(x.shape == (3, 1, 4410) for x in xs)
+    # crop k of clip 0 = padded clip [start_k : start_k + 4410], start_k = linspace(0, 4410, 3)
+    padded = F.pad(waves[(2, 0)], (2205, 2205))
+    for k, s in enumerate((0, 2205, 4410)):
+        assert torch.equal(xs[k][0], padded[:, s:s + 4410])
+    lit = LitClassifier({"_target_": "tests._toy.TinyNet", "num_classes": 4, "in_samples": 4410},
+                        {"_target_": "torch.optim.Adam", "lr": 1e-3})
+    lit.datamodule = dm
+    with torch.no_grad():
+        loss = lit._step((xs, y), "test")
+        mean_logits = torch.stack([lit(x) for x in xs]).mean(0)
+    assert torch.allclose(loss, F.cross_entropy(mean_logits, y))
