@@ -14,6 +14,8 @@
 // kernel recomputes S^T, dP^T with the query on the lane and accumulates dQ^T.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 64;
@@ -173,158 +175,220 @@ __device__ __forceinline__ int xcd_work_item(int L, int total) {
   return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
 }
 
-constexpr int FWD_Q = 256;
-// Deferred max (T13 of the CDNA4 playbook): the running max moves only when a tile's scores exceed it
-// by more than FWD_THR log2 units, so P stays <= 2^8 (exact in f32, same relative precision in bf16)
-// and the O / l rescale pass runs on a handful of tiles instead of on almost every tile.
-constexpr float FWD_THR = 8.f;
+// Forward structure (the loop is vector-issue bound at head dim 64, so the design is a VALU diet):
+//  * one wave = 32 queries (query on the lane), 4 waves = 128 queries per block, <= 168 registers so
+//    three waves share each SIMD and one wave's softmax issues beside the others' MFMAs;
+//  * K / V tiles arrive by LDS-DMA (global_load_lds_dwordx4, no staging registers, no ds_write),
+//    double-buffered: tile j+1 is requested before tile j is computed;
+//  * Q is pre-scaled by scale * log2(e) (bf16) and the running max m is rounded UP to a
+//    bf16-representable value, so "- m" rides the QK^T MFMA chain as a fifth k-step
+//    (ones column of K x (-m) row of Q): the scores leave the MFMA as s - m, p = exp2(.) directly;
+//  * the running max is not recomputed per tile: m only has to keep every p finite and O in range,
+//    so a tile whose exp-sum stays <= 2^16 (each p <= 2^16) is accepted as is, and only a tile that
+//    exceeds it (or the first tile) takes the wave-uniform rare path that computes the tile max,
+//    moves m, rescales O / l and recomputes the tile's p.
+constexpr int FWD_Q = 128;
+constexpr float FWD_SUM_LIMIT = 65536.f;
 
-struct FwdState {
-  bf16x8 qf[2][4];
-  f32x16 o[2][2];  // [d half][query group]
-  float l[2];      // row sums (this lane's half of the keys)
-  float m[2];      // running max (log2 units); set from the first tile
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef const __attribute__((address_space(1))) void* glb_vp;
+
+// x rounded toward +inf to a bf16-representable float (its negation is exact in bf16)
+__device__ __forceinline__ float bf16_ceil(float x) {
+  unsigned u = __builtin_bit_cast(unsigned, x);
+  if (!(u & 0x80000000u)) u += 0xFFFFu;
+  return __builtin_bit_cast(float, u & 0xFFFF0000u);
+}
+
+// One 64-row x 64-col bf16 tile (8 KB, sw_off layout) by LDS-DMA: 8 pieces of 1 KB = 8 rows each,
+// wave w issues pieces 2w and 2w + 1; lane i of a piece fills 16-B slot (i & 7) of row 8p + (i >> 3),
+// i.e. it loads chunk (i & 7) ^ swz(row) of that row (the swizzle rides the SOURCE address).  Buffer
+// loads: the per-lane byte offset is fixed, the tile start rides soffset (no VALU per tile), and rows
+// past the sequence end fall outside the descriptor's range and read as zeros (their keys are masked,
+// their V rows meet p = 0).
+struct TileDMA {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned voff[2];
+  __device__ __forceinline__ void init(const bf16* g, int64_t ld, int N, int wave, int lane) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(((int64_t)(N - 1) * ld + 64) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 8 * (2 * wave + i) + (lane >> 3);
+      voff[i] = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(bf16* tile, unsigned row0_bytes, int wave) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + (2 * wave + i) * 512), 16, voff[i], row0_bytes,
+                                               0, 0);
+  }
 };
 
-// One 64-key tile of the forward; TAIL masks keys >= N (only the last tile, peeled off the loop).
-template <bool TAIL>
-__device__ __forceinline__ void fwd_tile(FwdState& st, const bf16* K_, const bf16* V_, int k0, int N, bool first,
-                                         int lane) {
-  // S^T = K . Q'^T (log2 units): 16 MFMAs, 8 K fragments each feeding both query groups
-  f32x16 s[2][2];  // [key half][query group]
+// S^T - m for one 64-key tile: [key half] accumulators (rows = keys, lane column = query)
+__device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const bf16* K_, const bf16x8 (&qf)[4], bf16x8 one,
+                                       bf16x8 mrow, int lane) {
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
+  for (int kh = 0; kh < 2; ++kh) {
+    s[kh] = mfma(frag_row_sw(K_, 32 * kh + (lane & 31), 0, lane), qf[0], zero16());
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const bf16x8 kf = frag_row(K_, 32 * kh + (lane & 31), ks, lane);
-      s[kh][0] = mfma(kf, st.qf[0][ks], ks == 0 ? zero16() : s[kh][0]);
-      s[kh][1] = mfma(kf, st.qf[1][ks], ks == 0 ? zero16() : s[kh][1]);
-    }
+    for (int ks = 1; ks < 4; ++ks) s[kh] = mfma(frag_row_sw(K_, 32 * kh + (lane & 31), ks, lane), qf[ks], s[kh]);
+    s[kh] = mfma(one, mrow, s[kh]);
   }
-  bf16x8 pf[2][4];  // [query group][16-key chunk]
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    if constexpr (TAIL) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (k0 + acc_row(r, lane) >= N) s[0][g][r] = -INFINITY;
-        if (k0 + 32 + acc_row(r, lane) >= N) s[1][g][r] = -INFINITY;
-      }
-    }
-    float mx = max3(s[0][g][0], s[1][g][0], s[0][g][1]);
-#pragma unroll
-    for (int r = 1; r < 15; ++r) mx = max3(mx, s[1][g][r], s[0][g][r + 1]);
-    mx = max3(mx, s[1][g][15], s[1][g][15]);
-    mx = half_exchange_max(mx);  // this tile's max for this lane's query
-    // move the running max (wave-uniform branch): always on the first tile, later only past FWD_THR
-    if (__builtin_expect(first || __any(mx > st.m[g] + FWD_THR), 0)) {
-      const float mn = first ? mx : fmaxf(mx, st.m[g]);
-      if (!first) {
-        const float alpha = __builtin_amdgcn_exp2f(st.m[g] - mn);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { st.o[0][g][r] *= alpha; st.o[1][g][r] *= alpha; }
-        st.l[g] *= alpha;
-      }
-      st.m[g] = mn;
-    }
-    const float nm = -st.m[g];
-    float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[0][g][r] = __builtin_amdgcn_exp2f(s[0][g][r] + nm);
-      s[1][g][r] = __builtin_amdgcn_exp2f(s[1][g][r] + nm);
-      l0 += s[0][g][r];
-      l1 += s[1][g][r];
-    }
-    st.l[g] += l0 + l1;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) pf[g][c] = acc_frag(s[c >> 1][g], c & 1);
-  }
-  // O^T += V^T . P^T: 16 MFMAs, 8 transposed V fragments each feeding both query groups
+}
+
+struct FwdAcc {
+  f32x16 o[2];  // O^T [d half]: rows = d, lane column = query
+  float l;      // this lane's half of the row sum
+  float mb;     // running max (log2 units, bf16-exact)
+  bf16x8 mrow;  // fifth-k-step fragment: element 0 of the low lane half = -mb
+};
+
+// p = exp2(s - d) -> bf16 P^T fragments, row-sum partials
+__device__ __forceinline__ void fwd_exp(const f32x16 (&s)[2], float d, bf16x8 (&pf)[4], float& la, float& lb) {
+  la = 0.f; lb = 0.f;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const bf16x8 vf = frag_tr<VROW>(V_, 16 * c, 32 * dh, lane);
-      st.o[dh][0] = mfma(vf, pf[0][c], st.o[dh][0]);
-      st.o[dh][1] = mfma(vf, pf[1][c], st.o[dh][1]);
+    for (int j = 0; j < 8; ++j) {
+      const float p = __builtin_amdgcn_exp2f(s[c >> 1][8 * (c & 1) + j] - d);
+      if (c & 1) lb += p; else la += p;
+      pf[c][j] = (bf16)p;
     }
   }
 }
 
-// Each wave owns 64 queries as two 32-query groups sharing every K / V fragment read from LDS (one
-// LDS fragment feeds 2 MFMAs); 4 waves = 256 queries per block; 64-key tiles double-buffered in LDS
-// with the next tile's global loads in flight under the current tile's MFMAs.
-// VALU diet (the loop is vector-issue bound at head dim 64): Q is pre-scaled by scale*log2(e) once
-// (bf16) so p = exp2(s - m) is one add + one exp per score; the running max is deferred (FWD_THR);
-// the key mask exists only in the peeled last tile.
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                       float* __restrict__ lse, int N, int H, int nqb,
-                                                       float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * LROW];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * VROW];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+template <bool FIRST, bool TAIL>
+__device__ __forceinline__ void fwd_softmax(f32x16 (&s)[2], FwdAcc& a, bf16x8 (&pf)[4], int k0, int N, int lane) {
+  if constexpr (TAIL) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (k0 + acc_row(r, lane) >= N) s[0][r] = -INFINITY;
+      if (k0 + 32 + acc_row(r, lane) >= N) s[1][r] = -INFINITY;
+    }
+  }
+  float la, lb;
+  if (!FIRST) fwd_exp(s, 0.f, pf, la, lb);
+  if (FIRST || __builtin_expect(__any(la + lb > FWD_SUM_LIMIT), 0)) {
+    // rare path: move m to (at least) this tile's max, rounded up to bf16
+    float mx = fmaxf(s[0][0], s[1][0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+    mx = half_exchange_max(mx);
+    const float mn = FIRST ? bf16_ceil(mx) : fmaxf(a.mb, bf16_ceil(a.mb + mx));
+    const float d = mn - a.mb;
+    if (!FIRST) {
+      const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { a.o[0][r] *= alpha; a.o[1][r] *= alpha; }
+      a.l *= alpha;
+    }
+    fwd_exp(s, d, pf, la, lb);
+    a.mb = mn;
+    a.mrow[0] = (lane < 32) ? (bf16)(-mn) : (bf16)0.f;
+  }
+  a.l += la + lb;
+}
+
+__device__ __forceinline__ void fwd_pv(FwdAcc& a, const bf16* V_, const bf16x8 (&pf)[4], int lane) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) a.o[dh] = mfma(frag_tr_sw(V_, 16 * c, 32 * dh, lane), pf[c], a.o[dh]);
+  }
+}
+
+__global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                          float* __restrict__ lse, int N, int H, int nqb,
+                                                          float scale_log2) {
+  __shared__ __attribute__((aligned(1024))) bf16 Ks[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Vs[2][64 * 64];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
   const int bh = w / nqb, qb = w - bh * nqb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const int q0 = qb * FWD_Q + wave * 64;
-  const bool active = q0 < N;  // wave-uniform: a wave past the last query only helps staging
-  FwdState st;
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int q = q0 + 32 * g + (lane & 31);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) st.qf[g][ks][j] = (bf16)((float)r[j] * scale_log2);
-    }
-    st.o[0][g] = zero16(); st.o[1][g] = zero16();
-    st.m[g] = 0.f;
-    st.l[g] = 0.f;
-  }
   const int ntiles = (N + 63) / 64;
-  Stage64 kreg, vreg;
-  kreg.load(base + H * D, ldt, N, t);
-  vreg.load(base + 2 * H * D, ldt, N, t);
-  kreg.store(Ks[0], t);
-  vreg.store<VROW>(Vs[0], t);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles - 1; ++kt) {
-    // next tile's loads in flight under this tile's MFMAs
-    const int kn = (kt + 1) * 64;
-    kreg.load(base + (int64_t)kn * ldt + H * D, ldt, N - kn, t);
-    vreg.load(base + (int64_t)kn * ldt + 2 * H * D, ldt, N - kn, t);
-    if (active) fwd_tile<false>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
-    kreg.store(Ks[(kt + 1) & 1], t);
-    vreg.store<VROW>(Vs[(kt + 1) & 1], t);
-    __syncthreads();
+  const unsigned tile_bytes = (unsigned)(64 * ldt * 2);
+  TileDMA kdma, vdma;
+  kdma.init(base + H * D, ldt, N, wave, lane);
+  vdma.init(base + 2 * H * D, ldt, N, wave, lane);
+  kdma.issue(Ks[0], 0, wave);
+  vdma.issue(Vs[0], 0, wave);
+  // a wave past the last query computes on zero queries (finite, never stored): no branch in the loop
+  const int q = qb * FWD_Q + wave * 32 + (lane & 31);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
   }
-  if (!active) return;
-  {
-    const int kt = ntiles - 1;
-    if ((kt + 1) * 64 > N) fwd_tile<true>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
-    else fwd_tile<false>(st, Ks[kt & 1], Vs[kt & 1], kt * 64, N, kt == 0, lane);
-  }
+  bf16x8 one;
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int q = q0 + 32 * g + (lane & 31);
-    const float lt = half_exchange_sum(st.l[g]);
-    if (q < N) {
-      const float inv = 1.f / lt;
-      bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
-        const int d0 = 8 * g4 + 4 * (lane >> 5);
-        bf16x4 v0, v1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(st.o[0][g][4 * g4 + i] * inv); v1[i] = (bf16)(st.o[1][g][4 * g4 + i] * inv); }
-        *reinterpret_cast<bf16x4*>(orow + d0) = v0;
-        *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
-      }
-      if (lane < 32) lse[(int64_t)bh * N + q] = (st.m[g] + log2f(lt)) / LOG2E;
+  for (int j = 0; j < 8; ++j) one[j] = (bf16)0.f;
+  one[0] = (lane < 32) ? (bf16)1.f : (bf16)0.f;
+  FwdAcc a;
+  a.o[0] = zero16(); a.o[1] = zero16();
+  a.l = 0.f; a.mb = 0.f;
+  a.mrow = one;
+  a.mrow[0] = (bf16)0.f;
+  f32x16 s[2];
+  bf16x8 pf[4];
+  // one tile; P = buffer parity (compile-time, so every LDS address is base + immediate)
+  auto tile = [&](auto first, auto tail, auto par, int j) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    if (j + 1 < ntiles) {  // next tile's DMA flies under this tile's work
+      kdma.issue(Ks[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+      vdma.issue(Vs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
     }
+    fwd_qk(s, Ks[P], qf, one, a.mrow, lane);
+    fwd_softmax<decltype(first)::value, decltype(tail)::value>(s, a, pf, j * 64, N, lane);
+    fwd_pv(a, Vs[P], pf, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool tail = (ntiles * 64 != N);
+  if (ntiles == 1) {
+    if (tail) tile(T{}, T{}, P0{}, 0);
+    else tile(T{}, F{}, P0{}, 0);
+  } else {
+    tile(T{}, F{}, P0{}, 0);
+    int j = 1;
+    for (; j + 2 < ntiles; j += 2) {
+      tile(F{}, F{}, P1{}, j);
+      tile(F{}, F{}, P0{}, j + 1);
+    }
+    if (j + 1 < ntiles) {  // tiles j (odd) and j + 1 = last remain
+      tile(F{}, F{}, P1{}, j);
+      if (tail) tile(F{}, T{}, P0{}, j + 1);
+      else tile(F{}, F{}, P0{}, j + 1);
+    } else {  // tile j (odd) is the last
+      if (tail) tile(F{}, T{}, P1{}, j);
+      else tile(F{}, F{}, P1{}, j);
+    }
+  }
+  const float lt = half_exchange_sum(a.l);
+  if (q < N) {
+    const float inv = 1.f / lt;
+    bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
+      const int d0 = 8 * g4 + 4 * (lane >> 5);
+      bf16x4 v0, v1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(a.o[0][4 * g4 + i] * inv); v1[i] = (bf16)(a.o[1][4 * g4 + i] * inv); }
+      *reinterpret_cast<bf16x4*>(orow + d0) = v0;
+      *reinterpret_cast<bf16x4*>(orow + 32 + d0) = v1;
+    }
+    if (lane < 32) lse[(int64_t)bh * N + q] = (a.mb + log2f(lt)) / LOG2E;
   }
 }
 
