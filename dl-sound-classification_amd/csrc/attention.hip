@@ -393,284 +393,343 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
 }
 
 // ------------------------------------------------------------------------------ backward
-// delta[b,h,q] = sum_d dO[q][d] * O[q][d]
-__global__ void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout, float* __restrict__ delta,
-                                  int B, int N, int H) {
-  const int total = B * N * H;  // < 2^31 (checked by the launcher)
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int hd = i % H;
-    const int bq = i / H;
-    const int q = bq % N;
-    const int b = bq / N;
-    const bf16* o = out + (int64_t)i * D;
-    const bf16* g = dout + (int64_t)i * D;
-    float s = 0.f;
+// Both backward kernels recompute P from the SAME MFMA operands the forward used (Q' = bf16(q * scale
+// * log2 e) against K), so P sums to one exactly as the forward's lse normalised it.  The per-query
+// row constants ride the MFMA chains as a fifth k-step, each split into three bf16 parts (exact to
+// f32): S' = Q'K^T - L2 (L2 = lse * log2 e) gives p = exp2(S') directly, and dP' = dO V^T - delta
+// gives dS = p * dP' with one multiply.
+//
+// prep: per (b, q, h) row, Q' (B, N, H, 64) bf16 and the fragment rows (B*H, 2, N, 8) bf16:
+// part 0 = [-L2 (3 parts), 0 x 5], part 1 = [-delta (3 parts), 0 x 5], delta = sum_d dO * O.
+// 8 lanes per row.
+// x = h + m + l (three bf16 parts, exact to f32 rounding) into elements 0..2 of f
+__device__ __forceinline__ void split3(float x, bf16x8& f) {
+  const bf16 h = (bf16)x;
+  const float r1 = x - (float)h;
+  const bf16 m = (bf16)r1;
+  f[0] = h;
+  f[1] = m;
+  f[2] = (bf16)(r1 - (float)m);
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ out,
+                                                            const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                            bf16* __restrict__ qs, bf16* __restrict__ frag, int B,
+                                                            int N, int H, float scale_log2) {
+  const int64_t rows = (int64_t)B * N * H;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int part = threadIdx.x & 7;
+  if (i >= rows) return;  // whole 8-lane groups leave together
+  const int hd = (int)(i % H);
+  const int64_t bq = i / H;
+  const int q = (int)(bq % N), b = (int)(bq / N);
+  const bf16x8 o = *reinterpret_cast<const bf16x8*>(out + i * D + part * 8);
+  const bf16x8 g = *reinterpret_cast<const bf16x8*>(dout + i * D + part * 8);
+  const bf16x8 qv = *reinterpret_cast<const bf16x8*>(qkv + (bq * 3 * H + hd) * D + part * 8);
+  float s = 0.f;
+  bf16x8 qsc;
 #pragma unroll
-    for (int c = 0; c < D / 8; ++c) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(o + 8 * c);
-      const bf16x8 e = *reinterpret_cast<const bf16x8*>(g + 8 * c);
+  for (int j = 0; j < 8; ++j) {
+    s = fmaf((float)o[j], (float)g[j], s);
+    qsc[j] = (bf16)((float)qv[j] * scale_log2);
+  }
+  *reinterpret_cast<bf16x8*>(qs + i * D + part * 8) = qsc;
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  s += __shfl_xor(s, 4);
+  if (part < 2) {
+    const int64_t bhh = (int64_t)b * H + hd;
+    const float x = part == 0 ? -lse[bhh * N + q] * LOG2E : -s;
+    bf16x8 f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf((float)a[j], (float)e[j], s);
-    }
-    delta[((int64_t)b * H + hd) * N + q] = s;
+    for (int j = 0; j < 8; ++j) f[j] = (bf16)0.f;
+    split3(x, f);
+    *reinterpret_cast<bf16x8*>(frag + ((bhh * 2 + part) * N + q) * 8) = f;
   }
 }
 
-// 4 consecutive accumulator rows r = 4j..4j+3 of a 32-row block are rows 8j + 4h + 0..3: one float4
-__device__ __forceinline__ float4 rows4(const float* v, int j, int lane) {
-  return *reinterpret_cast<const float4*>(v + 8 * j + 4 * (lane >> 5));
+// ones fragment for the fifth k-step: elements 0..2 of the low lane half = 1
+__device__ __forceinline__ bf16x8 ones3(int lane) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (bf16)0.f;
+  if (lane < 32) { f[0] = (bf16)1.f; f[1] = (bf16)1.f; f[2] = (bf16)1.f; }
+  return f;
 }
 
-// Key-parallel dK / dV.  Each wave owns 64 keys as two 32-key groups (4 waves = 256 keys per block)
-// and sweeps 64-query tiles staged in LDS (Q, dO, lse, delta); with the key on the lane the S / dP
-// accumulators are query rows x key columns, and every Q / dO fragment read from LDS (row or
-// transposed) feeds both key groups.  dK, dV accumulate in registers; no atomics.
-constexpr int BWD_K = 256;
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                            const float* __restrict__ lse,
-                                                            const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                            int N, int H, int nkb, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Qs[2][64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16 Gs[2][64 * 64];
-  __shared__ __attribute__((aligned(16))) float Ls[2][64];
-  __shared__ __attribute__((aligned(16))) float Ds[2][64];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+// The fragment rows of 64 queries by LDS-DMA into [part][64][8]: waves 0 and 1 issue part 0 / 1
+// (1 KB each, 16-B rows: the per-lane row reads are conflict-free).  Past the sequence end part 0
+// reads part 1's rows (finite; those queries are masked) and part 1 reads zeros.
+struct FragDMA {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned part_bytes;
+  __device__ __forceinline__ void init(const bf16* g, int N) {
+    part_bytes = (unsigned)N * 16;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(2 * part_bytes), 0x00020000);
+  }
+  __device__ __forceinline__ void issue(bf16* tile, unsigned row0, int wave, int lane) const {
+    if (wave < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 512), 16,
+                                               (unsigned)wave * part_bytes + lane * 16, row0 * 16, 0, 0);
+  }
+};
+
+// A fifth-k-step fragment row read by every lane: the high lane half carries k = 8..15, which meet
+// the zero half of the ones fragment, so its (finite) copy of the row contributes nothing.
+__device__ __forceinline__ bf16x8 row_frag(const bf16* row) { return *reinterpret_cast<const bf16x8*>(row); }
+
+// Key-parallel dK / dV.  One wave = 32 keys (key on the lane), 4 waves = 128 keys per block; the
+// block sweeps 64-query tiles of Q', dO and their fragment rows (LDS-DMA, double-buffered).  With
+// the key on the lane the S / dP accumulators are query rows x key columns and are used as the B
+// operands of dV^T += dO^T P and dK^T += Q'^T dS directly (no LDS round trip); dK, dV accumulate in
+// registers over the whole sequence: no atomics, deterministic.
+constexpr int BWD_K = 128;
+
+template <bool TAIL>
+__device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
+                                          const bf16* F_, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one,
+                                          int q0, int N, int lane) {
+#pragma unroll
+  for (int sq = 0; sq < 2; ++sq) {
+    const int qr = sq * 32 + (lane & 31);
+    f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), kf[0], zero16());
+    f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
+#pragma unroll
+    for (int ks = 1; ks < 4; ++ks) {
+      sc = mfma(frag_row_sw(Q_, qr, ks, lane), kf[ks], sc);
+      dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
+    }
+    sc = mfma(row_frag(F_ + qr * 8), one, sc);
+    dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(sc[r]);
+      if constexpr (TAIL) {
+        if (q0 + sq * 32 + acc_row(r, lane) >= N) p = 0.f;
+      }
+      sc[r] = p;
+      dp[r] *= p;
+    }
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        dv[dh] = mfma(frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane), pf, dv[dh]);
+        dk[dh] = mfma(frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane), df, dk[dh]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                               const bf16* __restrict__ qs, const bf16* __restrict__ frag,
+                                                               bf16* __restrict__ dqkv, int N, int H, int nkb,
+                                                               float dk_scale) {
+  __shared__ __attribute__((aligned(1024))) bf16 Qs[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Gs[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Fs[2][64 * 16];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
   const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const bf16* gbase = dout + (int64_t)b * N * ldo + hd * D;
-  const int k0w = kb * BWD_K + wave * 64;
-  const bool active = k0w < N;
-  bf16x8 kf[2][4], vf[2][4];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int key = k0w + 32 * g + (lane & 31);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[g][ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, key < N);
-      vf[g][ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
-    }
-  }
-  f32x16 dv[2][2], dk[2][2];  // [d half][key group]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int g = 0; g < 2; ++g) { dv[i][g] = zero16(); dk[i][g] = zero16(); }
   const int ntiles = (N + 63) / 64;
-  Stage64 qreg, greg;
-  float lreg = 0.f, dreg = 0.f;
-  auto load_rows = [&](int q0) __attribute__((always_inline)) {
-    qreg.load(base + (int64_t)q0 * ldt, ldt, N - q0, t);
-    greg.load(gbase + (int64_t)q0 * ldo, ldo, N - q0, t);
-    if (t < 64) {
-      const int q = q0 + t;
-      lreg = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;  // q >= N -> p = 0
-      dreg = q < N ? delta[(int64_t)bh * N + q] : 0.f;
-    }
-  };
-  auto store_rows = [&](int buf) __attribute__((always_inline)) {
-    qreg.store_sw(Qs[buf], t);
-    greg.store_sw(Gs[buf], t);
-    if (t < 64) { Ls[buf][t] = lreg; Ds[buf][t] = dreg; }
-  };
-  load_rows(0);
-  store_rows(0);
-  __syncthreads();
-  for (int qt = 0; qt < ntiles; ++qt) {
-    load_rows(min(qt + 1, ntiles - 1) * 64);  // the last iteration re-stages into the idle buffer
-    if (active) {
-      const bf16* Q_ = Qs[qt & 1];
-      const bf16* G_ = Gs[qt & 1];
-      const float* L_ = Ls[qt & 1];
-      const float* D_ = Ds[qt & 1];
+  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
+  TileDMA qd, gd;
+  FragDMA fd;
+  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  fd.init(frag + (int64_t)bh * 2 * N * 8, N);
+  qd.issue(Qs[0], 0, wave);
+  gd.issue(Gs[0], 0, wave);
+  fd.issue(Fs[0], 0, wave, lane);
+  const int key = kb * BWD_K + wave * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
 #pragma unroll
-      for (int sq = 0; sq < 2; ++sq) {
-        f32x16 sc[2], dp[2];
-        sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8 qa = frag_row_sw(Q_, sq * 32 + (lane & 31), ks, lane);
-          const bf16x8 ga = frag_row_sw(G_, sq * 32 + (lane & 31), ks, lane);
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            sc[g] = mfma(qa, kf[g][ks], sc[g]);
-            dp[g] = mfma(ga, vf[g][ks], dp[g]);
-          }
-        }
-        // accumulator rows are queries sq*32 + acc_row(r); their lse / delta as 4 float4 each
-        float lr[16], dr[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float4 l4 = rows4(L_ + sq * 32, j, lane), d4 = rows4(D_ + sq * 32, j, lane);
-          lr[4 * j] = l4.x; lr[4 * j + 1] = l4.y; lr[4 * j + 2] = l4.z; lr[4 * j + 3] = l4.w;
-          dr[4 * j] = d4.x; dr[4 * j + 1] = d4.y; dr[4 * j + 2] = d4.z; dr[4 * j + 3] = d4.w;
-        }
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(sc[g][r], scale_log2, -lr[r]));
-            sc[g][r] = p;
-            dp[g][r] = p * (dp[g][r] - dr[r]);
-          }
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-          bf16x8 tg[2], tq[2];
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) {
-            tg[dh] = frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane);
-            tq[dh] = frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane);
-          }
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            const bf16x8 pf = acc_frag(sc[g], sk);
-            const bf16x8 df = acc_frag(dp[g], sk);
-#pragma unroll
-            for (int dh = 0; dh < 2; ++dh) {
-              dv[dh][g] = mfma(tg[dh], pf, dv[dh][g]);
-              dk[dh][g] = mfma(tq[dh], df, dk[dh][g]);
-            }
-          }
-        }
-      }
-    }
-    store_rows((qt + 1) & 1);
-    __syncthreads();
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, key < N);
+    vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
   }
-  if (!active) return;
+  const bf16x8 one = ones3(lane);
+  f32x16 dk[2], dv[2];
+  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+  auto tile = [&](auto tail, auto par, int j) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    if (j + 1 < ntiles) {
+      qd.issue(Qs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+      gd.issue(Gs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+      fd.issue(Fs[P ^ 1], (unsigned)(j + 1) * 64u, wave, lane);
+    }
+    dkdv_tile<decltype(tail)::value>(dk, dv, Qs[P], Gs[P], Fs[P], kf, vf, one, j * 64, N, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool tail = (ntiles * 64 != N);
+  int j = 0;
+  for (; j + 2 < ntiles; j += 2) {
+    tile(F{}, P0{}, j);
+    tile(F{}, P1{}, j + 1);
+  }
+  if (j + 1 < ntiles) {  // tiles j (even) and j + 1 = last
+    tile(F{}, P0{}, j);
+    if (tail) tile(T{}, P1{}, j + 1);
+    else tile(F{}, P1{}, j + 1);
+  } else {  // tile j (even) is the last
+    if (tail) tile(T{}, P0{}, j);
+    else tile(F{}, P0{}, j);
+  }
+  if (key >= N) return;
+  bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
+  bf16* vrow = krow + H * D;
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int key = k0w + 32 * g + (lane & 31);
-    if (key >= N) continue;
-    bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
-    bf16* vrow = krow + H * D;
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d0 = 8 * g4 + 4 * (lane >> 5);
+    bf16x4 a0, a1, c0, c1;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d0 = 8 * g4 + 4 * (lane >> 5);
-      bf16x4 a0, a1, c0, c1;
+    for (int i = 0; i < 4; ++i) {
+      a0[i] = (bf16)(dk[0][4 * g4 + i] * dk_scale);
+      a1[i] = (bf16)(dk[1][4 * g4 + i] * dk_scale);
+      c0[i] = (bf16)dv[0][4 * g4 + i];
+      c1[i] = (bf16)dv[1][4 * g4 + i];
+    }
+    *reinterpret_cast<bf16x4*>(krow + d0) = a0;
+    *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
+    *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
+    *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
+  }
+}
+
+// Query-parallel dQ.  One wave = 32 queries (query on the lane), 4 waves = 128 per block, sweeping
+// 64-key tiles of K and V (LDS-DMA, double-buffered): S'^T = K Q'^T - L2, dP'^T = V dO^T - delta with
+// the row constants as fifth k-steps (B-side fragments in registers), dQ^T += K^T dS^T with dS^T
+// straight from the accumulators.
+constexpr int BWD_Q = 128;
+
+template <bool TAIL>
+__device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const bf16* V_, const bf16x8 (&qf)[4],
+                                        const bf16x8 (&gf)[4], bf16x8 one, bf16x8 lf, bf16x8 df_, int k0, int N,
+                                        int lane) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a0[i] = (bf16)(dk[0][g][4 * g4 + i] * scale);
-        a1[i] = (bf16)(dk[1][g][4 * g4 + i] * scale);
-        c0[i] = (bf16)dv[0][g][4 * g4 + i];
-        c1[i] = (bf16)dv[1][g][4 * g4 + i];
+  for (int kh = 0; kh < 2; ++kh) {
+    const int kr = 32 * kh + (lane & 31);
+    f32x16 sc = mfma(frag_row_sw(K_, kr, 0, lane), qf[0], zero16());
+    f32x16 dp = mfma(frag_row_sw(V_, kr, 0, lane), gf[0], zero16());
+#pragma unroll
+    for (int ks = 1; ks < 4; ++ks) {
+      sc = mfma(frag_row_sw(K_, kr, ks, lane), qf[ks], sc);
+      dp = mfma(frag_row_sw(V_, kr, ks, lane), gf[ks], dp);
+    }
+    sc = mfma(one, lf, sc);
+    dp = mfma(one, df_, dp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(sc[r]);
+      if constexpr (TAIL) {
+        if (k0 + 32 * kh + acc_row(r, lane) >= N) p = 0.f;
       }
-      *reinterpret_cast<bf16x4*>(krow + d0) = a0;
-      *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
-      *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
-      *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
+      dp[r] *= p;
+    }
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 dsf = acc_frag(dp, sk);
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) acc[dh] = mfma(frag_tr_sw(K_, 32 * kh + 16 * sk, 32 * dh, lane), dsf, acc[dh]);
     }
   }
 }
 
-// Query-parallel dQ: each wave owns 64 queries as two 32-query groups (256 per block), sweeps 64-key
-// tiles (K swizzled for its row AND transposed reads, V row-read only), recomputes S^T and dP^T with
-// the query on the lane and accumulates dQ^T; every K / V fragment read feeds both query groups.
-constexpr int BWD_Q = 256;
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          bf16* __restrict__ dqkv, int N, int H, int nqb, float scale,
-                                                          float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * LROW];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                             const bf16* __restrict__ frag, bf16* __restrict__ dqkv,
+                                                             int N, int H, int nqb, float scale, float scale_log2) {
+  __shared__ __attribute__((aligned(1024))) bf16 Ks[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Vs[2][64 * 64];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
   const int bh = w / nqb, qb = w - bh * nqb, b = bh / H, hd = bh % H;
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const int q0w = qb * BWD_Q + wave * 64;
-  const bool active = q0w < N;
-  bf16x8 qf[2][4], gf[2][4];
-  float lq[2], dl[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int q = q0w + 32 * g + (lane & 31);
-    const bool qv = q < N;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qf[g][ks] = load_frag_global(base + (int64_t)q * ldt, ks, lane, qv);
-      gf[g][ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
-    }
-    lq[g] = qv ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
-    dl[g] = qv ? delta[(int64_t)bh * N + q] : 0.f;
-  }
-  f32x16 acc[2][2];  // [d half][query group]
-#pragma unroll
-  for (int i = 0; i < 2; ++i) { acc[i][0] = zero16(); acc[i][1] = zero16(); }
   const int ntiles = (N + 63) / 64;
-  Stage64 kreg, vreg;
-  kreg.load(base + H * D, ldt, N, t);
-  vreg.load(base + 2 * H * D, ldt, N, t);
-  kreg.store_sw(Ks[0], t);
-  vreg.store(Vs[0], t);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int k0 = kt * 64;
-    const int kn = min(k0 + 64, (ntiles - 1) * 64);
-    kreg.load(base + (int64_t)kn * ldt + H * D, ldt, N - kn, t);
-    vreg.load(base + (int64_t)kn * ldt + 2 * H * D, ldt, N - kn, t);
-    if (active) {
-      const bf16* K_ = Ks[kt & 1];
-      const bf16* V_ = Vs[kt & 1];
+  const unsigned tile_bytes = (unsigned)(64 * ldt * 2);
+  TileDMA kd, vd;
+  kd.init(base + H * D, ldt, N, wave, lane);
+  vd.init(base + 2 * H * D, ldt, N, wave, lane);
+  kd.issue(Ks[0], 0, wave);
+  vd.issue(Vs[0], 0, wave);
+  const int q = qb * BWD_Q + wave * 32 + (lane & 31);
+  const bool qv = q < N;
+  bf16x8 qf[4], gf[4];
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        f32x16 sc[2], dp[2];
-        sc[0] = zero16(); sc[1] = zero16(); dp[0] = zero16(); dp[1] = zero16();
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, qv);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8 ka = frag_row_sw(K_, st * 32 + (lane & 31), ks, lane);
-          const bf16x8 va = frag_row(V_, st * 32 + (lane & 31), ks, lane);
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            sc[g] = mfma(ka, qf[g][ks], sc[g]);
-            dp[g] = mfma(va, gf[g][ks], dp[g]);
-          }
-        }
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + st * 32 + acc_row(r, lane);
-            const float p = key < N ? __builtin_amdgcn_exp2f(fmaf(sc[g][r], scale_log2, -lq[g])) : 0.f;
-            dp[g][r] = p * (dp[g][r] - dl[g]);
-          }
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-          bf16x8 tk[2];
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) tk[dh] = frag_tr_sw(K_, st * 32 + 16 * sk, 32 * dh, lane);
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            const bf16x8 df = acc_frag(dp[g], sk);
-#pragma unroll
-            for (int dh = 0; dh < 2; ++dh) acc[dh][g] = mfma(tk[dh], df, acc[dh][g]);
-          }
-        }
-      }
-    }
-    kreg.store_sw(Ks[(kt + 1) & 1], t);
-    vreg.store(Vs[(kt + 1) & 1], t);
-    __syncthreads();
+    for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
+    gf[ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
   }
-  if (!active) return;
+  // fifth-k-step B fragments of this lane's query (zero for a query past the end: p = 1, dS = 0)
+  bf16x8 lf, dlf;
+  {
+    const bf16* fr = frag + ((int64_t)bh * 2 * N + (qv ? q : 0)) * 8;
+    lf = row_frag(fr);
+    dlf = row_frag(fr + (int64_t)N * 8);
+    if (!qv) {
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int q = q0w + 32 * g + (lane & 31);
-    if (q >= N) continue;
-    bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d0 = 8 * g4 + 4 * (lane >> 5);
-      bf16x4 v0, v1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(acc[0][g][4 * g4 + i] * scale); v1[i] = (bf16)(acc[1][g][4 * g4 + i] * scale); }
-      *reinterpret_cast<bf16x4*>(qrow + d0) = v0;
-      *reinterpret_cast<bf16x4*>(qrow + 32 + d0) = v1;
+      for (int j = 0; j < 8; ++j) { lf[j] = (bf16)0.f; dlf[j] = (bf16)0.f; }
     }
+  }
+  const bf16x8 one = ones3(lane);
+  f32x16 acc[2];
+  acc[0] = zero16(); acc[1] = zero16();
+  auto tile = [&](auto tail, auto par, int j) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    if (j + 1 < ntiles) {
+      kd.issue(Ks[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+      vd.issue(Vs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+    }
+    dq_tile<decltype(tail)::value>(acc, Ks[P], Vs[P], qf, gf, one, lf, dlf, j * 64, N, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool tail = (ntiles * 64 != N);
+  int j = 0;
+  for (; j + 2 < ntiles; j += 2) {
+    tile(F{}, P0{}, j);
+    tile(F{}, P1{}, j + 1);
+  }
+  if (j + 1 < ntiles) {
+    tile(F{}, P0{}, j);
+    if (tail) tile(T{}, P1{}, j + 1);
+    else tile(F{}, P1{}, j + 1);
+  } else {
+    if (tail) tile(T{}, P0{}, j);
+    else tile(F{}, P0{}, j);
+  }
+  if (!qv) return;
+  bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d0 = 8 * g4 + 4 * (lane >> 5);
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v0[i] = (bf16)(acc[0][4 * g4 + i] * scale); v1[i] = (bf16)(acc[1][4 * g4 + i] * scale); }
+    *reinterpret_cast<bf16x4*>(qrow + d0) = v0;
+    *reinterpret_cast<bf16x4*>(qrow + 32 + d0) = v1;
   }
 }
-
 
 // ------------------------------------------------------------------------------ f32 path
 // Reference-precision kernels (exact f32 arithmetic, no flash tiling) used when the model runs
@@ -815,6 +874,7 @@ extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtyp
     return 0;
   }
   MIA_CHECK_ARG(dtype == MIA_BF16, "attn_fwd: dtype");
+  MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_fwd: one sequence must span < 2 GiB");
   const int nqb = (int)cdiv(N, FWD_Q);
   MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd: grid too large");
   attn_fwd_kernel<<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>((const bf16*)qkv, (bf16*)out, lse, N, H, nqb,
@@ -823,15 +883,22 @@ extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtyp
   return 0;
 }
 
+extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_t H) {
+  const int64_t rows = (int64_t)B * N * H;
+  if (dtype == MIA_F32) return rows * 4;  // delta
+  return rows * D * 2 + rows * 32;        // Q' + fragment rows
+}
+
 extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
-                            float* delta, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
+                            void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
                             mia_stream_t stream) {
-  MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && delta, "attn_bwd: null pointer");
+  MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && work, "attn_bwd: null pointer");
   MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_bwd: bad shape");
   hipStream_t s = as_stream(stream);
   const int64_t rows = (int64_t)B * N * H;
   if (dtype == MIA_F32) {
     MIA_CHECK_ARG(N <= MAXN, "attn_bwd f32: N must be <= %d", MAXN);
+    float* delta = (float*)work;
     attn_delta_f32_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
         (const float*)out, (const float*)dout, delta, B, N, H);
     MIA_LAUNCH_CHECK("attn_delta_f32");
@@ -845,16 +912,22 @@ extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, 
     return 0;
   }
   MIA_CHECK_ARG(dtype == MIA_BF16, "attn_bwd: dtype");
-  MIA_CHECK_ARG(rows < (1ll << 31), "attn_bwd: B*N*H too large");
-  attn_delta_kernel<<<(unsigned)std::min<int64_t>(cdiv(rows, 256), 16384), 256, 0, s>>>(
-      (const bf16*)out, (const bf16*)dout, delta, B, N, H);
-  MIA_LAUNCH_CHECK("attn_delta");
+  MIA_CHECK_ARG(rows * 8 < (1ll << 31), "attn_bwd: B*N*H too large");
+  MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_bwd: one sequence must span < 2 GiB");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(work) & 15) == 0, "attn_bwd: workspace must be 16-B aligned");
+  bf16* qs = (bf16*)work;
+  bf16* frag = qs + rows * D;
+  const float scale_log2 = scale * LOG2E;
+  attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
+                                                                     (const bf16*)dout, lse, qs, frag, B, N, H,
+                                                                     scale_log2);
+  MIA_LAUNCH_CHECK("attn_bwd_prep");
   const int nkb = (int)cdiv(N, BWD_K), nqb = (int)cdiv(N, BWD_Q);
-  attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                               (bf16*)dqkv, N, H, nkb, scale, scale * LOG2E);
+  attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag,
+                                                               (bf16*)dqkv, N, H, nkb, 1.f / LOG2E);
   MIA_LAUNCH_CHECK("attn_bwd_dkdv");
-  attn_bwd_dq_kernel<<<(unsigned)(nqb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                             (bf16*)dqkv, N, H, nqb, scale, scale * LOG2E);
+  attn_bwd_dq_kernel<<<(unsigned)(nqb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, frag, (bf16*)dqkv,
+                                                             N, H, nqb, scale, scale_log2);
   MIA_LAUNCH_CHECK("attn_bwd_dq");
   return 0;
 }

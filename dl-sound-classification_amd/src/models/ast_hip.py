@@ -186,11 +186,11 @@ class ASTFunction(torch.autograd.Function):
             da = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj")
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
-            delta = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
+            work = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8, device=dev)
             with K.probe("attn.bwd", 10.0 * B * Hh * N * N * (D // Hh),
                          (2 * dqkv.numel() + 2 * da.numel()) * dqkv.element_size()):
                 L.check(L.load().mia_attn_bwd(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
-                                              sb["lse"].data_ptr(), dqkv.data_ptr(), delta.data_ptr(), cd, B, N, Hh,
+                                              sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), cd, B, N, Hh,
                                               s["scale"], L.stream_ptr()), "mia_attn_bwd")
             dh = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")

@@ -380,9 +380,11 @@ int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtype, int32_t 
                  int32_t H, float scale, mia_stream_t stream);
 /* Deterministic backward (key-parallel dK/dV kernel + query-parallel dQ kernel, no atomics).
  * dout: (B, N, H, 64) bf16; dqkv: (B, N, 3, H, 64) bf16 (fully written);
- * delta: f32 (B, H, N) workspace (rowsum(dO * O)). */
+ * work: 16-B aligned workspace of mia_attn_bwd_workspace_bytes() bytes (bf16: the scaled Q operand
+ * and per-query row-constant fragments; f32: rowsum(dO * O)). */
+int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_t H);
 int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
-                 void* dqkv, float* delta, int32_t dtype, int32_t B, int32_t N, int32_t H,
+                 void* dqkv, void* work, int32_t dtype, int32_t B, int32_t N, int32_t H,
                  float scale, mia_stream_t stream);
 
 /* AST token assembly (ast.py:56-59): x[b][0] = cls + pos[0]; x[b][1+p] = patches[b][p] + pos[1+p].

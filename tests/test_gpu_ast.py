@@ -42,9 +42,9 @@ def test_attention_fwd_bwd(cuda, dt, B, N, H):
     lib = L.load()
     L.check(lib.mia_attn_fwd(tq.data_ptr(), out.data_ptr(), lse.data_ptr(), dt, B, N, H, 0.125, L.stream_ptr()), "fwd")
     dq = torch.empty_like(tq)
-    delta = torch.empty(B, H, N, device=cuda)
+    work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(dt, B, N, H)), dtype=torch.uint8, device=cuda)
     L.check(lib.mia_attn_bwd(tq.data_ptr(), out.data_ptr(), dout.to(cuda).data_ptr(), lse.data_ptr(), dq.data_ptr(),
-                             delta.data_ptr(), dt, B, N, H, 0.125, L.stream_ptr()), "bwd")
+                             work.data_ptr(), dt, B, N, H, 0.125, L.stream_ptr()), "bwd")
     torch.cuda.synchronize()
     tol = 2e-2 if dt == L.BF16 else 1e-5
     assert rel(out.view(B, N, H, 64).permute(0, 2, 1, 3), o) < tol
@@ -83,9 +83,9 @@ def test_attention_running_max_paths(cuda, profile):
     L.check(lib.mia_attn_fwd(tq.data_ptr(), out.data_ptr(), lse.data_ptr(), L.BF16, B, N, H, 0.125, L.stream_ptr()),
             "fwd")
     dq = torch.empty_like(tq)
-    delta = torch.empty(B, H, N, device=cuda)
+    work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H)), dtype=torch.uint8, device=cuda)
     L.check(lib.mia_attn_bwd(tq.data_ptr(), out.data_ptr(), dout.to(cuda).data_ptr(), lse.data_ptr(), dq.data_ptr(),
-                             delta.data_ptr(), L.BF16, B, N, H, 0.125, L.stream_ptr()), "bwd")
+                             work.data_ptr(), L.BF16, B, N, H, 0.125, L.stream_ptr()), "bwd")
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all() and torch.isfinite(dq.float()).all()
     # The kernel feeds Q * scale * log2(e) to the MFMA in bf16: one more rounding of q of the same size

@@ -19,8 +19,8 @@ out = torch.empty(B * N, H * D, dtype=torch.bfloat16, device=dev)
 lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
 dout = torch.randn(B * N, H * D, generator=g, device=dev).to(torch.bfloat16)
 dqkv = torch.empty_like(qkv)
-delta = torch.empty(B, H, N, dtype=torch.float32, device=dev)
 lib = L.load()
+work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H)), dtype=torch.uint8, device=dev)
 s = L.stream_ptr()
 
 
@@ -30,7 +30,7 @@ def fwd():
 
 def bwd():
     L.check(lib.mia_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), dqkv.data_ptr(),
-                             delta.data_ptr(), L.BF16, B, N, H, D ** -0.5, s), "bwd")
+                             work.data_ptr(), L.BF16, B, N, H, D ** -0.5, s), "bwd")
 
 
 flop_f = 4.0 * B * H * N * N * D
