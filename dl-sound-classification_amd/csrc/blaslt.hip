@@ -197,7 +197,7 @@ bool eligible(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, in
   if (B.layout == MIA_LAYOUT_KC) { if (B.rows != N || B.cols < K) return false; }
   else { if (B.rows < K || B.cols != N) return false; }
   if (E.dtype != MIA_F32 && E.dtype != MIA_BF16) return false;
-  if (E.accumulate || E.rm_inner || E.alpha != 1.f) return false;
+  if (E.accumulate || E.rm_inner || E.alpha != 1.f || E.sqsum) return false;
   if (E.act != MIA_ACT_NONE && E.act != MIA_ACT_RELU && E.act != MIA_ACT_ADD_AUX && E.act != MIA_ACT_GELU_SAVE &&
       E.act != MIA_DACT_GELU)
     return false;

@@ -1426,6 +1426,37 @@ bool tapconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, 
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
 
+// block-wide sum of one double per thread (4 waves), written by thread 0: a tile's sum of squares
+__device__ __forceinline__ void tile_sqsum_store(double* dst, double v) {
+  __shared__ double red[NT / 64];
+  v = wave_sum_d(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+    *dst = s;
+  }
+}
+
+// MiaEpilogue.sqsum for a GEMM whose kernel did not produce it (other paths, split-K): one block
+// per 128 x 128 tile of the f32 output C (ldc), same slots and per-tile order of accumulation
+__global__ __launch_bounds__(NT) void tile_sqsum_kernel(const float* __restrict__ c, int64_t ldc, int64_t M, int64_t N,
+                                                        int nbn, double* __restrict__ out) {
+  const int bm = blockIdx.x / nbn, bn = blockIdx.x - (blockIdx.x / nbn) * nbn;
+  const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
+  float sq = 0.f;
+  for (int e = threadIdx.x; e < 128 * 128; e += NT) {
+    const int64_t m = m0 + e / 128, n = n0 + e % 128;
+    if (m < M && n < N) {
+      const float v = c[m * ldc + n];
+      sq = fmaf(v, v, sq);
+    }
+  }
+  tile_sqsum_store(out + blockIdx.x, (double)sq);
+}
+
 template <int L>
 struct DLoader {
   // per-lane source pointers for this wave's 4 DMA instructions of a tile, advanced per K-tile
@@ -1576,6 +1607,7 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
         }
     __syncthreads();
     float* out = reinterpret_cast<float*>(g.e.ptr);
+    float sq = 0.f;
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {
       const int row = wave * 32 + it * 2 + (lane >> 5);
@@ -1583,7 +1615,9 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
       f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
       __builtin_nontemporal_store(v, dst);
+      if (g.e.sqsum) sq = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], sq))));
     }
+    if (g.e.sqsum) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq);
     return;
   }
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
@@ -1644,6 +1678,7 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   }
 
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * 33);
+  double sqg = 0.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1671,10 +1706,17 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
           }
         } else {
           epi_store16(g.e, m, nb, g.N, v);
+          if (g.e.sqsum) {
+            float sq = 0.f;
+            for (int c = 0; c < 16; ++c)
+              if (nb + c < g.N) sq = fmaf(v[c], v[c], sq);
+            sqg += sq;
+          }
         }
       }
       __syncthreads();
     }
+  if (g.e.sqsum && g.split == 1) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, sqg);
 }
 
 bool dgemm_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute) {
@@ -1792,6 +1834,7 @@ EpiDev to_dev(const MiaEpilogue& e) {
   d.ldc = e.ldc; d.rm_inner = e.rm_inner; d.rm_outer = e.rm_outer; d.rm_istride = e.rm_istride;
   d.rm_offset = e.rm_offset; d.bias = e.bias; d.aux = reinterpret_cast<const char*>(e.aux);
   d.ldaux = e.ldaux; d.alpha = e.alpha; d.act_scale = e.act_scale;
+  d.sqsum = e.sqsum;
   return d;
 }
 
@@ -2032,10 +2075,34 @@ static int gemm_autotune(const MiaOperand* A, const MiaOperand* B, const MiaEpil
   return 0;
 }
 
+extern "C" int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N) { return cdiv(M, 128) * cdiv(N, 128); }
+
+static int mia_gemm_impl(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N,
+                         int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace, mia_stream_t stream);
+
 extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
                         int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
                         mia_stream_t stream) {
   MIA_CHECK_ARG(A && B && E, "gemm: null descriptor");
+  if (!E->sqsum) return mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
+  MIA_CHECK_ARG(E->dtype == MIA_F32 && E->act == MIA_ACT_NONE && !E->bias && !E->accumulate && !E->rm_inner &&
+                    E->alpha == 1.f,
+                "gemm: sqsum needs a plain f32 output");
+  if (int r = mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
+  // the dense kernel writes the slots itself when it runs unsplit; every other path gets the pass
+  const bool fused = dgemm_ok(*A, *B, M, N, K, compute_dtype) && split_k <= 1;
+  if (!fused && M > 0 && N > 0) {
+    const int64_t nb = mia_gemm_sqsum_slots(M, N);
+    MIA_CHECK_ARG(nb < (1ll << 31), "gemm sqsum: too many tiles");
+    tile_sqsum_kernel<<<(unsigned)nb, NT, 0, as_stream(stream)>>>(reinterpret_cast<const float*>(E->ptr), E->ldc, M,
+                                                                   N, (int)cdiv(N, 128), E->sqsum);
+    MIA_LAUNCH_CHECK("gemm sqsum");
+  }
+  return 0;
+}
+
+static int mia_gemm_impl(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N,
+                         int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace, mia_stream_t stream) {
   if (E->ptr && M > 0 && N > 0 && K > 0 && mblas::eligible(*A, *B, *E, M, N, K, compute_dtype) &&
       (split_k <= 1 || workspace)) {
     const int pol = mblas::policy();

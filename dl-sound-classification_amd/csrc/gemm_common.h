@@ -13,6 +13,7 @@ struct EpiDev {
   const char* aux;
   int64_t ldaux;
   float alpha, act_scale;
+  double* sqsum;  // per-tile sum of squares of the stored output (see MiaEpilogue), or null
 };
 
 struct DArgs {

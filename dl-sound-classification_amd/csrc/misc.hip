@@ -118,16 +118,22 @@ constexpr int NF_NT = 1024;
 
 // Squared L2 norm partials of every gradient tensor: 16-B loads (tensor storage is 16-B aligned
 // torch allocations; a misaligned one takes the scalar path), f32 accumulation flushed to double.
+// A tensor with precomputed partials (pre_sq[tsr], e.g. the sqsum slots of the GEMM epilogue that
+// wrote it) is not re-read: its partials are summed instead, in the same fixed grid-stride order.
 __global__ __launch_bounds__(NT) void sqnorm_kernel(void* const* __restrict__ grads, const int64_t* __restrict__ sizes,
-                                                    float* __restrict__ ws) {
+                                                    const void* const* __restrict__ pre_sq,
+                                                    const int64_t* __restrict__ pre_n, float* __restrict__ ws) {
   const int tsr = blockIdx.y;
   const float* g = reinterpret_cast<const float*>(grads[tsr]);
   const int64_t n = sizes[tsr];
   const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nthr = (int64_t)gridDim.x * NT;
+  const double* pre = pre_sq ? reinterpret_cast<const double*>(pre_sq[tsr]) : nullptr;
   double s = 0.0;
   float fs = 0.f;
   int cnt = 0;
-  if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+  if (pre) {
+    for (int64_t i = tid; i < pre_n[tsr]; i += nthr) s += pre[i];
+  } else if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
     const int64_t n4 = n >> 2;
     const float4* g4 = reinterpret_cast<const float4*>(g);
     for (int64_t i = tid; i < n4; i += nthr) {
@@ -523,14 +529,16 @@ extern "C" int64_t mia_adam_workspace_bytes(int32_t ntensors) {
 extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg, void* const* exp_avg_sq,
                              void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
                              float beta2, float eps, float weight_decay, int32_t step, float clip,
-                             float* total_norm_out, void* sqnorm_ws, mia_stream_t stream) {
+                             float* total_norm_out, void* sqnorm_ws, const void* const* pre_sq,
+                             const int64_t* pre_n, mia_stream_t stream) {
   MIA_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && sizes && sqnorm_ws, "clip_adam: null table");
   MIA_CHECK_ARG(ntensors > 0 && ntensors < 65536 && step >= 1, "clip_adam: ntensors/step");
+  MIA_CHECK_ARG(!pre_sq || pre_n, "clip_adam: pre_sq needs pre_n");
   hipStream_t s = as_stream(stream);
   double* ws = reinterpret_cast<double*>(sqnorm_ws);
   float* coef = reinterpret_cast<float*>(ws + (int64_t)ntensors * ADAM_PARTS);
   const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 256)));
-  sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, reinterpret_cast<float*>(ws));
+  sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, pre_sq, pre_n, reinterpret_cast<float*>(ws));
   MIA_LAUNCH_CHECK("sqnorm");
   norm_final_kernel<<<1, NF_NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);
   MIA_LAUNCH_CHECK("norm_final");

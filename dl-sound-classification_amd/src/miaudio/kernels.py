@@ -65,7 +65,9 @@ def conv(t: torch.Tensor, layout: int, n, h, w, c, oh, ow, kh, kw, sh=1, sw=1, p
 
 def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=None, ldaux: int = 0,
              accumulate: bool = False, alpha: float = 1.0, act_scale: float = 1.0,
-             rowmap=None) -> L.MiaEpilogue:
+             rowmap=None, sqsum=None) -> L.MiaEpilogue:
+    """Output descriptor of a GEMM.  ``sqsum``: optional f64 tensor of ``mia_gemm_sqsum_slots(M, N)``
+    entries that receives the per-tile sums of squares of a plain f32 output (see ``sqsum_slots``)."""
     e = L.MiaEpilogue()
     e.ptr = out.data_ptr()
     e.dtype = L.dtype_code(out)
@@ -81,8 +83,38 @@ def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=
         e.ldaux = ldaux
     e.alpha = alpha
     e.act_scale = act_scale
-    e._keep = (out, bias, aux)
+    e.sqsum = L.ptr(sqsum)
+    e._keep = (out, bias, aux, sqsum)
     return e
+
+
+def sqsum_slots(out: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    """A sum-of-squares slot buffer (f64, one per 128 x 128 tile) for the plain f32 GEMM output ``out``
+    (M x N); pass it as ``epilogue(..., sqsum=)``, then ``tag_sqsum(param, out, buf)``."""
+    buf = torch.empty(int(L.load().mia_gemm_sqsum_slots(M, N)), dtype=torch.float64, device=out.device)
+    return buf
+
+
+def tag_sqsum(param: torch.Tensor, grad: torch.Tensor, buf: torch.Tensor) -> None:
+    """Record on ``param`` that ``buf`` holds the per-tile sums of squares of the gradient ``grad``, so
+    FusedAdam's clip-norm pass reads the slots instead of the tensor.  The tag lives on the parameter
+    (autograd hands ``grad``'s storage on as ``param.grad`` under a new Python object) and holds
+    ``grad``'s storage -- not ``grad``: a second tensor reference would make autograd copy the gradient
+    instead of adopting it -- so that memory cannot be reused by another tensor while tagged; with the
+    version it records, any later write to the gradient (an all-reduce, an accumulation) invalidates it."""
+    param._mia_sqsum = (buf, grad.untyped_storage(), grad.data_ptr(), grad.numel(), grad._version)
+
+
+def valid_sqsum(param: torch.Tensor, grad: torch.Tensor):
+    """The slot buffer tagged on ``param`` if it still describes ``grad``'s current contents, else None."""
+    tag = getattr(param, "_mia_sqsum", None)
+    if tag is None:
+        return None
+    buf, st, ptr, numel, ver = tag
+    if (grad.untyped_storage().data_ptr() != st.data_ptr() or grad.data_ptr() != ptr or grad.numel() != numel
+            or grad._version != ver):
+        return None
+    return buf
 
 
 def _tiles(M, N):

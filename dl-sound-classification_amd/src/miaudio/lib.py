@@ -41,7 +41,7 @@ class MiaEpilogue(C.Structure):
     _fields_ = [("ptr", vp), ("dtype", i32), ("act", i32), ("accumulate", i32), ("aux_dtype", i32),
                 ("ldc", i64), ("rm_inner", i64), ("rm_outer", i64), ("rm_istride", i64),
                 ("rm_offset", i64), ("bias", vp), ("aux", vp), ("ldaux", i64),
-                ("alpha", f32), ("act_scale", f32)]
+                ("alpha", f32), ("act_scale", f32), ("sqsum", vp)]
 
 
 class MiaMelCfg(C.Structure):
@@ -54,6 +54,7 @@ P = C.POINTER
 # name -> (restype, argtypes)
 SIGNATURES = {
     "mia_gemm_workspace_bytes": (i64, [i64, i64, i32]),
+    "mia_gemm_sqsum_slots": (i64, [i64, i64]),
     "mia_gemm": (C.c_int, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32, vp, vp]),
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
     "mia_gemm_set_policy": (C.c_int, [i32]),
@@ -94,7 +95,8 @@ SIGNATURES = {
     "mia_dropout": (C.c_int, [vp, i32, i64, f32, C.c_uint64, vp]),
     "mia_soft_ce": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "mia_adam_workspace_bytes": (i64, [i32]),
-    "mia_clip_adam": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp]),
+    "mia_clip_adam": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp, vp,
+                                vp]),
     "mia_layernorm_fwd": (C.c_int, [vp, i32, vp, vp, vp, i32, vp, vp, i64, i32, f32, vp]),
     "mia_layernorm_bwd": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp, vp, i64, i32, vp]),
     "mia_layernorm_partial_bytes": (i64, [i64, i32]),

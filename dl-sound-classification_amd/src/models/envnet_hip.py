@@ -307,8 +307,13 @@ class EnvNetFunction(torch.autograd.Function):
             fout, fin = Wt.shape
             hin = acts[li]
             dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
-            K.gemm(K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), K.epilogue(dW, fin), fout, fin, B, cd,
-                   tag=f"fc{li + 1}.wgrad")
+            # FC1/FC2: the GEMM epilogue also writes per-tile sums of squares of dW, so the clip-norm
+            # pass of FusedAdam does not re-read the 1.4 GB (K.sqsum_slots)
+            sq = K.sqsum_slots(dW, fout, fin) if li < 2 else None
+            K.gemm(K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), K.epilogue(dW, fin, sqsum=sq), fout,
+                   fin, B, cd, tag=f"fc{li + 1}.wgrad")
+            if sq is not None:
+                K.tag_sqsum(p[40 + 2 * li], dW, sq)
             grads[40 + 2 * li] = dW
             grads[41 + 2 * li] = K.colsum(dcur, B, fout)
             if li > 0:

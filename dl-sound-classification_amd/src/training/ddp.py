@@ -76,6 +76,7 @@ class GradAllReducer:
             if id(p) not in self.index or id(p) in self.done:
                 continue
             p.grad = g
+            p._mia_sqsum = None  # the averaged gradient is not what the GEMM's per-tile sums describe
             self.done.add(id(p))
             self.fired += 1
             (big if g.numel() * g.element_size() >= self.bucket_bytes // 4 else small).append(g)
@@ -87,6 +88,8 @@ class GradAllReducer:
     def finish(self):
         """Reduce every gradient not yet reduced, then wait for all buckets (on the compute stream)."""
         rest = [p.grad for p in self.params if p.grad is not None and id(p) not in self.done]
+        for p in self.params:
+            p._mia_sqsum = None
         bucket, size = [], 0
         for g in rest:
             bucket.append(g)

@@ -35,6 +35,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self.clip = float(clip or 0.0)
         self.last_total_norm = None
+        self.last_precomputed = 0  # tensors whose norm came from their GEMM's per-tile sums (last step)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -64,11 +65,18 @@ class FusedAdam(torch.optim.Optimizer):
         # parameters with a live bf16 operand copy (K.bf16_shadow) get it rewritten in the update pass
         shadows = [getattr(p, "_mia_bf16", None) if getattr(p, "_mia_bf16_ver", None) == p._version else None
                    for p in ps]
-        table = torch.tensor([[p.data_ptr() for p in ps], [g.data_ptr() for g in gs],
-                              [self.state[p]["exp_avg"].data_ptr() for p in ps],
-                              [self.state[p]["exp_avg_sq"].data_ptr() for p in ps],
-                              [0 if sh is None else sh.data_ptr() for sh in shadows],
-                              [p.numel() for p in ps]], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        # gradients whose producing GEMM left per-tile sums of squares (K.sqsum_slots) skip the norm read
+        pre = [K.valid_sqsum(p, g) for p, g in zip(ps, gs)]
+        self.last_precomputed = sum(q is not None for q in pre)
+        have_pre = self.last_precomputed > 0
+        rows = [[p.data_ptr() for p in ps], [g.data_ptr() for g in gs],
+                [self.state[p]["exp_avg"].data_ptr() for p in ps],
+                [self.state[p]["exp_avg_sq"].data_ptr() for p in ps],
+                [0 if sh is None else sh.data_ptr() for sh in shadows],
+                [p.numel() for p in ps]]
+        if have_pre:
+            rows += [[0 if q is None else q.data_ptr() for q in pre], [0 if q is None else q.numel() for q in pre]]
+        table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         n = len(ps)
         lib = L.load()
         ws = K.workspace(lib.mia_adam_workspace_bytes(n), dev, "adam")
@@ -78,16 +86,21 @@ class FusedAdam(torch.optim.Optimizer):
         # p, m, v written (28 B/param) + the bf16 operand copies rewritten (2 B/param where shadowed)
         nel = sum(p.numel() for p in ps)
         nbytes = 32 * nel + 2 * sum(p.numel() for p, sh in zip(ps, shadows) if sh is not None)
+        nbytes -= 4 * sum(g.numel() for g, q in zip(gs, pre) if q is not None)
         with K.probe("optim.step", 0.0, nbytes):
             L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
                                       table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
                                       max(p.numel() for p in ps),
                                       float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
                                       float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
+                                      table[6].data_ptr() if have_pre else None,
+                                      table[7].data_ptr() if have_pre else None,
                                       L.stream_ptr()), "mia_clip_adam")
         self.last_total_norm = tot
         for p, sh in zip(ps, shadows):
             if sh is not None:
                 p._mia_bf16_ver = p._version  # the copy now matches the updated parameter
-        self._keep = (table, gs)  # keep the pointer table alive until the next step
+        for p in ps:
+            p._mia_sqsum = None  # consumed (or stale): the next step's gradient brings its own
+        self._keep = (table, gs, pre)  # keep the pointer table alive until the next step
         return loss

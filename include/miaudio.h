@@ -73,6 +73,10 @@ typedef struct MiaEpilogue {
   const void* aux;
   int64_t ldaux;
   float alpha, act_scale;
+  /* Optional (NULL = off): per 128x128 output tile (bm, bn), slot bm * ceil(N/128) + bn receives the
+   * sum of squares of the values the GEMM stored there (double), for a gradient-clip norm that does
+   * not re-read the output.  Plain f32 output only (no act / bias / accumulate / row map, alpha 1). */
+  double* sqsum;
 } MiaEpilogue;
 
 /* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16; f32: v_mfma_f32_32x32x2_f32).
@@ -81,6 +85,8 @@ typedef struct MiaEpilogue {
  * ast.py:38,60-61) and the AST patch-embed conv (ast.py:30,55).
  * split_k > 1 needs a workspace of mia_gemm_workspace_bytes(M,N,split_k) bytes. */
 int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k);
+/* number of MiaEpilogue.sqsum slots (doubles) of an M x N output */
+int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N);
 int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
              int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
              mia_stream_t stream);
@@ -348,13 +354,16 @@ int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32
  * shadow_bf16: optional table of bf16* (entries may be NULL): the bf16 GEMM-operand copy of each
  * updated parameter is written in the same pass (replaces a separate cast of the weights).
  * sqnorm_ws: f32 workspace of mia_adam_workspace_bytes(ntensors) bytes.
+ * pre_sq / pre_n (optional device tables, may be NULL): for tensor i with pre_sq[i] != NULL the norm
+ * pass reads pre_n[i] partial sums of squares (doubles, e.g. a GEMM's MiaEpilogue.sqsum slots of the
+ * gradient it wrote) instead of re-reading grads[i]; the partials are added in a fixed order.
  * clip <= 0 disables clipping. step is 1-based. */
 int64_t mia_adam_workspace_bytes(int32_t ntensors);
 int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
                   void* const* exp_avg_sq, void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors,
                   int64_t max_numel, float lr, float beta1, float beta2, float eps,
                   float weight_decay, int32_t step, float clip, float* total_norm_out,
-                  void* sqnorm_ws, mia_stream_t stream);
+                  void* sqnorm_ws, const void* const* pre_sq, const int64_t* pre_n, mia_stream_t stream);
 
 /* LayerNorm over the last dim (timm Block norm1/norm2 and final norm, eps 1e-6).
  * x: (rows, D) -> y dtype; mean/rstd f32[rows] saved for backward. */

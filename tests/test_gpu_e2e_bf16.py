@@ -79,6 +79,7 @@ def test_envnet_bf16_train_step_vs_autocast_oracle(cuda):
     before = {n: p.detach().clone() for n, p in m.named_parameters()}
     opt = FusedAdam(m.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
     opt.step()
+    assert opt.last_precomputed == 2  # FC1/FC2 weight-gradient norms came from their GEMM epilogues
     deltas = {n: p.detach() - before[n] for n, p in m.named_parameters()}
 
     def ref(autocast):

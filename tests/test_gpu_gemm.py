@@ -637,3 +637,47 @@ def test_trunk_w2_dense(cuda, B, H, W, cin, cout):
     for kx in range(2):
         dxref[:, kx:kx + W - 1] += torch.einsum("rxo,oi->rxi", d4, wb[:, :, kx])
     assert rel(dx.double().cpu().view(B * H, W, cin), dxref) < 1e-2
+
+
+def _tile_sqsums(out, M, N):
+    nbm, nbn = -(-M // 128), -(-N // 128)
+    ref = torch.zeros(nbm * nbn, dtype=torch.float64)
+    o = out.double().cpu()
+    for bm in range(nbm):
+        for bn in range(nbn):
+            ref[bm * nbn + bn] = o[bm * 128:(bm + 1) * 128, bn * 128:(bn + 1) * 128].square().sum()
+    return ref
+
+
+@pytest.mark.parametrize("cd,M,N,Kd,split,la", [
+    (L.BF16, 384, 512, 256, 1, L.RC),   # dense kernel, full tiles (staged-tile epilogue)
+    (L.BF16, 200, 328, 128, 1, L.RC),   # dense kernel, ragged edge tiles (generic epilogue)
+    (L.BF16, 256, 384, 1024, 4, L.RC),  # split-K: per-tile pass after the reduce
+    (L.BF16, 256, 256, 192, 1, L.KC),   # another layout on the dense kernel
+    (L.F32, 150, 260, 40, 1, L.KC),     # tile kernel: per-tile pass
+])
+def test_sqsum_epilogue(cuda, cd, M, N, Kd, split, la):
+    """MiaEpilogue.sqsum (EnvNet FC wgrad -> clip norm): per-128x128-tile sums of squares of exactly
+    the values stored, on every path (fused in the dense kernel, a separate pass elsewhere)."""
+    g = torch.Generator().manual_seed(M + N + split)
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    a, A, ta = _mat(la, M, Kd, dt, cuda, g)
+    b, Bo, tb = _mat(L.RC, N, Kd, dt, cuda, g)
+    out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+    sq = K.sqsum_slots(out, M, N)
+    sq.fill_(float("nan"))
+    K.gemm(A, Bo, K.epilogue(out, N, sqsum=sq), M, N, Kd, cd, split_k=split)
+    torch.cuda.synchronize()
+    assert rel(out.cpu(), a.double() @ b.double().t()) < TOL[cd]
+    ref = _tile_sqsums(out, M, N)
+    assert torch.isfinite(sq).all()
+    assert torch.allclose(sq.cpu(), ref, rtol=1e-5, atol=0)
+
+
+def test_sqsum_needs_plain_f32(cuda):
+    out = torch.empty(128, 128, dtype=torch.bfloat16, device=cuda)
+    sq = torch.empty(1, dtype=torch.float64, device=cuda)
+    x = torch.randn(128, 64, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        K.gemm(K.dense(x, L.KC, 128, 64), K.dense(x, L.KC, 128, 64), K.epilogue(out, 128, sqsum=sq), 128, 128, 64,
+               L.BF16)

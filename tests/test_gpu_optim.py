@@ -33,3 +33,41 @@ def test_adam_refreshes_bf16_shadow(cuda):
     with torch.no_grad():
         ps[1].mul_(2.0)  # any other in-place change invalidates the copy
     assert torch.equal(K.bf16_shadow(ps[1]), ps[1].detach().to(torch.bfloat16))
+
+
+def test_adam_precomputed_sqsum(cuda):
+    """A gradient tagged with its GEMM's per-tile sums of squares (K.tag_sqsum) is not re-read by the
+    norm pass; the step matches torch's clip + Adam, and a stale tag (gradient written since) is
+    ignored."""
+    from src.miaudio import lib as L
+    g = torch.Generator().manual_seed(3)
+    M, N, Kd = 256, 384, 128
+    ps = [torch.nn.Parameter((0.05 * torch.randn(M, N, generator=g)).to(cuda)),
+          torch.nn.Parameter(torch.randn(77, generator=g).to(cuda))]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedAdam(ps, lr=1e-2, weight_decay=1e-4, clip=0.5)
+    ropt = torch.optim.Adam(ref, lr=1e-2, weight_decay=1e-4)
+    for it in range(3):
+        a = torch.randn(Kd, M, generator=g).to(torch.bfloat16).to(cuda)
+        b = torch.randn(Kd, N, generator=g).to(torch.bfloat16).to(cuda)
+        dW = torch.empty(M, N, dtype=torch.float32, device=cuda)
+        sq = K.sqsum_slots(dW, M, N)
+        K.gemm(K.dense(a, L.RC, Kd, M), K.dense(b, L.RC, Kd, N), K.epilogue(dW, N, sqsum=sq), M, N, Kd, L.BF16)
+        K.tag_sqsum(ps[0], dW, sq)
+        if it == 2:
+            dW.mul_(0.5)  # written after the GEMM: the tag no longer describes it
+            assert K.valid_sqsum(ps[0], dW) is None
+        else:
+            assert K.valid_sqsum(ps[0], dW) is sq
+            assert K.valid_sqsum(ps[0], dW.clone()) is None
+        gb = torch.randn(77, generator=g).to(cuda)
+        ps[0].grad, ps[1].grad = dW, gb.clone()
+        ref[0].grad, ref[1].grad = dW.clone(), gb.clone()
+        opt.step()
+        total = torch.nn.utils.clip_grad_norm_(ref, 0.5)
+        ropt.step()
+        torch.cuda.synchronize()
+        assert abs(float(opt.last_total_norm) - float(total)) <= 1e-5 * float(total)
+        for p, r in zip(ps, ref):
+            assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
+        assert ps[0]._mia_sqsum is None  # consumed
