@@ -1426,10 +1426,13 @@ bool tapconv_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, 
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
 
-// block-wide sum of one double per thread (4 waves), written by thread 0: a tile's sum of squares
-__device__ __forceinline__ void tile_sqsum_store(double* dst, double v) {
-  __shared__ double red[NT / 64];
+// block-wide sum of one double per thread (4 waves), written by thread 0: a tile's sum of squares.
+// `red` is NT/64 doubles of the caller's LDS (inside a GEMM kernel: its one staging array -- a second
+// __shared__ object there makes hipcc wait vmcnt(0) at every K-step barrier); the leading barrier
+// lets the caller's last reads of that space finish first.
+__device__ __forceinline__ void tile_sqsum_store(double* dst, double v, double* red) {
   v = wave_sum_d(v);
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1454,7 +1457,8 @@ __global__ __launch_bounds__(NT) void tile_sqsum_kernel(const float* __restrict_
       sq = fmaf(v, v, sq);
     }
   }
-  tile_sqsum_store(out + blockIdx.x, (double)sq);
+  __shared__ double red[NT / 64];
+  tile_sqsum_store(out + blockIdx.x, (double)sq, red);
 }
 
 template <int L>
@@ -1504,6 +1508,8 @@ __device__ __forceinline__ bf16x8 dfrag(const char* tile, int rbase, int ks, int
     const int col = rbase + 16 * (gq & 1) + 4 * (i16 & 3);
     const int kr = ks * 16 + 8 * (gq >> 1) + (i16 >> 2);
     const char* p0 = tile + kr * 256 + (((col >> 4) ^ (kr & 3)) * 32) + (col & 15) * 2;
+    // (hipcc waits vmcnt(0) -- for the next tile's DMA -- before the first of these builtin reads in
+    // each K-step; an inline-asm variant without that wait measured the same on the wgrad shapes)
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0 + 4 * 256));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -1511,6 +1517,7 @@ __device__ __forceinline__ bf16x8 dfrag(const char* tile, int rbase, int ks, int
     return __builtin_bit_cast(bf16x8, cc);
   }
 }
+
 
 template <int LA, int LB>
 __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
@@ -1617,7 +1624,7 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       __builtin_nontemporal_store(v, dst);
       if (g.e.sqsum) sq = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], sq))));
     }
-    if (g.e.sqsum) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq);
+    if (g.e.sqsum) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq, reinterpret_cast<double*>(smem));
     return;
   }
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
@@ -1716,7 +1723,8 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       }
       __syncthreads();
     }
-  if (g.e.sqsum && g.split == 1) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, sqg);
+  if (g.e.sqsum && g.split == 1)
+    tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, sqg, reinterpret_cast<double*>(smem));
 }
 
 bool dgemm_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, int64_t K, int compute) {
