@@ -375,17 +375,19 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
                                                         int xdt, const float* __restrict__ g,
                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
                                                         void* dx, int dxdt, int accumulate, void* dx2, int dx2dt,
-                                                        float* __restrict__ partial, int64_t rows) {
+                                                        float* __restrict__ partial, int64_t rows, int cs) {
+  // cs: also the column sums of the stored dx2 values (the next linear's bias gradient); partial
+  // rows are then [blk][3][D] instead of [blk][2][D]
   constexpr int D = 64 * PER;
-  __shared__ float red[4][2][D];
+  __shared__ float red[4][3][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d0 = lane * PER;
   float gg[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) gg[i] = g[d0 + i];
-  float ag[PER], ab[PER];
+  float ag[PER], ab[PER], ac[PER];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
+  for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; ac[i] = 0.f; }
   const int64_t r0 = (int64_t)blockIdx.x * LN_VEC_ROWS;
   for (int64_t row = r0 + wave; row < r0 + LN_VEC_ROWS && row < rows; row += 4) {
     const float mu = mean[row], rs = rstd[row];
@@ -415,23 +417,32 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
     }
     stv<PER>(dx, dxdt, row * D + d0, o);
     if (dx2) stv<PER>(dx2, dx2dt, row * D + d0, o);
-  }
+    if (cs) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) { red[wave][0][d0 + i] = ag[i]; red[wave][1][d0 + i] = ab[i]; }
+      for (int i = 0; i < PER; ++i) ac[i] += dx2dt == MIA_BF16 ? (float)(bf16)o[i] : o[i];
+    }
+  }
+  const int nq = cs ? 3 : 2;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { red[wave][0][d0 + i] = ag[i]; red[wave][1][d0 + i] = ab[i]; red[wave][2][d0 + i] = ac[i]; }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * D; i += NT) {
+  for (int i = threadIdx.x; i < nq * D; i += NT) {
     const int q = i / D, d = i % D;
-    partial[(int64_t)blockIdx.x * 2 * D + i] = ((red[0][q][d] + red[1][q][d]) + red[2][q][d]) + red[3][q][d];
+    partial[(int64_t)blockIdx.x * nq * D + i] = ((red[0][q][d] + red[1][q][d]) + red[2][q][d]) + red[3][q][d];
   }
 }
 
-__global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, float* dgamma, float* dbeta) {
+// partial rows [blk][nq][D] -> dgamma, dbeta (and, nq == 3, the dx2 column sums), in double
+__global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, int nq, float* dgamma,
+                                        float* dbeta, float* colsum) {
   const int d = blockIdx.x;  // one block per feature
-  const double a = block_sum_strided(partial + d, nblk, 2 * (int64_t)D);
-  const double b = block_sum_strided(partial + D + d, nblk, 2 * (int64_t)D);
+  const double a = block_sum_strided(partial + d, nblk, nq * (int64_t)D);
+  const double b = block_sum_strided(partial + D + d, nblk, nq * (int64_t)D);
+  const double c = nq == 3 ? block_sum_strided(partial + 2 * D + d, nblk, nq * (int64_t)D) : 0.0;
   if (threadIdx.x != 0) return;
   if (dgamma) dgamma[d] = (float)a;
   if (dbeta) dbeta[d] = (float)b;
+  if (colsum) colsum[d] = (float)c;
 }
 
 constexpr int LN_ROWS_PER_BLOCK = 256;
@@ -566,14 +577,16 @@ extern "C" int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gam
 }
 
 extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
-  return cdiv(rows, LN_VEC_ROWS) * 2 * D * 4;
+  const int64_t a = cdiv(rows, LN_VEC_ROWS) * 3 * D * 4, b = cdiv(rows, 256) * 2 * D * 4;
+  return a > b ? a : b;
 }
 
-extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
-                                 const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
-                                 void* dx2, int32_t dx2dtype, float* dgamma, float* dbeta, void* partial, int64_t rows,
-                                 int32_t D, mia_stream_t stream) {
+static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
+                              const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
+                              void* dx2, int32_t dx2dtype, float* dgamma, float* dbeta, float* dx2_colsum,
+                              void* partial, int64_t rows, int32_t D, mia_stream_t stream) {
   MIA_CHECK_ARG(dy && x && gamma && mean && rstd && dx && partial, "layernorm_bwd: null pointer");
+  MIA_CHECK_ARG(!dx2_colsum || dx2, "layernorm_bwd: the column sums are of dx2");
   MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_bwd: D must be <= 1024");
   hipStream_t s = as_stream(stream);
   unsigned nb;
@@ -581,7 +594,7 @@ extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x,
   if (D == 768 && al) {
     nb = (unsigned)cdiv(rows, LN_VEC_ROWS);
     ln_bwd_vec_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
-                                            dx2, dx2dtype, (float*)partial, rows);
+                                            dx2, dx2dtype, (float*)partial, rows, dx2_colsum ? 1 : 0);
   } else {
     MIA_CHECK_ARG(dx2 == nullptr, "layernorm_bwd: the bf16 copy needs D == 768 and aligned rows");
     nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
@@ -593,7 +606,26 @@ extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x,
                                           (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
   }
   MIA_LAUNCH_CHECK("layernorm_bwd");
-  ln_partial_final_kernel<<<(unsigned)D, 256, 0, s>>>((const float*)partial, (int)nb, D, dgamma, dbeta);
+  ln_partial_final_kernel<<<(unsigned)D, 256, 0, s>>>((const float*)partial, (int)nb, D, dx2_colsum ? 3 : 2, dgamma,
+                                                      dbeta, dx2_colsum);
   MIA_LAUNCH_CHECK("layernorm_partial_final");
   return 0;
+}
+
+extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
+                                 const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
+                                 void* dx2, int32_t dx2dtype, float* dgamma, float* dbeta, void* partial, int64_t rows,
+                                 int32_t D, mia_stream_t stream) {
+  return layernorm_bwd_impl(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate, dx2, dx2dtype, dgamma,
+                            dbeta, nullptr, partial, rows, D, stream);
+}
+
+extern "C" int mia_layernorm_bwd_colsum(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
+                                        const float* gamma, const float* mean, const float* rstd, void* dx,
+                                        int32_t dxdtype, int32_t accumulate, void* dx2, int32_t dx2dtype,
+                                        float* dgamma, float* dbeta, float* dx2_colsum, void* partial, int64_t rows,
+                                        int32_t D, mia_stream_t stream) {
+  MIA_CHECK_ARG(dx2_colsum && dx2 && D == 768, "layernorm_bwd_colsum: needs dx2, dx2_colsum and D == 768");
+  return layernorm_bwd_impl(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate, dx2, dx2dtype, dgamma,
+                            dbeta, dx2_colsum, partial, rows, D, stream);
 }

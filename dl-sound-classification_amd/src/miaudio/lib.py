@@ -100,6 +100,8 @@ SIGNATURES = {
     "mia_layernorm_fwd": (C.c_int, [vp, i32, vp, vp, vp, i32, vp, vp, i64, i32, f32, vp]),
     "mia_layernorm_bwd": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp, vp, i64, i32, vp]),
     "mia_layernorm_partial_bytes": (i64, [i64, i32]),
+    "mia_layernorm_bwd_colsum": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp, vp, vp, i64,
+                                           i32, vp]),
     "mia_attn_fwd": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_workspace_bytes": (C.c_int64, [i32, i32, i32, i32]),

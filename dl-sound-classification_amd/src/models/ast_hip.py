@@ -32,17 +32,27 @@ def _ln(x, g, b, out_dtype, rows, D):
 
 def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool, dx2=None):
     """LayerNorm backward into dx (optionally accumulating); dx2 receives a second copy of the result
-    (the bf16 operand of the next linear backward)."""
+    (the bf16 operand of the next linear backward).  Returns (dgamma, dbeta, colsum(dx2) or None): with
+    dx2 the column sums of its stored values -- the next linear's bias gradient -- come from the same
+    pass (mia_layernorm_bwd_colsum)."""
     dg = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty(D, dtype=torch.float32, device=x.device)
     lib = L.load()
     ws = K.workspace(lib.mia_layernorm_partial_bytes(rows, D), x.device, "ln")
+    if dx2 is not None and D == 768:
+        cs = torch.empty(D, dtype=torch.float32, device=x.device)
+        L.check(lib.mia_layernorm_bwd_colsum(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x),
+                                             g.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                             L.dtype_code(dx), int(accumulate), dx2.data_ptr(), L.dtype_code(dx2),
+                                             dg.data_ptr(), db.data_ptr(), cs.data_ptr(), ws.data_ptr(), rows, D,
+                                             L.stream_ptr()), "mia_layernorm_bwd_colsum")
+        return dg, db, cs
     L.check(lib.mia_layernorm_bwd(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x), g.data_ptr(),
                                   mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), L.dtype_code(dx), int(accumulate),
                                   L.ptr(dx2), L.dtype_code(dx2) if dx2 is not None else 0, dg.data_ptr(),
                                   db.data_ptr(), ws.data_ptr(), rows, D, L.stream_ptr()),
             "mia_layernorm_bwd")
-    return dg, db
+    return dg, db, None
 
 
 def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, tag=None):
@@ -52,15 +62,17 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
            K.epilogue(out, Nf, act=act, bias=bias, aux=aux, ldaux=Nf), M, Nf, Kf, cd, tag=tag)
 
 
-def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag=""):
-    """dW = dy^T x (f32), db = colsum(dy), dx = dy @ W (optionally with an activation backward)."""
+def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None):
+    """dW = dy^T x (f32), db = colsum(dy) (unless the producer of dy already summed it), dx = dy @ W
+    (optionally with an activation backward)."""
     Nf, Kf = W.shape
     if cd == L.BF16 and dy.dtype == torch.float32:
         dy = K.cast(dy, torch.bfloat16)  # bf16 GEMM operands (f32 accumulation inside)
     dW = torch.empty(Nf, Kf, dtype=torch.float32, device=dy.device)
     K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf), Nf, Kf, M, cd,
            tag=tag + ".wgrad")
-    db = K.colsum(dy, M, Nf)
+    if db is None:
+        db = K.colsum(dy, M, Nf)
     if dx_out is not None:
         K.gemm(K.dense(dy, L.KC, M, Nf), K.dense(W, L.RC, Nf, Kf),
                K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf),
@@ -160,7 +172,7 @@ class ASTFunction(torch.autograd.Function):
         dhc = torch.empty(B, D, dtype=torch.float32, device=dev)
         dWh, dbh = _linear_bwd(dz, s["hc"], wh, B, cd, dx_out=dhc, tag="head")
         dxc = torch.empty(B, D, dtype=torch.float32, device=dev)
-        dgn, dbn = _ln_bwd(dhc, s["xc"], gn, s["mc"], s["rc"], dxc, B, D, False)
+        dgn, dbn, _ = _ln_bwd(dhc, s["xc"], gn, s["mc"], s["rc"], dxc, B, D, False)
         grads[4 + 12 * nb: 8 + 12 * nb] = [dgn, dbn, dWh, dbh]
         emit(4 + 12 * nb, 8 + 12 * nb)
         dx = torch.zeros(Tt, D, dtype=torch.float32, device=dev)
@@ -168,6 +180,7 @@ class ASTFunction(torch.autograd.Function):
         # bf16 mode: a bf16 copy of the residual gradient feeds the next linear backward's GEMMs
         dxb = K.cast(dx, torch.bfloat16) if cd == L.BF16 else dx
         dxb2 = torch.empty_like(dxb) if cd == L.BF16 else None
+        db_next = None  # column sums of dxb from the LayerNorm backward that wrote it (bf16 mode)
         for i in reversed(range(nb)):
             sb = s["blocks"][i]
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = p[4 + 12 * i: 16 + 12 * i]
@@ -175,16 +188,16 @@ class ASTFunction(torch.autograd.Function):
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
             dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
-                                    tag="fc2")
+                                    tag="fc2", db=db_next)
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
             dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1")
-            dg2, dbt2 = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2)  # dx = d(xm)
+            dg2, dbt2, db_proj = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2)  # d(xm)
             if dxb2 is not None:
                 dxb, dxb2 = dxb2, dxb
             else:
                 dxb = dx
             da = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj")
+            dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj", db=db_proj)
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
             work = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8, device=dev)
             with K.probe("attn.bwd", 10.0 * B * Hh * N * N * (D // Hh),
@@ -194,7 +207,7 @@ class ASTFunction(torch.autograd.Function):
                                               s["scale"], L.stream_ptr()), "mia_attn_bwd")
             dh = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")
-            dg1, dbt1 = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2)  # d(block input)
+            dg1, dbt1, db_next = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2)  # d(block in)
             if dxb2 is not None:
                 dxb, dxb2 = dxb2, dxb
             else:

@@ -378,6 +378,14 @@ int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x, int32_t xd
                       const float* gamma, const float* mean, const float* rstd, void* dx,
                       int32_t dxdtype, int32_t accumulate, void* dx2, int32_t dx2dtype, float* dgamma,
                       float* dbeta, void* partial, int64_t rows, int32_t D, mia_stream_t stream);
+/* As mia_layernorm_bwd, also writing dx2_colsum[D] = sum over rows of the stored dx2 values: the
+ * bias gradient of the linear whose backward takes dx2 as its dy (timm Block proj / fc2 biases,
+ * replacing a separate column-sum pass over the residual gradient).  D == 768, dx2 required. */
+int mia_layernorm_bwd_colsum(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
+                             const float* gamma, const float* mean, const float* rstd, void* dx,
+                             int32_t dxdtype, int32_t accumulate, void* dx2, int32_t dx2dtype, float* dgamma,
+                             float* dbeta, float* dx2_colsum, void* partial, int64_t rows, int32_t D,
+                             mia_stream_t stream);
 int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
 
 /* Fused multi-head attention (timm Attention with F.scaled_dot_product_attention,

@@ -127,11 +127,42 @@ def test_layernorm(cuda, D):
     tx, tw, tb = x.to(cuda), w.to(cuda), b.to(cuda)
     yo, m, r = _ln(tx, tw, tb, torch.float32, 300, D)
     dx = torch.ones(300, D, device=cuda)
-    dg, db = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx, 300, D, True)
+    dg, db, cs = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx, 300, D, True)
     torch.cuda.synchronize()
+    assert cs is None
     assert rel(yo, y) < 1e-5
     assert rel(dx - 1.0, xr.grad) < 1e-4
     assert rel(dg, wr.grad) < 1e-4 and rel(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("rows", [300, 4096 + 17])
+def test_layernorm_bwd_colsum(cuda, rows):
+    """The LayerNorm backward that also returns the column sums of its bf16 copy dx2 (the proj / fc2
+    bias gradients in the AST backward): dx, dx2, dgamma, dbeta bit-identical to the plain backward,
+    the column sums equal to float64 sums of the stored dx2."""
+    from src.models.ast_hip import _ln, _ln_bwd
+    D = 768
+    g = torch.Generator(device=cuda).manual_seed(rows)
+    x = torch.randn(rows, D, generator=g, device=cuda) * 2 + 1
+    w = torch.rand(D, generator=g, device=cuda) + 0.5
+    b = torch.randn(D, generator=g, device=cuda)
+    dy = torch.randn(rows, D, generator=g, device=cuda).to(torch.bfloat16)
+    acc0 = torch.randn(rows, D, generator=g, device=cuda)
+    _, m, r = _ln(x, w, b, torch.bfloat16, rows, D)
+    dxa, dxb = acc0.clone(), acc0.clone()
+    d2a = torch.empty(rows, D, dtype=torch.bfloat16, device=cuda)
+    d2b = torch.empty_like(d2a)
+    lib = L.load()
+    dga, dba = torch.empty(D, device=cuda), torch.empty(D, device=cuda)
+    ws = torch.empty(int(lib.mia_layernorm_partial_bytes(rows, D)), dtype=torch.uint8, device=cuda)
+    L.check(lib.mia_layernorm_bwd(dy.data_ptr(), L.BF16, x.data_ptr(), L.F32, w.data_ptr(), m.data_ptr(), r.data_ptr(),
+                                  dxa.data_ptr(), L.F32, 1, d2a.data_ptr(), L.BF16, dga.data_ptr(), dba.data_ptr(),
+                                  ws.data_ptr(), rows, D, L.stream_ptr()), "ln_bwd")
+    dgb, dbb, cs = _ln_bwd(dy, x, w, m, r, dxb, rows, D, True, dx2=d2b)
+    torch.cuda.synchronize()
+    assert torch.equal(dxa, dxb) and torch.equal(d2a, d2b)
+    assert torch.equal(dga, dgb) and torch.equal(dba, dbb)
+    assert rel(cs, d2b.double().sum(0)) < 1e-5
 
 
 def _ast(cuda, compute):
