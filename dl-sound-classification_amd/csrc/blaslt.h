@@ -21,5 +21,13 @@ int policy();
 int choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K);
 void set_choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
                 int v);
+// whether run() delivers E.colsum itself (the dGELU pass sums its output's columns, GELU_CS_BLOCKS
+// row walkers with one f32 partial row each in the 64 MB library workspace)
+constexpr int GELU_CS_BLOCKS = 2048;
+inline bool fuses_colsum(const MiaEpilogue& E, int64_t N) {
+  return E.colsum && E.act == MIA_DACT_GELU && (size_t)GELU_CS_BLOCKS * N * 4 <= (64ull << 20);
+}
+// the device's library workspace (stream-ordered scratch) if `bytes` fit, else null
+void* scratch(size_t bytes);
 
 }  // namespace mblas

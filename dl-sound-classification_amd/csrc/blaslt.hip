@@ -180,9 +180,63 @@ __global__ __launch_bounds__(256) void gelu_rows_kernel(const bf16* __restrict__
   }
 }
 
+// dGELU pass that also sums its output's columns (MiaEpilogue.colsum: the bias gradient of the linear
+// whose dy this is -- timm Block fc1 behind the fc2 dgrad): block (bx, by) walks the row groups bx,
+// bx + gridDim.x, ... of 2048-column slab by, with the column sums of the stored bf16 values in
+// registers, then writes partial[bx][N]; gelu_cs_final_kernel adds the partials in order in double.
+__global__ __launch_bounds__(256) void gelu_dact_cs_kernel(const bf16* __restrict__ src, int64_t lds,
+                                                           bf16* __restrict__ out, int64_t ldo, int64_t rows,
+                                                           int cols8, int N, float* __restrict__ partial) {
+  const int c8 = blockIdx.y * 256 + threadIdx.x;
+  if (c8 >= cols8) return;  // no barriers below
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t r0 = (int64_t)blockIdx.x * GELU_ROWS; r0 < rows; r0 += (int64_t)gridDim.x * GELU_ROWS) {
+    uint4 u[GELU_ROWS], d[GELU_ROWS];
+#pragma unroll
+    for (int j = 0; j < GELU_ROWS; ++j) {
+      const int64_t r = r0 + j < rows ? r0 + j : rows - 1;  // clamped: the tail rows are not stored
+      u[j] = *reinterpret_cast<const uint4*>(src + r * lds + c8 * 8);
+      d[j] = *reinterpret_cast<const uint4*>(out + r * ldo + c8 * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < GELU_ROWS; ++j) {
+      if (r0 + j >= rows) break;
+      const uint32_t uw[4] = {u[j].x, u[j].y, u[j].z, u[j].w}, dw[4] = {d[j].x, d[j].y, d[j].z, d[j].w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16 bl = (bf16)(bf_lo(dw[q]) * gelu_erf_grad(bf_lo(uw[q])));
+        const bf16 bh = (bf16)(bf_hi(dw[q]) * gelu_erf_grad(bf_hi(uw[q])));
+        cs[2 * q] += (float)bl;
+        cs[2 * q + 1] += (float)bh;
+        ow[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+      }
+      *reinterpret_cast<uint4*>(out + (r0 + j) * ldo + c8 * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
+  }
+  float* p = partial + (int64_t)blockIdx.x * N + c8 * 8;
+  *reinterpret_cast<float4*>(p) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+}
+
+__global__ __launch_bounds__(256) void gelu_cs_final_kernel(const float* __restrict__ partial, int nblk, int N,
+                                                            float* __restrict__ colsum) {
+  const double v = block_sum_strided(partial + blockIdx.x, nblk, N);
+  if (threadIdx.x == 0) colsum[blockIdx.x] = (float)v;
+}
+
+constexpr int GCS_BLOCKS = GELU_CS_BLOCKS;  // row walkers of gelu_dact_cs_kernel
+
 }  // namespace
 
 int g_policy = MIA_GEMM_POLICY_AUTO;
+
+void* scratch(size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Dev* d = nullptr;
+  if (bytes > WS_BYTES || device_state(&d)) return nullptr;
+  return d->ws;
+}
 
 int policy() { return g_policy; }
 
@@ -258,8 +312,17 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
     MIA_CHECK_ARG(cdiv(M, GELU_ROWS) < (1ll << 31), "gemm gelu pass: too many rows");
     const bf16* src = reinterpret_cast<const bf16*>(E.aux);
     bf16* out = reinterpret_cast<bf16*>(E.ptr);
-    if (E.act == MIA_ACT_GELU_SAVE) gelu_rows_kernel<false><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
-    else gelu_rows_kernel<true><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+    if (E.act == MIA_ACT_GELU_SAVE) {
+      gelu_rows_kernel<false><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+    } else if (E.colsum && (size_t)GCS_BLOCKS * N * 4 <= WS_BYTES) {
+      // the matmul above is done with the workspace (same stream): the column partials reuse it
+      float* part = reinterpret_cast<float*>(d->ws);
+      gelu_dact_cs_kernel<<<dim3(GCS_BLOCKS, grid.y), 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8), (int)N,
+                                                                   part);
+      gelu_cs_final_kernel<<<(unsigned)N, 256, 0, s>>>(part, GCS_BLOCKS, (int)N, E.colsum);
+    } else {
+      gelu_rows_kernel<true><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+    }
     MIA_LAUNCH_CHECK("gemm gelu pass");
   }
   return 0;

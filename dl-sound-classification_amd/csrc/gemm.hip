@@ -2092,6 +2092,26 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
                         int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
                         mia_stream_t stream) {
   MIA_CHECK_ARG(A && B && E, "gemm: null descriptor");
+  if (E->colsum) {
+    MIA_CHECK_ARG(!E->sqsum && !E->accumulate && !E->rm_inner && E->ldc >= N &&
+                      (E->dtype == MIA_BF16 || E->dtype == MIA_F32),
+                  "gemm: colsum needs a plain row-major output");
+    // the library path's dGELU pass delivers the sums itself when the measured choice is known to be
+    // the library before the call; otherwise (tile kernel, or the autotuning call) a column-sum pass
+    // over the stored output
+    const int pol = mblas::policy();
+    const bool lib = E->ptr && M > 0 && N > 0 && K > 0 && mblas::eligible(*A, *B, *E, M, N, K, compute_dtype) &&
+                     (split_k <= 1 || workspace) &&
+                     (pol == MIA_GEMM_POLICY_LIB ||
+                      (pol == MIA_GEMM_POLICY_AUTO && mblas::choice(*A, *B, *E, M, N, K) == 1));
+    if (int r = mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
+    if (!(lib && mblas::fuses_colsum(*E, N)) && M > 0 && N > 0) {
+      void* ws = mblas::scratch((size_t)MIA_COLSUM_MAXBLK * N * 4);
+      MIA_CHECK_ARG(ws, "gemm colsum: no scratch for N=%lld", (long long)N);
+      if (int r = mia_colsum(E->ptr, E->dtype, M, (int32_t)N, E->ldc, E->colsum, ws, stream)) return r;
+    }
+    return 0;
+  }
   if (!E->sqsum) return mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
   MIA_CHECK_ARG(E->dtype == MIA_F32 && E->act == MIA_ACT_NONE && !E->bias && !E->accumulate && !E->rm_inner &&
                     E->alpha == 1.f,

@@ -65,9 +65,11 @@ def conv(t: torch.Tensor, layout: int, n, h, w, c, oh, ow, kh, kw, sh=1, sw=1, p
 
 def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=None, ldaux: int = 0,
              accumulate: bool = False, alpha: float = 1.0, act_scale: float = 1.0,
-             rowmap=None, sqsum=None) -> L.MiaEpilogue:
+             rowmap=None, sqsum=None, colsum=None) -> L.MiaEpilogue:
     """Output descriptor of a GEMM.  ``sqsum``: optional f64 tensor of ``mia_gemm_sqsum_slots(M, N)``
-    entries that receives the per-tile sums of squares of a plain f32 output (see ``sqsum_slots``)."""
+    entries that receives the per-tile sums of squares of a plain f32 output (see ``sqsum_slots``).
+    ``colsum``: optional f32 (N,) tensor receiving the column sums of the stored output (the bias
+    gradient of the linear whose dy this output is)."""
     e = L.MiaEpilogue()
     e.ptr = out.data_ptr()
     e.dtype = L.dtype_code(out)
@@ -84,7 +86,8 @@ def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=
     e.alpha = alpha
     e.act_scale = act_scale
     e.sqsum = L.ptr(sqsum)
-    e._keep = (out, bias, aux, sqsum)
+    e.colsum = L.ptr(colsum)
+    e._keep = (out, bias, aux, sqsum, colsum)
     return e
 
 

@@ -41,7 +41,7 @@ class MiaEpilogue(C.Structure):
     _fields_ = [("ptr", vp), ("dtype", i32), ("act", i32), ("accumulate", i32), ("aux_dtype", i32),
                 ("ldc", i64), ("rm_inner", i64), ("rm_outer", i64), ("rm_istride", i64),
                 ("rm_offset", i64), ("bias", vp), ("aux", vp), ("ldaux", i64),
-                ("alpha", f32), ("act_scale", f32), ("sqsum", vp)]
+                ("alpha", f32), ("act_scale", f32), ("sqsum", vp), ("colsum", vp)]
 
 
 class MiaMelCfg(C.Structure):

@@ -62,9 +62,11 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
            K.epilogue(out, Nf, act=act, bias=bias, aux=aux, ldaux=Nf), M, Nf, Kf, cd, tag=tag)
 
 
-def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None):
+def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None,
+                dx_colsum=None):
     """dW = dy^T x (f32), db = colsum(dy) (unless the producer of dy already summed it), dx = dy @ W
-    (optionally with an activation backward)."""
+    (optionally with an activation backward; dx_colsum receives dx's column sums, the next linear's
+    bias gradient)."""
     Nf, Kf = W.shape
     if cd == L.BF16 and dy.dtype == torch.float32:
         dy = K.cast(dy, torch.bfloat16)  # bf16 GEMM operands (f32 accumulation inside)
@@ -75,7 +77,8 @@ def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.
         db = K.colsum(dy, M, Nf)
     if dx_out is not None:
         K.gemm(K.dense(dy, L.KC, M, Nf), K.dense(W, L.RC, Nf, Kf),
-               K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf),
+               K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf,
+                          colsum=dx_colsum),
                M, Kf, Nf, cd, tag=tag + ".dgrad")
     return dW, db
 
@@ -187,10 +190,11 @@ class ASTFunction(torch.autograd.Function):
             wqkv, wproj, w1, w2 = s["wcast"][i]
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
+            db1_ = torch.empty(w1.shape[0], dtype=torch.float32, device=dev)  # fc1 bias grad = colsum(du)
             dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
-                                    tag="fc2", db=db_next)
+                                    tag="fc2", db=db_next, dx_colsum=db1_)
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1")
+            dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1", db=db1_)
             dg2, dbt2, db_proj = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2)  # d(xm)
             if dxb2 is not None:
                 dxb, dxb2 = dxb2, dxb

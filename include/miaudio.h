@@ -77,6 +77,12 @@ typedef struct MiaEpilogue {
    * sum of squares of the values the GEMM stored there (double), for a gradient-clip norm that does
    * not re-read the output.  Plain f32 output only (no act / bias / accumulate / row map, alpha 1). */
   double* sqsum;
+  /* Optional (NULL = off): colsum[n] = sum over the M rows of the stored output column n (f32 result,
+   * summed from the stored -- for bf16, rounded -- values): the bias gradient of the linear whose dy
+   * this output is.  The library path's dGELU pass sums it on the way (timm fc1 behind the fc2
+   * dgrad); any other path gets a column-sum pass over the output.  Row-major output, no accumulate
+   * / row map / sqsum. */
+  float* colsum;
 } MiaEpilogue;
 
 /* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16; f32: v_mfma_f32_32x32x2_f32).

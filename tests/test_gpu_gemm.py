@@ -503,6 +503,29 @@ def test_plain_gemm_epilogues_both_paths(cuda, policy, pol, case):
     assert rel(out.float(), ref) < tol
 
 
+@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB, L.GEMM_POLICY_AUTO])
+@pytest.mark.parametrize("case", ["dact_gelu", "plain"])
+def test_gemm_output_colsum(cuda, policy, pol, case):
+    """MiaEpilogue.colsum: the column sums of the stored output (the next linear's bias gradient) --
+    fused into the library path's dGELU pass (AST fc1 bias behind the fc2 dgrad), a column-sum pass
+    otherwise -- equal to float64 sums of what was stored, on every path (the auto policy's first
+    call runs both paths)."""
+    policy(pol)
+    M, N, Kd = 8192 + 37, 3072, 768
+    a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 13)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    for it in range(2 if pol == L.GEMM_POLICY_AUTO else 1):  # auto: the measuring call, then the chosen path
+        cs = torch.full((N,), float("nan"), device=cuda)
+        if case == "dact_gelu":
+            u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
+            K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs), M, N, Kd, L.BF16)
+        else:
+            K.gemm(A, Bo, K.epilogue(out, N, colsum=cs), M, N, Kd, L.BF16)
+        torch.cuda.synchronize()
+        ref = out.double().sum(0)
+        assert rel(cs, ref) < 1e-5, it
+
+
 def test_wgrad8_many_items(cuda):
     """Rolling-window 8x8 wgrad (trunk conv4) with more (clip, chunk) items than blocks, ragged
     column chunks: vs a PyTorch fp32 autograd weight gradient of the same bf16 operands."""
