@@ -82,6 +82,64 @@ def test_esc50_datamodule_files(tmp_path):
     assert yv.shape == (4, 4) and torch.equal(yv.argmax(1), y)
 
 
+def test_envnet_pad_crop_matches_reference_restatement(tmp_path):
+    """EnvNet-v2 batch source without BC mixing (reference preprocessing.py:814-884, esc50.py:228-236):
+    T/2 zero padding each side, the training crop randint(0, total - window) drawn from python's
+    `random` in the same order, the centre crop for eval and the multi-crop starts, against the
+    oracle restatement on clips shorter than, equal to and longer than the window."""
+    import random
+
+    from oracle import data as odata
+    from src.datasets.esc50 import ESC50Dataset
+    d = tmp_path / "fold_0"
+    d.mkdir()
+    lens = [1000, 4410, 9000, 13230]  # window_length 0.1 s -> 4410-sample window, 2205 padding
+    g = torch.Generator().manual_seed(0)
+    for i, n in enumerate(lens):
+        torch.save({"waveform": torch.randn(1, n, generator=g), "label": i}, d / f"{i}.pt")
+    kw = dict(pad_crop=True, window_length=0.1)
+    train = ESC50Dataset(tmp_path, folds=[0], training=True, **kw)
+    evals = ESC50Dataset(tmp_path, folds=[0], training=False, **kw)
+    multi = ESC50Dataset(tmp_path, folds=[0], training=False, multi_crop_test=True, test_crops=5, **kw)
+    for i in range(len(lens)):
+        w = train.load(i)[0]
+        padded = odata.envnet_preprocess(w, window_length=0.1)
+        for seed in (1, 2, 3):
+            random.seed(seed)
+            got = train[i][0]
+            random.seed(seed)
+            assert torch.equal(got, odata.envnet_random_crop(padded, True, window_length=0.1))
+        assert torch.equal(evals[i][0], odata.envnet_random_crop(padded, False, window_length=0.1))
+        ref = odata.envnet_multi_crop(padded, 5, window_length=0.1)
+        got = multi[i][0]
+        assert len(got) == len(ref) and all(torch.equal(a, b) for a, b in zip(got, ref))
+        assert all(c.shape[-1] == 4410 for c in ref)
+
+
+def test_esc50_split_matches_reference_restatement(tmp_path):
+    """ESC50DataModule.setup's train/val split = the reference's (esc50.py:508-546): sorted fold files of
+    the four training folds, StratifiedShuffleSplit(test_size=ceil(len * val_split), random_state=42)."""
+    from oracle import data as odata
+    files, labels = [], []
+    for f in range(5):
+        d = tmp_path / f"fold_{f}"
+        d.mkdir()
+        for i in range(24):
+            lab = (3 * f + i) % 8
+            torch.save({"waveform": torch.zeros(1, 100), "label": lab}, d / f"{i:03d}.pt")
+    for f in (0, 1, 3, 4):
+        for pth in sorted((tmp_path / f"fold_{f}").glob("*.pt")):
+            files.append(pth)
+            labels.append(int(torch.load(pth, weights_only=True)["label"]))
+    dm = ESC50DataModule(root=str(tmp_path), fold=2, batch_size=4, num_workers=0, num_classes=8, val_split=0.1,
+                         preprocessing_config={"window_length": 0.1})
+    dm.setup("fit")
+    tr_ref, va_ref = odata.stratified_split(files, labels, 0.1)
+    assert [str(p) for p in dm._val_set.files] == [str(p) for p in va_ref]
+    assert [str(p) for p in dm._train_set.files] == [str(p) for p in tr_ref]
+    assert len(va_ref) == 10 and not set(map(str, va_ref)) & set(map(str, tr_ref))
+
+
 def test_urbansound8k_datamodule_files(tmp_path):
     """UrbanSound8K: ten folds, 10 classes, clips shorter than the 5 s EnvNet window are zero-padded
     into it (pad T/2 each side, crop); fold 10 is out of range; config composes to the class."""
