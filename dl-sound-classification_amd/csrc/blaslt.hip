@@ -45,11 +45,18 @@ struct KeyHash {
   }
 };
 
+constexpr int MAX_ALGO = 8;  // heuristic candidates timed on the first call of a shape
+
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
   hipblasLtMatmulAlgo_t algo;
   size_t ws = 0;
+  // the heuristic's candidates; `tuned` once the first call has timed them and kept the fastest
+  hipblasLtMatmulAlgo_t cand[MAX_ALGO];
+  size_t cand_ws[MAX_ALGO];
+  int ncand = 0;
+  bool tuned = false;
 };
 
 struct Dev {
@@ -123,16 +130,26 @@ int make_plan(Dev& d, const Key& k, Plan& p) {
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   const uint64_t wsb = WS_BYTES;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
-  hipblasLtMatmulHeuristicResult_t res[1];
+  hipblasLtMatmulHeuristicResult_t res[MAX_ALGO];
   int got = 0;
-  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d.handle, p.desc, p.la, p.lb, p.lc, p.ld, pref, 1, res,
-                                                              &got);
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d.handle, p.desc, p.la, p.lb, p.lc, p.ld, pref, MAX_ALGO,
+                                                              res, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || got < 1)
     return mia::fail(-5, "hipBLASLt: no algorithm for M=%lld N=%lld K=%lld (status %d)", (long long)k.m,
                      (long long)k.n, (long long)k.k, (int)st);
   p.algo = res[0].algo;
   p.ws = res[0].workspaceSize;
+  p.ncand = 0;
+  for (int i = 0; i < got && i < MAX_ALGO; ++i) {
+    if (res[i].workspaceSize > WS_BYTES) continue;
+    p.cand[p.ncand] = res[i].algo;
+    p.cand_ws[p.ncand++] = res[i].workspaceSize;
+  }
+  // only the weight-gradient shapes (both operands RC: K = tokens) are tuned -- measured: fc1 / fc2
+  // wgrad 2.36 / 2.43 -> 2.20 / 2.25 ms per AST block; for the forward and dgrad shapes the
+  // isolated timing picked algorithms that ran slower inside the step (qkv fwd 1.34 -> 1.56 ms)
+  p.tuned = p.ncand <= 1 || !(k.la == MIA_LAYOUT_RC && k.lb == MIA_LAYOUT_RC);
   return 0;
 }
 
@@ -305,6 +322,36 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
   const float alpha = 1.f, beta = E.act == MIA_ACT_ADD_AUX ? 1.f : 0.f;
   void* dptr = E.act == MIA_ACT_GELU_SAVE ? const_cast<void*>(E.aux) : E.ptr;
   const void* cptr = E.act == MIA_ACT_ADD_AUX ? E.aux : dptr;
+  if (!p.tuned) {
+    // first call of this shape: time the heuristic's candidates on the caller's buffers (every
+    // matmul here rewrites D from A, B and C != D, so repeating it is harmless) and keep the fastest;
+    // the heuristic's first choice is not always it (tools/probe/mxfp8_time.cpp: algo 4 of 8 on qkv)
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+      float best = 3.4e38f;
+      int bi = 0;
+      for (int i = 0; i < p.ncand; ++i) {
+        float tot = 0.f;
+        bool ok = true;
+        for (int rep = 0; rep < 3 && ok; ++rep) {
+          (void)hipEventRecord(e0, s);
+          ok = hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
+                               &p.cand[i], d->ws, p.cand_ws[i], s) == HIPBLAS_STATUS_SUCCESS;
+          (void)hipEventRecord(e1, s);
+          (void)hipEventSynchronize(e1);
+          float ms = 0.f;
+          (void)hipEventElapsedTime(&ms, e0, e1);
+          if (rep > 0) tot += ms;
+        }
+        if (ok && tot < best) { best = tot; bi = i; }
+      }
+      p.algo = p.cand[bi];
+      p.ws = p.cand_ws[bi];
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
+    p.tuned = true;
+  }
   LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
                            &p.algo, d->ws, p.ws, s));
   if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
