@@ -1,0 +1,11 @@
+#!/bin/bash
+# conv1 / conv3 forward with three items' loads in flight: their parity tests, EnvNet model tests, bench
+OUT=gpurun_out/r2s3; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_norm.py tests/test_gpu_envnet.py tests/test_gpu_e2e_bf16.py -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?
+tail -2 $OUT/tests.log
+[ $rc -ne 0 ] && { grep -E "FAILED|Error|^E " $OUT/tests.log | head -20; exit $rc; }
+timeout -k 10 600 python -u bench.py --model envnet --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+python - <<'PY'
+import json; d=json.load(open('gpurun_out/r2s3/bench.json'))
+print(d['value'], d['ms_per_step'], d['frontend_path']); print({k:v['ms'] for k,v in d['kernels'].items()})
+PY
