@@ -46,6 +46,7 @@ def build_ast_step(args, dev, rank, world, B):
         return loss
 
     tags = ["attn.fwd", "attn.bwd", "qkv.fwd", "proj.fwd", "fc1.fwd", "fc2.fwd", "qkv.wgrad", "qkv.dgrad",
+            "proj.wgrad", "proj.dgrad",
             "fc1.wgrad", "fc1.dgrad", "fc2.wgrad", "fc2.dgrad", "logmel.fwd", "optim.step"]
     workload = ("AST train step (log-mel, SpecAugment+Mixup, fwd, soft-CE, bwd, clip, Adam), "
                 "5 s @ 44.1 kHz -> 128x1379 log-mel -> 1645 tokens, DeiT-base/384 geometry")

@@ -16,6 +16,8 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 #include <mutex>
 #include <unordered_map>
 
@@ -46,15 +48,30 @@ struct KeyHash {
 };
 
 constexpr int MAX_ALGO = 8;  // heuristic candidates timed on the first call of a shape
+// Split-K variants of the weight-gradient shapes (both operands RC, K = tokens, few output tiles):
+// the matmul runs as a strided batch over S contiguous K-slices into f32 partials [S][M][N], then
+// splitk_sum_kernel adds the S partials in slice order (deterministic) into the output.
+constexpr int NSPLIT = 3;
+constexpr int SPLITS[NSPLIT] = {4, 8, 16};
+constexpr int SPLIT_ALGO = 4;  // heuristic candidates per split variant
+constexpr int MAX_CAND = MAX_ALGO + NSPLIT * SPLIT_ALGO;
+
+struct Layouts {
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
+  int split = 1;  // 1 = the plain matmul into the output
+};
 
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
-  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
+  Layouts v[1 + NSPLIT];  // v[0] plain, v[1..] split-K
+  int nvar = 1;
   hipblasLtMatmulAlgo_t algo;
   size_t ws = 0;
-  // the heuristic's candidates; `tuned` once the first call has timed them and kept the fastest
-  hipblasLtMatmulAlgo_t cand[MAX_ALGO];
-  size_t cand_ws[MAX_ALGO];
+  int var = 0;
+  // the heuristic's candidates (per variant); `tuned` once the first call has timed them and kept the fastest
+  hipblasLtMatmulAlgo_t cand[MAX_CAND];
+  size_t cand_ws[MAX_CAND];
+  int cand_var[MAX_CAND];
   int ncand = 0;
   bool tuned = false;
 };
@@ -62,6 +79,8 @@ struct Plan {
 struct Dev {
   hipblasLtHandle_t handle = nullptr;
   void* ws = nullptr;
+  float* part = nullptr;  // split-K partials (grown on plan creation, never during a run)
+  size_t part_bytes = 0;
   std::unordered_map<Key, Plan, KeyHash> plans;
   std::unordered_map<Key, int, KeyHash> choice;
 };
@@ -102,6 +121,56 @@ int device_state(Dev** out) {
   return 0;
 }
 
+bool split_shape(const Key& k) {
+  return k.la == MIA_LAYOUT_RC && k.lb == MIA_LAYOUT_RC && k.act == MIA_ACT_NONE && !k.bias && k.k >= 65536 &&
+         (k.n & 3) == 0 && (k.ldc & 3) == 0;
+}
+
+int heuristics(Dev& d, Plan& p, int var, int want) {
+  const Layouts& L = p.v[var];
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  const uint64_t wsb = WS_BYTES;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
+  hipblasLtMatmulHeuristicResult_t res[MAX_ALGO];
+  int got = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d.handle, p.desc, L.la, L.lb, L.lc, L.ld, pref, want, res,
+                                                              &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS) got = 0;
+  int added = 0;
+  for (int i = 0; i < got && i < want && p.ncand < MAX_CAND; ++i) {
+    if (res[i].workspaceSize > WS_BYTES) continue;
+    p.cand[p.ncand] = res[i].algo;
+    p.cand_ws[p.ncand] = res[i].workspaceSize;
+    p.cand_var[p.ncand++] = var;
+    ++added;
+  }
+  return added;
+}
+
+// batched layouts of split variant S: slice s of the operands starts K/S rows further, partial s at
+// s * M * N of the partial buffer (row-major [M][N], ld N)
+int add_split(Dev& d, const Key& k, Plan& p, int S) {
+  const int64_t ks = k.k / S;
+  Layouts& L = p.v[p.nvar];
+  L.split = S;
+  const int32_t bc = S;
+  const int64_t sa = ks * k.ldb, sb = ks * k.lda, sd = k.n * k.m;
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.la, HIP_R_16BF, k.n, ks, k.ldb));  // RC B operand, op N
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.lb, HIP_R_16BF, k.m, ks, k.lda));  // RC A operand, op T
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.ld, HIP_R_32F, k.n, k.m, k.n));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.lc, HIP_R_32F, k.n, k.m, k.n));
+  const std::pair<hipblasLtMatrixLayout_t, int64_t> all[4] = {{L.la, sa}, {L.lb, sb}, {L.ld, sd}, {L.lc, sd}};
+  for (const auto& [lay, stride] : all) {
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(lay, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(lay, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &stride,
+                                               sizeof(stride)));
+  }
+  if (heuristics(d, p, p.nvar, SPLIT_ALGO) > 0) ++p.nvar;
+  return 0;
+}
+
 int make_plan(Dev& d, const Key& k, Plan& p) {
   // D' = op(A') op(B'): m' = N, n' = M
   const hipblasOperation_t opa = k.lb == MIA_LAYOUT_KC ? HIPBLAS_OP_T : HIPBLAS_OP_N;
@@ -117,39 +186,43 @@ int make_plan(Dev& d, const Key& k, Plan& p) {
     const hipDataType bt = HIP_R_32F;
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
   }
-  if (opa == HIPBLAS_OP_T) LT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k.k, k.n, k.ldb));
-  else LT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k.n, k.k, k.ldb));
-  if (opb == HIPBLAS_OP_N) LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k.k, k.m, k.lda));
-  else LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k.m, k.k, k.lda));
+  Layouts& L = p.v[0];
+  if (opa == HIPBLAS_OP_T) LT_CHECK(hipblasLtMatrixLayoutCreate(&L.la, HIP_R_16BF, k.k, k.n, k.ldb));
+  else LT_CHECK(hipblasLtMatrixLayoutCreate(&L.la, HIP_R_16BF, k.n, k.k, k.ldb));
+  if (opb == HIPBLAS_OP_N) LT_CHECK(hipblasLtMatrixLayoutCreate(&L.lb, HIP_R_16BF, k.k, k.m, k.lda));
+  else LT_CHECK(hipblasLtMatrixLayoutCreate(&L.lb, HIP_R_16BF, k.m, k.k, k.lda));
   // GELU_SAVE: the GEMM writes the pre-activation into aux (ld = ldaux); C is unused (beta = 0)
   const int64_t ldd = k.act == MIA_ACT_GELU_SAVE ? k.ldaux : k.ldc;
   const int64_t ldcc = k.act == MIA_ACT_ADD_AUX ? k.ldaux : ldd;
-  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.ld, dt(k.odt), k.n, k.m, ldd));
-  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lc, dt(k.odt), k.n, k.m, ldcc));
-  hipblasLtMatmulPreference_t pref;
-  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
-  const uint64_t wsb = WS_BYTES;
-  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
-  hipblasLtMatmulHeuristicResult_t res[MAX_ALGO];
-  int got = 0;
-  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d.handle, p.desc, p.la, p.lb, p.lc, p.ld, pref, MAX_ALGO,
-                                                              res, &got);
-  hipblasLtMatmulPreferenceDestroy(pref);
-  if (st != HIPBLAS_STATUS_SUCCESS || got < 1)
-    return mia::fail(-5, "hipBLASLt: no algorithm for M=%lld N=%lld K=%lld (status %d)", (long long)k.m,
-                     (long long)k.n, (long long)k.k, (int)st);
-  p.algo = res[0].algo;
-  p.ws = res[0].workspaceSize;
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.ld, dt(k.odt), k.n, k.m, ldd));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&L.lc, dt(k.odt), k.n, k.m, ldcc));
   p.ncand = 0;
-  for (int i = 0; i < got && i < MAX_ALGO; ++i) {
-    if (res[i].workspaceSize > WS_BYTES) continue;
-    p.cand[p.ncand] = res[i].algo;
-    p.cand_ws[p.ncand++] = res[i].workspaceSize;
-  }
+  if (int r = heuristics(d, p, 0, MAX_ALGO); r < 1)
+    return mia::fail(-5, "hipBLASLt: no algorithm for M=%lld N=%lld K=%lld", (long long)k.m, (long long)k.n,
+                     (long long)k.k);
+  p.algo = p.cand[0];
+  p.ws = p.cand_ws[0];
+  p.var = 0;
   // only the weight-gradient shapes (both operands RC: K = tokens) are tuned -- measured: fc1 / fc2
   // wgrad 2.36 / 2.43 -> 2.20 / 2.25 ms per AST block; for the forward and dgrad shapes the
   // isolated timing picked algorithms that ran slower inside the step (qkv fwd 1.34 -> 1.56 ms)
-  p.tuned = p.ncand <= 1 || !(k.la == MIA_LAYOUT_RC && k.lb == MIA_LAYOUT_RC);
+  const bool rcrc = k.la == MIA_LAYOUT_RC && k.lb == MIA_LAYOUT_RC;
+  if (rcrc && split_shape(k)) {
+    const size_t need = (size_t)SPLITS[NSPLIT - 1] * k.m * k.n * 4;
+    if (need > d.part_bytes) {
+      // grown here (first call of a shape, outside any timed or captured region), never in a run
+      if (d.part) (void)hipFree(d.part);
+      d.part = nullptr;
+      d.part_bytes = 0;
+      if (hipMalloc(&d.part, need) == hipSuccess) d.part_bytes = need;
+      else (void)hipGetLastError();
+    }
+    if (d.part_bytes >= need)
+      for (int S : SPLITS)
+        if (k.k % S == 0)
+          if (int r = add_split(d, k, p, S)) return r;
+  }
+  p.tuned = p.ncand <= 1 || !rcrc;
   return 0;
 }
 
@@ -244,9 +317,47 @@ __global__ __launch_bounds__(256) void gelu_cs_final_kernel(const float* __restr
 
 constexpr int GCS_BLOCKS = GELU_CS_BLOCKS;  // row walkers of gelu_dact_cs_kernel
 
+// out[m][4q..4q+3] = sum over s = 0..S-1 (in order) of part[s][m][4q..]; all S loads issued first
+template <int S, typename T>
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ part, int64_t M, int N4,
+                                                         T* __restrict__ out, int64_t ldc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * N4) return;
+  const int64_t slice = M * N4;
+  typedef float fv4 __attribute__((ext_vector_type(4)));
+  const fv4* p = reinterpret_cast<const fv4*>(part) + i;
+  fv4 v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = __builtin_nontemporal_load(p + s * slice);
+  fv4 a = v[0];
+#pragma unroll
+  for (int s = 1; s < S; ++s) a += v[s];
+  const int64_t m = i / N4, q = i - m * N4;
+  T* o = out + m * ldc + 4 * q;
+  if constexpr (std::is_same<T, float>::value) {
+    *reinterpret_cast<fv4*>(o) = a;
+  } else {
+    bf16x4 b;
+    b[0] = (bf16)a.x; b[1] = (bf16)a.y; b[2] = (bf16)a.z; b[3] = (bf16)a.w;
+    *reinterpret_cast<bf16x4*>(o) = b;
+  }
+}
+
+template <typename T>
+void splitk_sum(int S, const float* part, int64_t M, int64_t N, T* out, int64_t ldc, hipStream_t s) {
+  const int N4 = (int)(N / 4);
+  const unsigned g = (unsigned)cdiv(M * N4, 256);
+  switch (S) {
+    case 4: splitk_sum_kernel<4, T><<<g, 256, 0, s>>>(part, M, N4, out, ldc); break;
+    case 8: splitk_sum_kernel<8, T><<<g, 256, 0, s>>>(part, M, N4, out, ldc); break;
+    default: splitk_sum_kernel<16, T><<<g, 256, 0, s>>>(part, M, N4, out, ldc); break;
+  }
+}
+
 }  // namespace
 
 int g_policy = MIA_GEMM_POLICY_AUTO;
+int g_force_split = 0;  // mia_gemm_lib_split: 0 = the timed choice, else that variant's first candidate
 
 void* scratch(size_t bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -322,6 +433,31 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
   const float alpha = 1.f, beta = E.act == MIA_ACT_ADD_AUX ? 1.f : 0.f;
   void* dptr = E.act == MIA_ACT_GELU_SAVE ? const_cast<void*>(E.aux) : E.ptr;
   const void* cptr = E.act == MIA_ACT_ADD_AUX ? E.aux : dptr;
+  // candidate i of variant var: the plain matmul, or the batched split-K matmul + the ordered sum
+  auto launch = [&](const hipblasLtMatmulAlgo_t& algo, size_t ws, int var) -> bool {
+    const Layouts& L = p.v[var];
+    if (L.split == 1)
+      return hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, L.la, A.ptr, L.lb, &beta, cptr, L.lc, dptr, L.ld, &algo,
+                             d->ws, ws, s) == HIPBLAS_STATUS_SUCCESS;
+    const float zero = 0.f;
+    if (hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, L.la, A.ptr, L.lb, &zero, d->part, L.lc, d->part, L.ld,
+                        &algo, d->ws, ws, s) != HIPBLAS_STATUS_SUCCESS)
+      return false;
+    if (E.dtype == MIA_F32) splitk_sum(L.split, d->part, M, N, reinterpret_cast<float*>(E.ptr), E.ldc, s);
+    else splitk_sum(L.split, d->part, M, N, reinterpret_cast<bf16*>(E.ptr), E.ldc, s);
+    return hipGetLastError() == hipSuccess;
+  };
+  if (g_force_split > 0) {
+    for (int i = 0; i < p.ncand; ++i)
+      if (p.v[p.cand_var[i]].split == g_force_split) {
+        if (!launch(p.cand[i], p.cand_ws[i], p.cand_var[i]))
+          return mia::fail(-5, "hipBLASLt matmul failed (M=%lld N=%lld K=%lld, split %d)", (long long)M, (long long)N,
+                           (long long)K, g_force_split);
+        return 0;
+      }
+    return mia::fail(-22, "gemm library path: no split-%d variant for M=%lld N=%lld K=%lld", g_force_split,
+                     (long long)M, (long long)N, (long long)K);
+  }
   if (!p.tuned) {
     // first call of this shape: time the heuristic's candidates on the caller's buffers (every
     // matmul here rewrites D from A, B and C != D, so repeating it is harmless) and keep the fastest;
@@ -335,8 +471,7 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
         bool ok = true;
         for (int rep = 0; rep < 3 && ok; ++rep) {
           (void)hipEventRecord(e0, s);
-          ok = hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
-                               &p.cand[i], d->ws, p.cand_ws[i], s) == HIPBLAS_STATUS_SUCCESS;
+          ok = launch(p.cand[i], p.cand_ws[i], p.cand_var[i]);
           (void)hipEventRecord(e1, s);
           (void)hipEventSynchronize(e1);
           float ms = 0.f;
@@ -347,13 +482,15 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
       }
       p.algo = p.cand[bi];
       p.ws = p.cand_ws[bi];
+      p.var = p.cand_var[bi];
       (void)hipEventDestroy(e0);
       (void)hipEventDestroy(e1);
     }
     p.tuned = true;
   }
-  LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, B.ptr, p.la, A.ptr, p.lb, &beta, cptr, p.lc, dptr, p.ld,
-                           &p.algo, d->ws, p.ws, s));
+  if (!launch(p.algo, p.ws, p.var))
+    return mia::fail(-5, "hipBLASLt matmul failed (M=%lld N=%lld K=%lld, split %d)", (long long)M, (long long)N,
+                     (long long)K, p.v[p.var].split);
   if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
     const dim3 grid((unsigned)cdiv(M, GELU_ROWS), (unsigned)cdiv(N / 8, 256));  // rows on x (< 2^31)
     MIA_CHECK_ARG(cdiv(M, GELU_ROWS) < (1ll << 31), "gemm gelu pass: too many rows");
@@ -382,5 +519,13 @@ extern "C" int mia_gemm_set_policy(int32_t policy) {
   std::lock_guard<std::mutex> lk(mblas::g_mu);
   mblas::g_policy = policy;
   for (auto& d : mblas::g_dev) d.choice.clear();
+  return 0;
+}
+
+extern "C" int mia_gemm_lib_split(int32_t split) {
+  MIA_CHECK_ARG(split == 0 || split == 1 || split == 4 || split == 8 || split == 16, "gemm library split %d",
+                (int)split);
+  std::lock_guard<std::mutex> lk(mblas::g_mu);
+  mblas::g_force_split = split;
   return 0;
 }

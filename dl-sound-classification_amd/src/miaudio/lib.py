@@ -58,6 +58,7 @@ SIGNATURES = {
     "mia_gemm": (C.c_int, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32, vp, vp]),
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
     "mia_gemm_set_policy": (C.c_int, [i32]),
+    "mia_gemm_lib_split": (C.c_int, [i32]),
     "mia_splitk_reduce": (C.c_int, [vp, i32, i64, i64, P(MiaEpilogue), vp]),
     "mia_logmel_workspace_bytes": (i64, [i64, i64]),
     "mia_logmel_fwd": (C.c_int, [vp, i64, i64, i64, P(MiaMelCfg), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

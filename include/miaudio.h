@@ -114,6 +114,11 @@ int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N
  * always run on the tile kernels. */
 enum { MIA_GEMM_POLICY_TILE = 0, MIA_GEMM_POLICY_LIB = 1, MIA_GEMM_POLICY_AUTO = 2 };
 int mia_gemm_set_policy(int32_t policy);
+/* Library path, weight-gradient shapes (both operands RC, K >= 65536, no bias/activation): besides
+ * the plain matmul, split-K variants (a strided batch over S = 4, 8, 16 contiguous K-slices into f32
+ * partials, then a fixed-order sum of the S partials) are timed on the first call and the fastest is
+ * kept.  split = 0 (default) uses that choice; 1, 4, 8, 16 force the plain / split-S variant (tests). */
+int mia_gemm_lib_split(int32_t split);
 
 /* Fused log-mel: frame gather + 1024-pt real FFT (LDS) + |X|^2 + htk mel (sparse bands)
  * + 10log10 + per-clip top_db clamp + per-clip mean/unbiased-std normalisation.

@@ -526,6 +526,37 @@ def test_gemm_output_colsum(cuda, policy, pol, case):
         assert rel(cs, ref) < 1e-5, it
 
 
+@pytest.fixture
+def lib_split():
+    """Force one library weight-gradient variant for a test, restore the timed choice afterwards."""
+    yield lambda s: L.check(L.load().mia_gemm_lib_split(s), "mia_gemm_lib_split")
+    L.check(L.load().mia_gemm_lib_split(0), "mia_gemm_lib_split")
+
+
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("split", [1, 4, 8, 16, 0])
+def test_wgrad_lib_split_k(cuda, policy, lib_split, odt, split):
+    """Library weight-gradient shapes (RC x RC, K = tokens >= 65536): the plain matmul and the split-K
+    variants (strided batch over S K-slices into f32 partials + the fixed-order partial sum), forced one
+    by one, and the timed choice (0) -- vs a PyTorch fp32 matmul of the same bf16 operands, into a
+    strided output (ldc > N), bit-identical from call to call."""
+    policy(L.GEMM_POLICY_LIB)
+    lib_split(split)
+    M, N, Kd = 768, 1152, 69632
+    a, b, A, Bo, g = _big_operands(cuda, L.RC, L.RC, M, N, Kd, 17)
+    ref = a.float() @ b.float().t()
+    full = torch.full((M, N + 64), float("nan"), dtype=odt, device=cuda)
+    out = full[:, :N]
+    outs = []
+    for _ in range(2):
+        K.gemm(A, Bo, K.epilogue(out, N + 64), M, N, Kd, L.BF16)
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+    assert torch.isnan(full[:, N:].float()).all()  # nothing written past N
+    assert torch.equal(outs[0], outs[1])
+    assert rel(out.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
+
+
 def test_wgrad8_many_items(cuda):
     """Rolling-window 8x8 wgrad (trunk conv4) with more (clip, chunk) items than blocks, ragged
     column chunks: vs a PyTorch fp32 autograd weight gradient of the same bf16 operands."""
