@@ -28,7 +28,8 @@ def _attn_ref(qkv, B, N, H):
 
 
 @pytest.mark.parametrize("dt", [L.BF16, L.F32])
-@pytest.mark.parametrize("B,N,H", [(2, 100, 2), (1, 257, 3), (2, 1645, 1), (3, 37, 2), (4, 300, 2), (8, 1645, 1)])
+@pytest.mark.parametrize("B,N,H", [(2, 100, 2), (1, 257, 3), (2, 1645, 1), (3, 37, 2), (4, 300, 2), (8, 1645, 1),
+                                   (1, 64, 2), (1, 128, 1), (1, 192, 1), (1, 520, 1)])
 def test_attention_fwd_bwd(cuda, dt, B, N, H):
     g = torch.Generator().manual_seed(N + H)
     tdt = torch.bfloat16 if dt == L.BF16 else torch.float32

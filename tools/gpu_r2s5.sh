@@ -1,0 +1,12 @@
+#!/bin/bash
+# ping-pong attention forward: attention parity tests, AST model tests, AST bench leg
+OUT=gpurun_out/r2s5; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ast.py -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?
+tail -2 $OUT/tests.log
+[ $rc -ne 0 ] && { grep -E "FAILED|Error|^E " $OUT/tests.log | head -30; exit $rc; }
+timeout -k 10 600 python -u bench.py --model ast --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+python - <<'PY'
+import json; d=json.load(open('gpurun_out/r2s5/bench.json'))
+d=d.get('ast', d)
+print(d['value'], d['ms_per_step']); print({k:v['ms'] for k,v in d['kernels'].items()})
+PY
