@@ -238,7 +238,7 @@ template <bool DACT>
 __global__ __launch_bounds__(256) void gelu_rows_kernel(const bf16* __restrict__ src, int64_t lds,
                                                         bf16* __restrict__ out, int64_t ldo, int64_t rows,
                                                         int cols8) {
-  const int c8 = blockIdx.y * 256 + threadIdx.x;
+  const int c8 = blockIdx.y * blockDim.x + threadIdx.x;
   if (c8 >= cols8) return;
   const int64_t r0 = (int64_t)blockIdx.x * GELU_ROWS;
   uint4 u[GELU_ROWS], d[GELU_ROWS];
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void gelu_rows_kernel(const bf16* __restrict__
 __global__ __launch_bounds__(256) void gelu_dact_cs_kernel(const bf16* __restrict__ src, int64_t lds,
                                                            bf16* __restrict__ out, int64_t ldo, int64_t rows,
                                                            int cols8, int N, float* __restrict__ partial) {
-  const int c8 = blockIdx.y * 256 + threadIdx.x;
+  const int c8 = blockIdx.y * blockDim.x + threadIdx.x;
   if (c8 >= cols8) return;  // no barriers below
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int64_t r0 = (int64_t)blockIdx.x * GELU_ROWS; r0 < rows; r0 += (int64_t)gridDim.x * GELU_ROWS) {
@@ -307,6 +307,15 @@ __global__ __launch_bounds__(256) void gelu_dact_cs_kernel(const bf16* __restric
   float* p = partial + (int64_t)blockIdx.x * N + c8 * 8;
   *reinterpret_cast<float4*>(p) = make_float4(cs[0], cs[1], cs[2], cs[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+}
+
+// threads per block of the two passes: a multiple of 64 that divides the row's 8-column groups when one
+// exists (N = 3072: 384 groups = 2 x 192, no half-empty second slab), else 256
+int gelu_tpb(int cols8) {
+  if (cols8 <= 256) return (cols8 + 63) / 64 * 64;
+  for (int c : {256, 192, 128})
+    if (cols8 % c == 0) return c;
+  return 256;
 }
 
 __global__ __launch_bounds__(256) void gelu_cs_final_kernel(const float* __restrict__ partial, int nblk, int N,
@@ -492,20 +501,21 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
     return mia::fail(-5, "hipBLASLt matmul failed (M=%lld N=%lld K=%lld, split %d)", (long long)M, (long long)N,
                      (long long)K, p.v[p.var].split);
   if (E.act == MIA_ACT_GELU_SAVE || E.act == MIA_DACT_GELU) {
-    const dim3 grid((unsigned)cdiv(M, GELU_ROWS), (unsigned)cdiv(N / 8, 256));  // rows on x (< 2^31)
+    const int tpb = gelu_tpb((int)(N / 8));
+    const dim3 grid((unsigned)cdiv(M, GELU_ROWS), (unsigned)cdiv(N / 8, tpb));  // rows on x (< 2^31)
     MIA_CHECK_ARG(cdiv(M, GELU_ROWS) < (1ll << 31), "gemm gelu pass: too many rows");
     const bf16* src = reinterpret_cast<const bf16*>(E.aux);
     bf16* out = reinterpret_cast<bf16*>(E.ptr);
     if (E.act == MIA_ACT_GELU_SAVE) {
-      gelu_rows_kernel<false><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+      gelu_rows_kernel<false><<<grid, tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
     } else if (E.colsum && (size_t)GCS_BLOCKS * N * 4 <= WS_BYTES) {
       // the matmul above is done with the workspace (same stream): the column partials reuse it
       float* part = reinterpret_cast<float*>(d->ws);
-      gelu_dact_cs_kernel<<<dim3(GCS_BLOCKS, grid.y), 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8), (int)N,
+      gelu_dact_cs_kernel<<<dim3(GCS_BLOCKS, grid.y), tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8), (int)N,
                                                                    part);
       gelu_cs_final_kernel<<<(unsigned)N, 256, 0, s>>>(part, GCS_BLOCKS, (int)N, E.colsum);
     } else {
-      gelu_rows_kernel<true><<<grid, 256, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
+      gelu_rows_kernel<true><<<grid, tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
     }
     MIA_LAUNCH_CHECK("gemm gelu pass");
   }
