@@ -61,16 +61,23 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default=None, help="comma list of probe tags to time live (default: auto)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL, the product path); gloo only to rehearse N > 1 ranks on one GPU")
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":  # rehearsal: ranks may share a device (RCCL refuses duplicate GPUs)
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -270,7 +277,8 @@ def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_c
         "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (peak-normalised 0.1*N(0,1) clips, uniform labels)",
         "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B, "clip_samples": 220_500,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + ("" if world == 1 or args.dist_backend == "nccl"
+                                                  else f" ({args.dist_backend} rehearsal, not RCCL)")},
         "roofline": roofline(model, roof_tag or dom, ks[roof_tag or dom], peak_tf) if (roof_tag or dom) in ks else None,
         "dominant_kernel": roofline(model, dom, ks[dom], peak_tf) if dom and roof_tag else None,
         "step_tflops": round(flop_per_clip * B / (ms * 1e-3) / 1e12, 2),
@@ -389,7 +397,7 @@ def free_leg():
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    world, rank, local = setup_dist(args.dist_backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     results = {}

@@ -1,0 +1,85 @@
+"""GPU: the data-parallel gradient exchange of the benched path with the real HIP backward.
+
+Two ranks share the one GPU (gloo carries the GPU tensors: RCCL refuses two ranks on one device, and
+the 8-GPU RCCL run is the driver's).  Each rank runs EnvNetV2(compute_dtype="bf16") on its own clips:
+a warm-up step (the auto GEMM policy measures its first calls), a plain step whose gradients are the
+reference, then the same step under GradAllReducer (src/training/ddp.py), whose buckets leave from
+inside EnvNetFunction.backward through ``_grad_ready`` on the side stream (the FC gradients) and from
+``finish()`` (the rest).  The kernels are deterministic, so every averaged gradient must equal
+(g_0 + g_1) * 0.5 of the two ranks' plain gradients bit for bit (Lightning DDP's mean over ranks,
+reference base_training.yaml:45-51)."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.test_training_cpu import _free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle.synth import synth_waveform
+        from src.miaudio import kernels as K
+        from src.training.ddp import GradAllReducer
+        from tests._util import envnet_with_hash_params
+        dev = torch.device("cuda", 0)
+        m = envnet_with_hash_params(dev, compute_dtype="bf16").train()
+        B = 2
+        x = torch.from_numpy(synth_waveform(31 + rank, B, 220_500)[:, None, :]).to(dev)
+        y = torch.zeros(B, 50, device=dev)
+        y[0, 3 + rank] = 1.0
+        y[1, 20], y[1, 40 - rank] = 0.3, 0.7
+
+        def step():
+            m.zero_grad(set_to_none=True)
+            z = m(x)
+            _, dz, _ = K.soft_ce(z.detach().float().contiguous(), y, input_sigmoid=False)
+            z.backward(dz)
+
+        step()
+        step()
+        plain = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        red = GradAllReducer(m, world)
+        step()
+        red.finish()
+        torch.cuda.synchronize()
+        mism = []
+        for n, p in m.named_parameters():
+            parts = [torch.empty_like(plain[n], device="cpu") for _ in range(world)]
+            dist.all_gather(parts, plain[n].cpu())
+            ref = (parts[0] + parts[1]) * (1.0 / world)
+            if not torch.equal(p.grad.cpu(), ref):
+                mism.append((n, float((p.grad.cpu() - ref).abs().max())))
+        q.put((rank, red.last_fired, len(plain), mism, None))
+        dist.destroy_process_group()
+    except Exception as e:  # surface the worker's failure in the parent's assertion
+        q.put((rank, 0, 0, [], repr(e)))
+
+
+@pytest.mark.timeout(600)
+def test_grad_allreducer_envnet_hip_backward_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, fired, nparam, mism, err = q.get(timeout=500)
+        res[r] = (fired, nparam, mism, err)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, (fired, nparam, mism, err) in res.items():
+        assert err is None, (r, err)
+        assert fired > 0, "no gradient left through _grad_ready inside the HIP backward"
+        assert nparam > 20
+        assert not mism, (r, mism[:5])
