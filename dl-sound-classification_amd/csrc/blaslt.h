@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/miaudio.h"
+#include "common.h"
 
 namespace mblas {
 
@@ -22,10 +23,13 @@ int choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
 void set_choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
                 int v);
 // whether run() delivers E.colsum itself (the dGELU pass sums its output's columns, GELU_CS_BLOCKS
-// row walkers with one f32 partial row each in the 64 MB library workspace)
+// row walkers with one f32 partial row each in the 64 MB library workspace, then the slice sums of
+// colsum_pass1 behind them)
 constexpr int GELU_CS_BLOCKS = 2048;
+inline int64_t gelu_cs_rows_bytes(int64_t N) { return ((int64_t)GELU_CS_BLOCKS * N * 4 + 255) / 256 * 256; }
 inline bool fuses_colsum(const MiaEpilogue& E, int64_t N) {
-  return E.colsum && E.act == MIA_DACT_GELU && (size_t)GELU_CS_BLOCKS * N * 4 <= (64ull << 20);
+  return E.colsum && E.act == MIA_DACT_GELU && N < (1 << 30) &&
+         gelu_cs_rows_bytes(N) + (int64_t)COLSUM_SLICES * N * 8 <= (int64_t)(64ull << 20);
 }
 // the device's library workspace (stream-ordered scratch) if `bytes` fit, else null
 void* scratch(size_t bytes);

@@ -318,10 +318,11 @@ int gelu_tpb(int cols8) {
   return 256;
 }
 
-__global__ __launch_bounds__(256) void gelu_cs_final_kernel(const float* __restrict__ partial, int nblk, int N,
+// (colsum_pass1 over the partial rows) slice sums -> colsum, one thread per column
+__global__ __launch_bounds__(256) void gelu_cs_final_kernel(const double* __restrict__ part2, int N,
                                                             float* __restrict__ colsum) {
-  const double v = block_sum_strided(partial + blockIdx.x, nblk, N);
-  if (threadIdx.x == 0) colsum[blockIdx.x] = (float)v;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) colsum[c] = (float)colsum_slices(part2, N, c);
 }
 
 constexpr int GCS_BLOCKS = GELU_CS_BLOCKS;  // row walkers of gelu_dact_cs_kernel
@@ -508,12 +509,14 @@ int run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t 
     bf16* out = reinterpret_cast<bf16*>(E.ptr);
     if (E.act == MIA_ACT_GELU_SAVE) {
       gelu_rows_kernel<false><<<grid, tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
-    } else if (E.colsum && (size_t)GCS_BLOCKS * N * 4 <= WS_BYTES) {
+    } else if (fuses_colsum(E, N)) {
       // the matmul above is done with the workspace (same stream): the column partials reuse it
       float* part = reinterpret_cast<float*>(d->ws);
+      double* part2 = reinterpret_cast<double*>(static_cast<char*>(d->ws) + gelu_cs_rows_bytes(N));
       gelu_dact_cs_kernel<<<dim3(GCS_BLOCKS, grid.y), tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8), (int)N,
                                                                    part);
-      gelu_cs_final_kernel<<<(unsigned)N, 256, 0, s>>>(part, GCS_BLOCKS, (int)N, E.colsum);
+      colsum_pass1(part, GCS_BLOCKS, (int)N, N, part2, s);
+      gelu_cs_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, s>>>(part2, (int)N, E.colsum);
     } else {
       gelu_rows_kernel<true><<<grid, tpb, 0, s>>>(src, E.ldaux, out, E.ldc, M, (int)(N / 8));
     }

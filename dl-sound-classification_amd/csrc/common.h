@@ -85,6 +85,40 @@ __device__ __forceinline__ double block_sum_strided(const float* __restrict__ p,
   return r;
 }
 
+// Coalesced deterministic column sums of a row-major f32 matrix p[rows][cols] (ld = row stride),
+// the per-block partial rows of the fixed-order reductions: pass 1, block (x, y) = 64 columns of
+// row slice y; its 4 waves sum rows g, g + 4, ... of the slice (lane = column, 256-B row segments,
+// in double) and are combined in a fixed order -> part2[y][cols]; colsum_slices() then adds the
+// slices in order.  Replaces one-column-per-block strided walks (one 4-B read per line).
+constexpr int COLSUM_SLICES = 16;
+inline int64_t colsum_part2_bytes(int cols) { return (int64_t)COLSUM_SLICES * cols * 8; }
+static __global__ __launch_bounds__(256) void colsum_pass1_kernel(const float* __restrict__ p, int64_t rows, int cols,
+                                                                  int64_t ld, double* __restrict__ part2) {
+  __shared__ double red_cp[4][64];
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = r0 + per < rows ? r0 + per : rows;
+  double s = 0.0;
+  if (c < cols) {
+#pragma unroll 8
+    for (int64_t r = r0 + g; r < r1; r += 4) s += (double)p[r * ld + c];
+  }
+  red_cp[g][l] = s;
+  __syncthreads();
+  if (g == 0 && c < cols)
+    part2[(int64_t)blockIdx.y * cols + c] = ((red_cp[0][l] + red_cp[1][l]) + red_cp[2][l]) + red_cp[3][l];
+}
+inline void colsum_pass1(const float* p, int64_t rows, int cols, int64_t ld, double* part2, hipStream_t s) {
+  colsum_pass1_kernel<<<dim3((unsigned)((cols + 63) / 64), COLSUM_SLICES), 256, 0, s>>>(p, rows, cols, ld, part2);
+}
+__device__ __forceinline__ double colsum_slices(const double* __restrict__ part2, int cols, int c) {
+  double v = 0.0;
+#pragma unroll
+  for (int y = 0; y < COLSUM_SLICES; ++y) v += part2[(int64_t)y * cols + c];
+  return v;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -432,17 +432,16 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
   }
 }
 
-// partial rows [blk][nq][D] -> dgamma, dbeta (and, nq == 3, the dx2 column sums), in double
-__global__ void ln_partial_final_kernel(const float* __restrict__ partial, int nblk, int D, int nq, float* dgamma,
+// partial rows [blk][nq][D] -> (colsum_pass1) slice sums [COLSUM_SLICES][nq * D] -> dgamma, dbeta
+// (and, nq == 3, the dx2 column sums), in double; one thread per (q, d)
+__global__ void ln_partial_final_kernel(const double* __restrict__ part2, int D, int nq, float* dgamma,
                                         float* dbeta, float* colsum) {
-  const int d = blockIdx.x;  // one block per feature
-  const double a = block_sum_strided(partial + d, nblk, nq * (int64_t)D);
-  const double b = block_sum_strided(partial + D + d, nblk, nq * (int64_t)D);
-  const double c = nq == 3 ? block_sum_strided(partial + 2 * D + d, nblk, nq * (int64_t)D) : 0.0;
-  if (threadIdx.x != 0) return;
-  if (dgamma) dgamma[d] = (float)a;
-  if (dbeta) dbeta[d] = (float)b;
-  if (colsum) colsum[d] = (float)c;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq * D) return;
+  const int q = i / D, d = i - q * D;
+  const float v = (float)colsum_slices(part2, nq * D, i);
+  float* dst = q == 0 ? dgamma : q == 1 ? dbeta : colsum;
+  if (dst) dst[d] = v;
 }
 
 constexpr int LN_ROWS_PER_BLOCK = 256;
@@ -576,9 +575,13 @@ extern "C" int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gam
   return 0;
 }
 
-extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
+// partial rows of the widest form, then (256-B aligned) the slice sums of colsum_pass1
+static int64_t ln_rows_bytes(int64_t rows, int32_t D) {
   const int64_t a = cdiv(rows, LN_VEC_ROWS) * 3 * D * 4, b = cdiv(rows, 256) * 2 * D * 4;
-  return a > b ? a : b;
+  return cdiv(a > b ? a : b, 256) * 256;
+}
+extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
+  return ln_rows_bytes(rows, D) + colsum_part2_bytes(3 * D);
 }
 
 static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
@@ -606,8 +609,10 @@ static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, in
                                           (float*)partial, rows, D, LN_ROWS_PER_BLOCK);
   }
   MIA_LAUNCH_CHECK("layernorm_bwd");
-  ln_partial_final_kernel<<<(unsigned)D, 256, 0, s>>>((const float*)partial, (int)nb, D, dx2_colsum ? 3 : 2, dgamma,
-                                                      dbeta, dx2_colsum);
+  const int nq = dx2_colsum ? 3 : 2;
+  double* part2 = reinterpret_cast<double*>(static_cast<char*>(partial) + ln_rows_bytes(rows, D));
+  colsum_pass1((const float*)partial, (int64_t)nb, nq * D, (int64_t)nq * D, part2, s);
+  ln_partial_final_kernel<<<(unsigned)cdiv(nq * D, 256), 256, 0, s>>>(part2, D, nq, dgamma, dbeta, dx2_colsum);
   MIA_LAUNCH_CHECK("layernorm_partial_final");
   return 0;
 }
