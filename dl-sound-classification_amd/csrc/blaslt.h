@@ -25,7 +25,7 @@ void set_choice(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, 
 // whether run() delivers E.colsum itself (the dGELU pass sums its output's columns, GELU_CS_BLOCKS
 // row walkers with one f32 partial row each in the 64 MB library workspace, then the slice sums of
 // colsum_pass1 behind them)
-constexpr int GELU_CS_BLOCKS = 2048;
+constexpr int GELU_CS_BLOCKS = 4096;
 inline int64_t gelu_cs_rows_bytes(int64_t N) { return ((int64_t)GELU_CS_BLOCKS * N * 4 + 255) / 256 * 256; }
 inline bool fuses_colsum(const MiaEpilogue& E, int64_t N) {
   return E.colsum && E.act == MIA_DACT_GELU && N < (1 << 30) &&
