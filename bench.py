@@ -11,8 +11,11 @@ Default invocation (what the driver runs) times BOTH configs on the same GPUs, o
     own value / ms_per_step / roofline (attention forward, the north-star MFMA kernel) / cpu_baseline.
 Synthetic 5 s @ 44.1 kHz clips resident in HBM.  `--model envnet|ast` times one leg only (profiling).
 
-python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch one process per GPU with
-torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env).  Rank 0 prints ONE line.
+python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one process per GPU: under a launcher
+(torch.distributed.run: RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env) WORLD_SIZE must equal N;
+without one, this process starts ``torch.distributed.run --nproc-per-node N`` itself (before it
+touches the GPU) and exits with its status.  Every rank checks dist.get_world_size() == N.  Rank 0
+prints ONE line; for N > 1 it carries each rank's exposed gradient-exchange time ("comm").
 """
 from __future__ import annotations
 
@@ -20,6 +23,8 @@ import argparse
 import gc
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -52,7 +57,8 @@ def log(msg):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", choices=["both", "envnet", "ast"], default="both")
@@ -64,6 +70,30 @@ def parse():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N > 1 ranks on one GPU")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, script: str, argv: list[str]) -> int:
+    """One process per GPU through torch.distributed.run on this node (rendezvous on 127.0.0.1); the
+    children inherit stdout, so rank 0's JSON line is this process's output.  Must run before anything
+    in this process touches the GPU (it never does: the children do the work)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script, *argv]
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd)
+
+
+def check_world(requested, world: int) -> None:
+    """--gpus N and the process group must agree: a mismatch would time the wrong number of ranks."""
+    if requested is not None and requested != world:
+        raise SystemExit(f"bench.py: --gpus {requested} but the process group has {world} ranks")
 
 
 def setup_dist(backend="nccl"):
@@ -112,6 +142,7 @@ def build_envnet_step(args, dev, rank, world, B):
         opt.zero_grad(set_to_none=True)
         return loss
 
+    step.ddp = ddp
     tags = ["t0b.fwd", "t0b.dgrad", "t0b.wgrad", "conv1.fwd", "conv1.wgrad", "conv2.fwd", "conv2.dgrad",
             "conv2.wgrad", "fc1.fwd", "fc1.wgrad", "fc1.dgrad", "optim.step", "frontend.fwd", "frontend.bwd"]
     workload = "EnvNet-v2 train step (BC-mix, fwd, soft-CE, bwd, clip, Adam), ESC-50 shape"
@@ -236,6 +267,9 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
     torch.cuda.synchronize()
     log("warm-up done, timing")
     K.PROBE = {t: [] for t in probe_tags}
+    ddp = getattr(step, "ddp", None)
+    if ddp is not None:
+        ddp.timing = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -247,10 +281,20 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     probes, K.PROBE = K.PROBE, None
+    comm = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+        if ddp is not None:
+            mine = torch.tensor([ddp.exposed_ms() or 0.0], device=dev)
+            every = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(every, mine)
+            nbytes = sum(p.numel() * p.element_size() for p in ddp.params)
+            comm = {"exposed_ms_per_step": [round(float(v), 3) for v in every],
+                    "allreduce_bytes_per_step": nbytes, "chunks_per_step": ddp.last_chunks,
+                    "backend": dist.get_backend()}
+            ddp.timing = None
     kstats = {}
     for tag, recs in probes.items():
         if not recs:
@@ -259,12 +303,15 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
         flops, byts = recs[0][2], recs[0][3]
         kstats[tag] = {"ms": dur, "tflops": flops / (dur * 1e-3) / 1e12, "gbs": byts / (dur * 1e-3) / 1e9,
                        "launches_per_step": len(recs) / steps, "flop": flops, "bytes": byts}
+    if comm is not None:
+        kstats["_comm"] = comm
     return elapsed, float(loss), kstats
 
 
 def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_clip, args, workload,
                roof_tag=None):
     ms = elapsed / steps * 1e3
+    comm = kstats.pop("_comm", None)
     regions = {k: v for k, v in kstats.items() if k.startswith("frontend.")}
     ks = {k: v for k, v in kstats.items() if k not in regions}
     peak_tf = BF16_MFMA_PEAK_TF if args.dtype == "bf16" else F32_PEAK_TF
@@ -286,6 +333,8 @@ def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_c
                     for k, v in ks.items()},
         "loss": loss,
     }
+    if comm is not None:
+        out["comm"] = comm
     if model == "envnet":
         out["frontend_path"] = frontend_summary(regions, B)
     if out["dominant_kernel"] is None:
@@ -397,7 +446,10 @@ def free_leg():
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, str(Path(__file__).resolve()), sys.argv[1:]))
     world, rank, local = setup_dist(args.dist_backend)
+    check_world(args.gpus, dist.get_world_size() if world > 1 else 1)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     results = {}

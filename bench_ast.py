@@ -45,6 +45,7 @@ def build_ast_step(args, dev, rank, world, B):
         opt.zero_grad(set_to_none=True)
         return loss
 
+    step.ddp = ddp
     tags = ["attn.fwd", "attn.bwd", "qkv.fwd", "proj.fwd", "fc1.fwd", "fc2.fwd", "qkv.wgrad", "qkv.dgrad",
             "proj.wgrad", "proj.dgrad",
             "fc1.wgrad", "fc1.dgrad", "fc2.wgrad", "fc2.dgrad", "logmel.fwd", "optim.step"]

@@ -190,8 +190,13 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
                                                   void* const* __restrict__ shadow,
                                                   const int64_t* __restrict__ sizes, const float* __restrict__ coef_p,
                                                   float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps,
-                                                  float wd) {
+                                                  float wd, const int32_t* __restrict__ steps, float lr) {
   const int tsr = blockIdx.y;
+  if (steps) {  // per-tensor step counts (a parameter that missed gradients keeps its own count, as torch's Adam)
+    const double st = (double)steps[tsr];
+    lr_over_bc1 = (float)(lr / (1.0 - pow((double)beta1, st)));
+    bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, st));
+  }
   float* p = reinterpret_cast<float*>(params[tsr]);
   const float* g = reinterpret_cast<const float*>(grads[tsr]);
   float* m = reinterpret_cast<float*>(m1[tsr]);
@@ -530,7 +535,7 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
                              void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
                              float beta2, float eps, float weight_decay, int32_t step, float clip,
                              float* total_norm_out, void* sqnorm_ws, const void* const* pre_sq,
-                             const int64_t* pre_n, mia_stream_t stream) {
+                             const int64_t* pre_n, const int32_t* steps, mia_stream_t stream) {
   MIA_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && sizes && sqnorm_ws, "clip_adam: null table");
   MIA_CHECK_ARG(ntensors > 0 && ntensors < 65536 && step >= 1, "clip_adam: ntensors/step");
   MIA_CHECK_ARG(!pre_sq || pre_n, "clip_adam: pre_sq needs pre_n");
@@ -547,7 +552,7 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   const int ablocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(max_numel, 256 * 32)));
   adam_kernel<<<dim3(ablocks, ntensors), NT, 0, s>>>(params, grads, exp_avg, exp_avg_sq, shadow_bf16, sizes, coef,
                                                      (float)(lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
-                                                     weight_decay);
+                                                     weight_decay, steps, lr);
   MIA_LAUNCH_CHECK("adam");
   return 0;
 }

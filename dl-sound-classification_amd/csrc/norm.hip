@@ -370,16 +370,17 @@ __device__ __forceinline__ void stv(void* p, int dt, int64_t off, const float* f
   }
 }
 
-template <int PER>
+template <int PER, bool CS>
 __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__ dy, int dydt, const void* __restrict__ x,
                                                         int xdt, const float* __restrict__ g,
                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
                                                         void* dx, int dxdt, int accumulate, void* dx2, int dx2dt,
-                                                        float* __restrict__ partial, int64_t rows, int cs) {
-  // cs: also the column sums of the stored dx2 values (the next linear's bias gradient); partial
-  // rows are then [blk][3][D] instead of [blk][2][D]
+                                                        float* __restrict__ partial, int64_t rows) {
+  // CS: also the column sums of the stored dx2 values (the next linear's bias gradient); partial
+  // rows are then [blk][3][D] instead of [blk][2][D] (and the LDS plane for them exists only then)
   constexpr int D = 64 * PER;
-  __shared__ float red[4][3][D];
+  constexpr int nq = CS ? 3 : 2;
+  __shared__ float red[4][nq][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d0 = lane * PER;
   float gg[PER];
@@ -417,14 +418,17 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
     }
     stv<PER>(dx, dxdt, row * D + d0, o);
     if (dx2) stv<PER>(dx2, dx2dt, row * D + d0, o);
-    if (cs) {
+    if constexpr (CS) {
 #pragma unroll
       for (int i = 0; i < PER; ++i) ac[i] += dx2dt == MIA_BF16 ? (float)(bf16)o[i] : o[i];
     }
   }
-  const int nq = cs ? 3 : 2;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) { red[wave][0][d0 + i] = ag[i]; red[wave][1][d0 + i] = ab[i]; red[wave][2][d0 + i] = ac[i]; }
+  for (int i = 0; i < PER; ++i) {
+    red[wave][0][d0 + i] = ag[i];
+    red[wave][1][d0 + i] = ab[i];
+    if constexpr (CS) red[wave][nq - 1][d0 + i] = ac[i];
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < nq * D; i += NT) {
     const int q = i / D, d = i % D;
@@ -596,8 +600,12 @@ static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, in
   const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0;
   if (D == 768 && al) {
     nb = (unsigned)cdiv(rows, LN_VEC_ROWS);
-    ln_bwd_vec_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
-                                            dx2, dx2dtype, (float*)partial, rows, dx2_colsum ? 1 : 0);
+    if (dx2_colsum)
+      ln_bwd_vec_kernel<12, true><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
+                                                    dx2, dx2dtype, (float*)partial, rows);
+    else
+      ln_bwd_vec_kernel<12, false><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype,
+                                                     accumulate, dx2, dx2dtype, (float*)partial, rows);
   } else {
     MIA_CHECK_ARG(dx2 == nullptr, "layernorm_bwd: the bf16 copy needs D == 768 and aligned rows");
     nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);

@@ -21,6 +21,7 @@ from ..miaudio import kernels as K
 from ..miaudio import lib as L
 
 _SEED = itertools.count(0x5EED)
+FC1_CHUNK_ROWS = 256  # rows of FC1's weight gradient per data-parallel all-reduce (256 x 84480 f32 = 86.5 MB)
 
 
 def _use_conv8(cd: int, cin: int, cout: int, kh: int, kw: int) -> bool:
@@ -289,6 +290,7 @@ class EnvNetFunction(torch.autograd.Function):
         glogits = glogits.contiguous().float()
         keep_scale = 1.0 / (1.0 - s["drop_p"]) if s["drop_p"] > 0 else 1.0
         ready = getattr(ctx.model, "_grad_ready", None)
+        chunk_ready = getattr(ctx.model, "_grad_chunk_ready", None)
 
         def emit(lo, hi):
             # hand finished gradients to the data-parallel reducer now (overlaps the rest of the
@@ -307,13 +309,23 @@ class EnvNetFunction(torch.autograd.Function):
             fout, fin = Wt.shape
             hin = acts[li]
             dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
-            # FC1/FC2: the GEMM epilogue also writes per-tile sums of squares of dW, so the clip-norm
-            # pass of FusedAdam does not re-read the 1.4 GB (K.sqsum_slots)
-            sq = K.sqsum_slots(dW, fout, fin) if li < 2 else None
-            K.gemm(K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), K.epilogue(dW, fin, sqsum=sq), fout,
-                   fin, B, cd, tag=f"fc{li + 1}.wgrad")
-            if sq is not None:
-                K.tag_sqsum(p[40 + 2 * li], dW, sq)
+            if li == 0 and chunk_ready is not None and fout % FC1_CHUNK_ROWS == 0 and fout > FC1_CHUNK_ROWS:
+                # data-parallel: FC1's 1.38 GB weight gradient as row chunks of 86.5 MB, each all-reduced
+                # as soon as its GEMM is enqueued (the reducer averages it in place; the per-tile sums of
+                # squares would describe the un-averaged gradient, so none are written)
+                for lo in range(0, fout, FC1_CHUNK_ROWS):
+                    part = dW[lo:lo + FC1_CHUNK_ROWS]
+                    K.gemm(K.dense(dcur[:, lo:], L.RC, B, FC1_CHUNK_ROWS, ld=fout), K.dense(hin, L.RC, B, fin),
+                           K.epilogue(part, fin), FC1_CHUNK_ROWS, fin, B, cd, tag="fc1.wgrad")
+                    chunk_ready(p[40], dW, part, lo + FC1_CHUNK_ROWS == fout)
+            else:
+                # FC1/FC2: the GEMM epilogue also writes per-tile sums of squares of dW, so the clip-norm
+                # pass of FusedAdam does not re-read the 1.4 GB (K.sqsum_slots)
+                sq = K.sqsum_slots(dW, fout, fin) if li < 2 else None
+                K.gemm(K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), K.epilogue(dW, fin, sqsum=sq), fout,
+                       fin, B, cd, tag=f"fc{li + 1}.wgrad")
+                if sq is not None:
+                    K.tag_sqsum(p[40 + 2 * li], dW, sq)
             grads[40 + 2 * li] = dW
             grads[41 + 2 * li] = K.colsum(dcur, B, fout)
             if li > 0:

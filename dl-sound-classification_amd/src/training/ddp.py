@@ -11,8 +11,20 @@ reports gradients as they become ready (the EnvNetV2 and AST autograd nodes do, 
 FC-head gradients (1.4 GB for EnvNet) overlaps the convolution backward; everything else is flushed
 in ``finish()``.  The hook is installed on the wrapped module AND every submodule, because the
 drop-in path wraps the LitClassifier while the autograd nodes look for it on the inner model.
+A gradient too large for one bucket can also be handed over in row chunks as its producer writes them
+(``module._grad_chunk_ready``): EnvNet's FC1 weight gradient (4096 x 84480 f32, 1.38 GB) is computed
+as 16 weight-gradient GEMMs of 256 rows (86.5 MB each) and every chunk's all-reduce is launched as
+soon as its GEMM is enqueued, so the transfer of the largest gradient starts after 1/16 of its
+GEMM instead of after all of it (64-128 MB chunks, FC head first).
+
 The per-step BatchNorm buffer broadcast (DDP ``broadcast_buffers``) is one coalesced collective per
-dtype.
+dtype, issued after the gradient exchange.  torch DDP broadcasts rank 0's buffers at the start of
+each forward; the values it sends there (rank 0's statistics after the previous step's forward) are
+the ones sent here at the end of that previous step, so every forward sees the same buffers.
+
+``timing`` (a list, or None): when set, ``finish()`` appends one (compute done, exchange done) HIP
+event pair per step; ``exposed_ms()`` turns them into the communication time the backward did not
+hide (bench.py reports it per rank).
 """
 from __future__ import annotations
 
@@ -43,7 +55,10 @@ class GradAllReducer:
                 dist.broadcast(b.data, 0)
         for m in model.modules():
             m._grad_ready = self.grad_ready
+            m._grad_chunk_ready = self.grad_chunk_ready
         self.fired = self.last_fired = 0  # gradients received through _grad_ready per step (tests)
+        self.chunks = self.last_chunks = 0  # row chunks launched through _grad_chunk_ready per step
+        self.timing = None
 
     # ------------------------------------------------------------------ async launches
     def _launch(self, tensors):
@@ -85,8 +100,33 @@ class GradAllReducer:
         if small:
             self._launch(small)
 
+    def grad_chunk_ready(self, param, full, rows, last: bool):
+        """Called from inside the backward with ``rows``, a contiguous row block of ``full`` (the
+        gradient of ``param``) that is final: its all-reduce is launched now, in place.  With ``last``
+        the whole gradient is handed to ``param.grad`` (the caller then gives autograd None for it)."""
+        if id(param) not in self.index or id(param) in self.done:
+            return
+        self._launch([rows])
+        self.chunks += 1
+        if last:
+            param.grad = full
+            param._mia_sqsum = None
+            self.done.add(id(param))
+            self.fired += 1
+
+    def exposed_ms(self):
+        """Mean over the recorded steps of the time the exchange ran past the end of the backward."""
+        if not self.timing:
+            return None
+        ts = [max(0.0, e0.elapsed_time(e1)) for e0, e1 in self.timing]
+        return sum(ts) / len(ts)
+
     def finish(self):
         """Reduce every gradient not yet reduced, then wait for all buckets (on the compute stream)."""
+        t0 = None
+        if self.cuda and self.timing is not None:
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record(torch.cuda.current_stream())
         rest = [p.grad for p in self.params if p.grad is not None and id(p) not in self.done]
         for p in self.params:
             p._mia_sqsum = None
@@ -99,6 +139,10 @@ class GradAllReducer:
                 bucket, size = [], 0
         if bucket:
             self._launch(bucket)
+        if t0 is not None:
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record(self.stream)
+            self.timing.append((t0, t1))
         if self.cuda:
             torch.cuda.current_stream().wait_stream(self.stream)
         for flat, tensors, copied in self.pending:
@@ -111,6 +155,7 @@ class GradAllReducer:
         self.pending.clear()
         self.done.clear()
         self.last_fired, self.fired = self.fired, 0
+        self.last_chunks, self.chunks = self.chunks, 0
         if self.broadcast_buffers:
             self._broadcast_buffers()
 

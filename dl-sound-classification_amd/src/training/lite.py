@@ -162,7 +162,11 @@ class Trainer:
         self.devices = devices
         self.log_every_n_steps = log_every_n_steps
         self.logger = logger
-        self.callbacks = list(callbacks or [])
+        # ModelCheckpoint runs after every other callback (Lightning's _reorder_callbacks), so the
+        # checkpoint it writes holds EarlyStopping's state of the same epoch
+        cbs = list(callbacks or [])
+        self.callbacks = ([cb for cb in cbs if not isinstance(cb, ModelCheckpoint)] +
+                          [cb for cb in cbs if isinstance(cb, ModelCheckpoint)])
         self.limits = {"train": limit_train_batches, "val": limit_val_batches, "test": limit_test_batches}
         self.should_stop = False
         self.world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -84,8 +84,9 @@ def _avg_ranks(v: torch.Tensor) -> torch.Tensor:
 
 class AUROC:
     """MulticlassAUROC, average='macro', one-vs-rest.  Scores are softmaxed per update unless already in
-    [0, 1] (torchmetrics' rule: AST's sigmoid outputs are used as they are); classes without positives
-    are left out; ties get average ranks (= the trapezoidal ROC area).  Scores are gathered from every
+    [0, 1] (torchmetrics' rule: AST's sigmoid outputs are used as they are); a class without positives
+    (or without negatives) scores 0 and counts in the mean, as in torchmetrics 1.7 (parity unpinned:
+    torchmetrics is not importable here); ties get average ranks (= the trapezoidal ROC area).  Scores are gathered from every
     rank at compute()."""
 
     def __init__(self, num_classes: int):
@@ -115,6 +116,9 @@ class AUROC:
             pos = t == c
             npos, nneg = int(pos.sum()), int((~pos).sum())
             if npos == 0 or nneg == 0:
+                # torchmetrics 1.7 (_binary_roc_compute) returns an all-zero TPR (no positives) or FPR (no
+                # negatives) curve here, whose area 0 enters the macro mean (it drops only NaN)
+                aucs.append(torch.tensor(0.0, dtype=torch.float64))
                 continue
             r = _avg_ranks(s[:, c].double())
             aucs.append((r[pos].sum() - npos * (npos + 1) / 2) / (npos * nneg))

@@ -36,6 +36,9 @@ class FusedAdam(torch.optim.Optimizer):
         self.clip = float(clip or 0.0)
         self.last_total_norm = None
         self.last_precomputed = 0  # tensors whose norm came from their GEMM's per-tile sums (last step)
+        self._table_key = None     # pointer table of the last step (host pinned + device copy)
+        self._table = None
+        self.table_builds = 0
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -60,7 +63,11 @@ class FusedAdam(torch.optim.Optimizer):
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["step"] += 1
-        step = int(self.state[ps[0]]["step"].item())
+        # torch's Adam keeps one step count per parameter; they differ only after a parameter missed
+        # gradients, and then the kernel takes the per-tensor counts
+        steps = [int(self.state[p]["step"].item()) for p in ps]
+        step = steps[0]
+        per_tensor_steps = any(v != step for v in steps)
         gs = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
         # parameters with a live bf16 operand copy (K.bf16_shadow) get it rewritten in the update pass
         shadows = [getattr(p, "_mia_bf16", None) if getattr(p, "_mia_bf16_ver", None) == p._version else None
@@ -76,7 +83,17 @@ class FusedAdam(torch.optim.Optimizer):
                 [p.numel() for p in ps]]
         if have_pre:
             rows += [[0 if q is None else q.data_ptr() for q in pre], [0 if q is None else q.numel() for q in pre]]
-        table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        # the device pointer table is rebuilt only when a pointer changed: in steady state the caching
+        # allocator hands every gradient the same storage step after step
+        key = tuple(map(tuple, rows))
+        if key != self._table_key:
+            host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+            self._table = (host, host.to(dev, non_blocking=True))
+            self._table_key = key
+            self.table_builds += 1
+        table = self._table[1]
+        steps_host = torch.tensor(steps, dtype=torch.int32).pin_memory() if per_tensor_steps else None
+        steps_dev = steps_host.to(dev, non_blocking=True) if per_tensor_steps else None
         n = len(ps)
         lib = L.load()
         ws = K.workspace(lib.mia_adam_workspace_bytes(n), dev, "adam")
@@ -95,6 +112,7 @@ class FusedAdam(torch.optim.Optimizer):
                                       float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
                                       table[6].data_ptr() if have_pre else None,
                                       table[7].data_ptr() if have_pre else None,
+                                      steps_dev.data_ptr() if per_tensor_steps else None,
                                       L.stream_ptr()), "mia_clip_adam")
         self.last_total_norm = tot
         for p, sh in zip(ps, shadows):
@@ -102,5 +120,5 @@ class FusedAdam(torch.optim.Optimizer):
                 p._mia_bf16_ver = p._version  # the copy now matches the updated parameter
         for p in ps:
             p._mia_sqsum = None  # consumed (or stale): the next step's gradient brings its own
-        self._keep = (table, gs, pre)  # keep the pointer table alive until the next step
+        self._keep = (gs, pre, steps_host, steps_dev)  # alive until the next step (async copies, table targets)
         return loss

@@ -368,13 +368,16 @@ int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32
  * pre_sq / pre_n (optional device tables, may be NULL): for tensor i with pre_sq[i] != NULL the norm
  * pass reads pre_n[i] partial sums of squares (doubles, e.g. a GEMM's MiaEpilogue.sqsum slots of the
  * gradient it wrote) instead of re-reading grads[i]; the partials are added in a fixed order.
- * clip <= 0 disables clipping. step is 1-based. */
+ * clip <= 0 disables clipping. step is 1-based; steps (optional device int32[n], may be NULL) gives
+ * each tensor its own 1-based step for the bias corrections (torch.optim.Adam keeps a step count per
+ * parameter; a parameter that had no gradient in some step is behind the others). */
 int64_t mia_adam_workspace_bytes(int32_t ntensors);
 int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
                   void* const* exp_avg_sq, void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors,
                   int64_t max_numel, float lr, float beta1, float beta2, float eps,
                   float weight_decay, int32_t step, float clip, float* total_norm_out,
-                  void* sqnorm_ws, const void* const* pre_sq, const int64_t* pre_n, mia_stream_t stream);
+                  void* sqnorm_ws, const void* const* pre_sq, const int64_t* pre_n, const int32_t* steps,
+                  mia_stream_t stream);
 
 /* LayerNorm over the last dim (timm Block norm1/norm2 and final norm, eps 1e-6).
  * x: (rows, D) -> y dtype; mean/rstd f32[rows] saved for backward. */

@@ -16,8 +16,9 @@ class TinyNet(nn.Module):
 
 class _EmitFn(torch.autograd.Function):
     """Linear -> ReLU -> Linear as ONE autograd node whose backward hands the head's gradients to the
-    data-parallel reducer through ``model._grad_ready`` and returns None for them — the contract of
-    the EnvNetV2 / AST autograd nodes (envnet_hip.py emit(), ast_hip.py)."""
+    data-parallel reducer through ``model._grad_ready`` (and fc1's weight gradient as two row chunks
+    through ``model._grad_chunk_ready``) and returns None for them — the contract of the EnvNetV2 /
+    AST autograd nodes (envnet_hip.py emit() and its FC1 chunks, ast_hip.py)."""
 
     @staticmethod
     def forward(ctx, model, x, w1, b1, w2, b2):
@@ -36,6 +37,12 @@ class _EmitFn(torch.autograd.Function):
         if ready is not None:
             ready([(ctx.model.fc2.weight, gw2), (ctx.model.fc2.bias, gb2)])
             gw2 = gb2 = None
+        chunk = getattr(ctx.model, "_grad_chunk_ready", None)
+        if chunk is not None:  # fc1.weight in two row chunks (the EnvNet FC1 path, envnet_hip.py)
+            gw1 = gw1.contiguous()
+            chunk(ctx.model.fc1.weight, gw1, gw1[:16], False)
+            chunk(ctx.model.fc1.weight, gw1, gw1[16:], True)
+            gw1 = None
         return None, None, gw1, gb1, gw2, gb2
 
 

@@ -4,8 +4,9 @@ Two ranks share the one GPU (gloo carries the GPU tensors: RCCL refuses two rank
 the 8-GPU RCCL run is the driver's).  Each rank runs EnvNetV2(compute_dtype="bf16") on its own clips:
 a warm-up step (the auto GEMM policy measures its first calls), a plain step whose gradients are the
 reference, then the same step under GradAllReducer (src/training/ddp.py), whose buckets leave from
-inside EnvNetFunction.backward through ``_grad_ready`` on the side stream (the FC gradients) and from
-``finish()`` (the rest).  The kernels are deterministic, so every averaged gradient must equal
+inside EnvNetFunction.backward through ``_grad_ready`` on the side stream (the FC gradients; FC1's
+weight gradient as 16 row chunks through ``_grad_chunk_ready``, one all-reduce per chunk GEMM) and
+from ``finish()`` (the rest).  The kernels are deterministic, so every averaged gradient must equal
 (g_0 + g_1) * 0.5 of the two ranks' plain gradients bit for bit (Lightning DDP's mean over ranks,
 reference base_training.yaml:45-51)."""
 import os
@@ -57,10 +58,10 @@ def _worker(rank, world, port, q):
             ref = (parts[0] + parts[1]) * (1.0 / world)
             if not torch.equal(p.grad.cpu(), ref):
                 mism.append((n, float((p.grad.cpu() - ref).abs().max())))
-        q.put((rank, red.last_fired, len(plain), mism, None))
+        q.put((rank, (red.last_fired, red.last_chunks), len(plain), mism, None))
         dist.destroy_process_group()
     except Exception as e:  # surface the worker's failure in the parent's assertion
-        q.put((rank, 0, 0, [], repr(e)))
+        q.put((rank, (0, 0), 0, [], repr(e)))
 
 
 @pytest.mark.timeout(600)
@@ -80,6 +81,7 @@ def test_grad_allreducer_envnet_hip_backward_two_ranks():
         assert p.exitcode == 0
     for r, (fired, nparam, mism, err) in res.items():
         assert err is None, (r, err)
-        assert fired > 0, "no gradient left through _grad_ready inside the HIP backward"
+        assert fired[0] > 0, "no gradient left through _grad_ready inside the HIP backward"
+        assert fired[1] == 4096 // 256, "FC1's weight gradient must leave as 16 row chunks of 86.5 MB"
         assert nparam > 20
         assert not mism, (r, mism[:5])

@@ -71,3 +71,31 @@ def test_adam_precomputed_sqsum(cuda):
         for p, r in zip(ps, ref):
             assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
         assert ps[0]._mia_sqsum is None  # consumed
+
+
+def test_adam_per_parameter_steps_and_table_reuse(cuda):
+    """torch.optim.Adam counts steps per parameter: a parameter without a gradient in some step is
+    skipped and its bias corrections lag the others'.  The fused step takes per-tensor counts then
+    (mia_clip_adam's ``steps`` table) and matches torch; with unchanged pointers the device pointer
+    table is not rebuilt."""
+    g = torch.Generator().manual_seed(5)
+    ps = [torch.nn.Parameter(torch.randn(n, generator=g).to(cuda)) for n in (515, 64, 3)]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedAdam(ps, lr=1e-2, weight_decay=1e-4, clip=0.0)
+    ropt = torch.optim.Adam(ref, lr=1e-2, weight_decay=1e-4)
+    grads = [torch.empty_like(p) for p in ps]  # fixed storage: the table key stays the same
+    for it in range(5):
+        for i, (p, r) in enumerate(zip(ps, ref)):
+            if it == 1 and i == 1:  # parameter 1 misses step 1
+                p.grad = r.grad = None
+                continue
+            grads[i].copy_(torch.randn(p.shape, generator=g).to(cuda))
+            p.grad, r.grad = grads[i], grads[i].clone()
+        opt.step()
+        ropt.step()
+        torch.cuda.synchronize()
+        for p, r in zip(ps, ref):
+            assert torch.allclose(p, r, rtol=1e-5, atol=1e-6), it
+    assert [int(opt.state[p]["step"]) for p in ps] == [5, 4, 5]
+    # builds: step 0 (3 tensors), step 1 (2 tensors), steps 2-4 (per-tensor counts, same pointers)
+    assert opt.table_builds == 3

@@ -264,7 +264,7 @@ def _emit_worker(rank, world, port, q):
         lit.model.bn.running_mean.fill_(float(rank + 1))  # rank 0's buffers must win
     lit.training_step((x, y), 0).backward()
     red.finish()
-    q.put((rank, red.last_fired, {n: p.detach().numpy().copy() for n, p in lit.named_parameters()},
+    q.put((rank, (red.last_fired, red.last_chunks), {n: p.detach().numpy().copy() for n, p in lit.named_parameters()},
            {n: p.grad.numpy().copy() for n, p in lit.named_parameters() if p.grad is not None},
            x.numpy().copy(), y.numpy().copy(),
            lit.model.bn.running_mean.numpy().copy()))
@@ -286,7 +286,7 @@ def test_grad_allreducer_emitting_backward_through_litclassifier_gloo():
         p.join(60)
         assert p.exitcode == 0
     for r in range(world):
-        assert res[r][0] == 2, "the head gradients must arrive through _grad_ready (overlapped path)"
+        assert res[r][0] == (3, 2), "head gradients through _grad_ready, fc1.weight as 2 row chunks (overlapped path)"
         assert (res[r][5] == 1.0).all()  # coalesced buffer broadcast from rank 0
     from src.training.engine import LitClassifier
     lit = LitClassifier({"_target_": "tests._toy.EmitNet", "num_classes": 5, "in_samples": 16},
@@ -406,6 +406,11 @@ def test_metrics_match_torchmetrics_weighting():
     # class 0: pos scores {0.2, 0.9}, neg {0.2, 0.4}: pairs (0.2,0.2)=0.5 (0.2,0.4)=0 (0.9,.)=1,1 -> 2.5/4
     # class 1: pos {0.5, 0.6}, neg {0.5, 0.1}: (0.5,0.5)=0.5 (0.5,0.1)=1 (0.6,.)=1,1 -> 3.5/4
     assert float(au.compute()) == pytest.approx((2.5 / 4 + 3.5 / 4) / 2)
+    # a class without positives (class 2 of 3) scores 0 and stays in the macro mean (torchmetrics 1.7
+    # _binary_roc_compute: all-zero TPR curve, area 0; only NaN is dropped)
+    au = M.AUROC(3)
+    au.update(torch.tensor([[0.7, 0.2, 0.1], [0.1, 0.8, 0.1], [0.6, 0.3, 0.1]]), torch.tensor([0, 1, 0]))
+    assert float(au.compute()) == pytest.approx((1.0 + 1.0 + 0.0) / 3)
 
 
 def test_config1_envnet_cpu_plumbing(tmp_path, monkeypatch):
@@ -460,3 +465,24 @@ def test_multi_crop_test_through_engine_step(tmp_path):
         loss = lit._step((xs, y), "test")
         mean_logits = torch.stack([lit(x) for x in xs]).mean(0)
     assert torch.allclose(loss, F.cross_entropy(mean_logits, y))
+
+
+def test_trainer_runs_modelcheckpoint_last(tmp_path):
+    """Lightning moves ModelCheckpoint callbacks behind the others (_reorder_callbacks), so a
+    checkpoint written at epoch end carries EarlyStopping's best/wait of that same epoch."""
+    from src.training.lite import EarlyStopping, ModelCheckpoint, Trainer
+    mc = ModelCheckpoint(monitor="val/acc", dirpath=str(tmp_path))
+    es = EarlyStopping(monitor="val/acc", patience=3)
+    tr = Trainer(callbacks=[mc, es], accelerator="cpu")
+    assert tr.callbacks == [es, mc]
+    saved = {}
+
+    class _M:  # the slice of the module / trainer that the two callbacks touch
+        current_epoch = 0
+
+    tr.save_checkpoint = lambda path: saved.update(es=dict(es.state_dict()))
+    for ep, v in enumerate((0.5, 0.7)):
+        _M.current_epoch = ep
+        for cb in tr.callbacks:
+            cb.on_epoch_end(tr, _M, {"val/acc": v, "epoch": ep})
+    assert saved["es"] == {"best": 0.7, "wait": 0}
