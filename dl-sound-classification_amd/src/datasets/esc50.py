@@ -61,8 +61,25 @@ class ESC50Dataset(Dataset):
     def _crop(self, w, start):
         return w[..., start:start + self.window]
 
+    def fit_window(self, w):
+        """A raw clip as the BC-mixing partner pool holds it: its first ``window`` samples, zero-padded
+        on the right when shorter (the reference mixes against the raw partner and truncates both to
+        the shorter length, BCMixingUtils.mix_waveforms preprocessing.py:462-466; ESC-50 clips are
+        exactly one window, so this is the identity there)."""
+        w = w[..., :self.window]
+        return torch.nn.functional.pad(w, (0, self.window - w.shape[-1])) if w.shape[-1] < self.window else w
+
     def __getitem__(self, idx):
         w, label = self.load(idx)
+        if self.mode == "envnet_v2" and not self.pad_crop:
+            # BC-mixing path: no T/2 padding, but the reference's random_crop still runs
+            # (esc50.py:233-234, preprocessing.py:841-855): a shorter clip (UrbanSound8K's <= 4 s) is
+            # right-padded to the window, a longer one cropped (random when training, else centred)
+            total = w.shape[-1]
+            if total <= self.window:
+                return torch.nn.functional.pad(w, (0, self.window - total)), label
+            start = random.randint(0, total - self.window) if self.training else (total - self.window) // 2
+            return self._crop(w, start), label
         if self.mode == "envnet_v2" and self.pad_crop:
             w = torch.nn.functional.pad(w, (self.pad, self.pad))
             total = w.shape[-1]
@@ -168,7 +185,10 @@ class ESC50DataModule:
         if self._pool is not None or not (self.enable_bc_mixing or self.enable_mixup):
             return
         ds = self._train_set
-        waves = torch.stack([ds.load(i)[0][0] for i in range(len(ds))]).to(self.device)
+        if self.is_spectrogram:
+            waves = torch.stack([ds.load(i)[0][0] for i in range(len(ds))]).to(self.device)
+        else:
+            waves = torch.stack([ds.fit_window(ds.load(i)[0])[0] for i in range(len(ds))]).to(self.device)
         self._pool_labels = torch.tensor(self._train_labels, dtype=torch.int64, device=self.device)
         if self.is_spectrogram:
             lm = self.logmel()

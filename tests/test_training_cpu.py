@@ -162,6 +162,16 @@ def test_urbansound8k_datamodule_files(tmp_path):
     assert yv.shape == (5, 10)
     cfg = compose(CFG, "training", ["dataset=urbansound8k"])
     assert cfg.dataset["_target_"] == "src.datasets.urbansound8k.UrbanSound8KDataModule"
+    # BC-mixing path (no T/2 pad): the reference's random_crop still right-pads a short clip to the
+    # window, and the partner pool holds window-length clips
+    dm = UrbanSound8KDataModule(root=str(tmp_path), fold=9, batch_size=5, num_workers=0, enable_bc_mixing=True,
+                                preprocessing_config={"window_length": 0.1})
+    dm.setup("fit")
+    w, _ = dm._train_set[0]
+    raw, _ = dm._train_set.load(0)
+    assert w.shape == (1, 4410) and torch.equal(w[:, :3000], raw) and not w[:, 3000:].any()
+    dm._pools()
+    assert dm._pool.shape == (len(dm._train_set), 4410)  # the train split (97 of 108)
 
 
 def test_train_script_toy(tmp_path, monkeypatch):
