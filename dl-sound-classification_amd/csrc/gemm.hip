@@ -16,7 +16,6 @@
 //  * 256 threads = 4 waves, each owning (BM/WM) x (BN/WN) of 32x32 accumulator tiles;
 //    register-staged double-buffered K loop (BK = 32), one barrier per K tile.
 //  * split-K writes f32 partial slabs; a reduce kernel applies the epilogue.
-#include "blaslt.h"
 #include "gemm_common.h"
 
 #include <cstdlib>
@@ -2049,74 +2048,46 @@ static int gemm_tile(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue
   return 0;
 }
 
-// Plain dense bf16 GEMMs (mblas::eligible) run on the tile kernel or on hipBLASLt by policy; under
-// MIA_GEMM_POLICY_AUTO the first call of each (shape, layout, epilogue) key times both on the
-// caller's stream (one warm-up + 3 timed runs each, HIP events) and keeps the faster for the
-// process.  Both write the same output buffer, so the last run leaves the correct result.
-static int gemm_autotune(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N,
-                         int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace, mia_stream_t stream) {
-  hipStream_t s = as_stream(stream);
-  hipEvent_t ev[4];
-  for (auto& e : ev)
-    if (hipEventCreate(&e) != hipSuccess) return mia::fail(-1, "gemm autotune: hipEventCreate");
-  float t_tile = 0.f, t_lib = 0.f;
-  int rc = 0;
-  for (int rep = 0; rep < 4 && rc == 0; ++rep) {
-    (void)hipEventRecord(ev[0], s);
-    rc = gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
-    (void)hipEventRecord(ev[1], s);
-    if (rc == 0) rc = mblas::run(*A, *B, *E, M, N, K, s);
-    (void)hipEventRecord(ev[2], s);
-    if (rc == 0) rc = gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);  // final result
-    (void)hipEventRecord(ev[3], s);
-    (void)hipEventSynchronize(ev[3]);
-    float a = 0.f, b = 0.f;
-    (void)hipEventElapsedTime(&a, ev[0], ev[1]);
-    (void)hipEventElapsedTime(&b, ev[1], ev[2]);
-    if (rep > 0) { t_tile += a; t_lib += b; }
-  }
-  for (auto& e : ev) (void)hipEventDestroy(e);
-  if (rc) return rc;
-  const int lib = t_lib < t_tile ? 1 : 0;
-  mblas::set_choice(*A, *B, *E, M, N, K, lib);
-  if (lib) return mblas::run(*A, *B, *E, M, N, K, s);
-  return 0;
-}
-
 extern "C" int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N) { return cdiv(M, 128) * cdiv(N, 128); }
 
-static int mia_gemm_impl(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N,
-                         int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace, mia_stream_t stream);
+// workspace layout of one mia_gemm call on paths 0-5: [split-K slabs][column-sum partials]
+static int64_t colsum_ws_offset(int64_t M, int64_t N, int32_t split_k) {
+  return cdiv(mia_gemm_workspace_bytes(M, N, split_k), 256) * 256;
+}
+
+extern "C" int64_t mia_gemm_workspace_bytes_ex(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E,
+                                               int64_t M, int64_t N, int64_t K, int32_t compute_dtype,
+                                               int32_t split_k) {
+  if (!A || !B || !E) return 0;
+  if (mgemm::mg_ok(*A, *B, *E, M, N, K, compute_dtype)) return mgemm::mg_workspace_bytes(M, N, K, E->colsum != nullptr);
+  int64_t b = mia_gemm_workspace_bytes(M, N, split_k);
+  if (E->colsum) b = colsum_ws_offset(M, N, split_k) + (int64_t)MIA_COLSUM_MAXBLK * N * 4;
+  return b;
+}
 
 extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
                         int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
                         mia_stream_t stream) {
   MIA_CHECK_ARG(A && B && E, "gemm: null descriptor");
+  if (E->ptr && M > 0 && N > 0 && K > 0 && mgemm::mg_ok(*A, *B, *E, M, N, K, compute_dtype))
+    return mgemm::mg_run(*A, *B, *E, M, N, K, workspace, as_stream(stream));
   if (E->colsum) {
     MIA_CHECK_ARG(!E->sqsum && !E->accumulate && !E->rm_inner && E->ldc >= N &&
                       (E->dtype == MIA_BF16 || E->dtype == MIA_F32),
                   "gemm: colsum needs a plain row-major output");
-    // the library path's dGELU pass delivers the sums itself when the measured choice is known to be
-    // the library before the call; otherwise (tile kernel, or the autotuning call) a column-sum pass
-    // over the stored output
-    const int pol = mblas::policy();
-    const bool lib = E->ptr && M > 0 && N > 0 && K > 0 && mblas::eligible(*A, *B, *E, M, N, K, compute_dtype) &&
-                     (split_k <= 1 || workspace) &&
-                     (pol == MIA_GEMM_POLICY_LIB ||
-                      (pol == MIA_GEMM_POLICY_AUTO && mblas::choice(*A, *B, *E, M, N, K) == 1));
-    if (int r = mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
-    if (!(lib && mblas::fuses_colsum(*E, N)) && M > 0 && N > 0) {
-      void* ws = mblas::scratch((size_t)MIA_COLSUM_MAXBLK * N * 4);
-      MIA_CHECK_ARG(ws, "gemm colsum: no scratch for N=%lld", (long long)N);
+    MIA_CHECK_ARG(workspace || M == 0 || N == 0, "gemm colsum: needs the workspace of mia_gemm_workspace_bytes_ex");
+    if (int r = gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
+    if (M > 0 && N > 0) {
+      void* ws = static_cast<char*>(workspace) + colsum_ws_offset(M, N, split_k);
       if (int r = mia_colsum(E->ptr, E->dtype, M, (int32_t)N, E->ldc, E->colsum, ws, stream)) return r;
     }
     return 0;
   }
-  if (!E->sqsum) return mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
+  if (!E->sqsum) return gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
   MIA_CHECK_ARG(E->dtype == MIA_F32 && E->act == MIA_ACT_NONE && !E->bias && !E->accumulate && !E->rm_inner &&
                     E->alpha == 1.f,
                 "gemm: sqsum needs a plain f32 output");
-  if (int r = mia_gemm_impl(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
+  if (int r = gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
   // the dense kernel writes the slots itself when it runs unsplit; every other path gets the pass
   const bool fused = dgemm_ok(*A, *B, M, N, K, compute_dtype) && split_k <= 1;
   if (!fused && M > 0 && N > 0) {
@@ -2129,36 +2100,13 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   return 0;
 }
 
-static int mia_gemm_impl(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N,
-                         int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace, mia_stream_t stream) {
-  if (E->ptr && M > 0 && N > 0 && K > 0 && mblas::eligible(*A, *B, *E, M, N, K, compute_dtype) &&
-      (split_k <= 1 || workspace)) {
-    const int pol = mblas::policy();
-    if (pol == MIA_GEMM_POLICY_LIB) return mblas::run(*A, *B, *E, M, N, K, as_stream(stream));
-    if (pol == MIA_GEMM_POLICY_AUTO) {
-      const int c = mblas::choice(*A, *B, *E, M, N, K);
-      if (c == 1) return mblas::run(*A, *B, *E, M, N, K, as_stream(stream));
-      if (c < 0) return gemm_autotune(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
-    }
-  }
-  return gemm_tile(A, B, E, M, N, K, compute_dtype, split_k, workspace, stream);
-}
-
 extern "C" int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                              int32_t compute_dtype, int32_t split_k) {
   if (!A || !B) return -1;
-  if (dgemm_ok(*A, *B, M, N, K, compute_dtype)) {
-    // 6 = hipBLASLt for a plain epilogue (no activation, no bias) when the policy (or the measured
-    // auto choice) selects it
-    MiaEpilogue e{};
-    e.ptr = reinterpret_cast<void*>(1); e.dtype = MIA_BF16; e.ldc = N; e.alpha = 1.f;
-    if (mblas::eligible(*A, *B, e, M, N, K, compute_dtype)) {
-      const int pol = mblas::policy();
-      if (pol == MIA_GEMM_POLICY_LIB || (pol == MIA_GEMM_POLICY_AUTO && mblas::choice(*A, *B, e, M, N, K) == 1))
-        return 6;
-    }
-    return 5;
-  }
+  MiaEpilogue e{};
+  e.ptr = reinterpret_cast<void*>(256); e.dtype = MIA_BF16; e.ldc = N; e.alpha = 1.f;
+  if (mgemm::mg_ok(*A, *B, e, M, N, K, compute_dtype)) return 7;
+  if (dgemm_ok(*A, *B, M, N, K, compute_dtype)) return 5;
   if (tapconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 4;
   if (rowconv_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 1;
   if (rowwgrad_ok(*A, *B, M, N, K, compute_dtype, split_k)) return 2;

@@ -175,6 +175,14 @@ struct W8Args {
 };
 hipError_t wgrad8_launch(const W8Args& a, hipStream_t s);
 
+// 256 x 256 dense bf16 GEMM of the AST linears (mgemm.hip): eligibility, workspace, launch
+bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+           int compute);
+int mg_split(int64_t M, int64_t N, int64_t K);
+int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum);
+int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+           void* workspace, hipStream_t s);
+
 
 
 }  // namespace mgemm

@@ -134,12 +134,6 @@ def _tiles(M, N):
     return math.ceil(M / bm) * math.ceil(N / bn)
 
 
-def gemm_policy(policy: int) -> None:
-    """Which kernel runs the plain dense bf16 GEMMs: L.GEMM_POLICY_TILE (hand-written tile kernel),
-    L.GEMM_POLICY_LIB (hipBLASLt) or L.GEMM_POLICY_AUTO (default: timed once per shape, faster kept)."""
-    L.check(L.load().mia_gemm_set_policy(int(policy)), "mia_gemm_set_policy")
-
-
 def auto_split(M: int, N: int, K: int, target_blocks: int = 1024, min_k: int = 1024) -> int:
     tiles = _tiles(M, N)
     if tiles >= target_blocks:
@@ -196,8 +190,9 @@ def gemm(A: L.MiaOperand, B: L.MiaOperand, E: L.MiaEpilogue, M: int, N: int, K: 
         else:
             split_k = auto_split(M, N, K)
     ws = None
-    if split_k > 1:
-        ws = workspace(lib.mia_gemm_workspace_bytes(M, N, split_k), device or torch.cuda.current_device(), "gemm")
+    nws = lib.mia_gemm_workspace_bytes_ex(A, B, E, M, N, K, compute, split_k)
+    if nws > 0:
+        ws = workspace(nws, device or torch.cuda.current_device(), "gemm")
     rec = PROBE is not None and tag in PROBE
     if rec:
         e0 = torch.cuda.Event(enable_timing=True)

@@ -20,7 +20,6 @@ OP_DENSE, OP_CONV, OP_CONVROW = 0, 1, 2
 KC, RC = 0, 1
 PRE_NONE, PRE_AFFINE, PRE_AFFINE_RELU, PRE_GELU = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU, ACT_ADD_AUX, ACT_GELU_SAVE = 0, 1, 2, 3, 4, 5, 6
-GEMM_POLICY_TILE, GEMM_POLICY_LIB, GEMM_POLICY_AUTO = 0, 1, 2
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -54,11 +53,10 @@ P = C.POINTER
 # name -> (restype, argtypes)
 SIGNATURES = {
     "mia_gemm_workspace_bytes": (i64, [i64, i64, i32]),
+    "mia_gemm_workspace_bytes_ex": (i64, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32]),
     "mia_gemm_sqsum_slots": (i64, [i64, i64]),
     "mia_gemm": (C.c_int, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32, vp, vp]),
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
-    "mia_gemm_set_policy": (C.c_int, [i32]),
-    "mia_gemm_lib_split": (C.c_int, [i32]),
     "mia_splitk_reduce": (C.c_int, [vp, i32, i64, i64, P(MiaEpilogue), vp]),
     "mia_logmel_workspace_bytes": (i64, [i64, i64]),
     "mia_logmel_fwd": (C.c_int, [vp, i64, i64, i64, P(MiaMelCfg), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

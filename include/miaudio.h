@@ -79,18 +79,23 @@ typedef struct MiaEpilogue {
   double* sqsum;
   /* Optional (NULL = off): colsum[n] = sum over the M rows of the stored output column n (f32 result,
    * summed from the stored -- for bf16, rounded -- values): the bias gradient of the linear whose dy
-   * this output is.  The library path's dGELU pass sums it on the way (timm fc1 behind the fc2
-   * dgrad); any other path gets a column-sum pass over the output.  Row-major output, no accumulate
-   * / row map / sqsum. */
+   * this output is.  The 256x256 kernel (path 7) sums it in its dGELU epilogue (timm fc1 behind the
+   * fc2 dgrad); any other path gets a column-sum pass over the output.  Row-major output, no
+   * accumulate / row map / sqsum.  Needs the workspace of mia_gemm_workspace_bytes_ex. */
   float* colsum;
 } MiaEpilogue;
 
-/* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16; f32: v_mfma_f32_32x32x2_f32).
+/* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16 / 16x16x32; f32: v_mfma_f32_32x32x2_f32).
  * Replaces cuDNN conv2d fwd/dgrad/wgrad for every EnvNetV2 conv (envnet_v2.py:15,19,31,34),
  * the nn.Linear layers (envnet_v2.py:51,55,59; ast.py:40 and timm Block qkv/proj/fc1/fc2,
- * ast.py:38,60-61) and the AST patch-embed conv (ast.py:30,55).
- * split_k > 1 needs a workspace of mia_gemm_workspace_bytes(M,N,split_k) bytes. */
+ * ast.py:38,60-61) and the AST patch-embed conv (ast.py:30,55).  Every path is a hand-written gfx950
+ * kernel; the kernel choice is a fixed function of the shapes, layouts and epilogue (no run-time
+ * timing), the library keeps no memory and never synchronises with the host.
+ * Workspace: mia_gemm_workspace_bytes_ex(...) bytes for exactly this call (split-K slabs, column-sum
+ * partials); mia_gemm_workspace_bytes(M, N, split_k) is the split-K part alone of paths 0-5. */
 int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k);
+int64_t mia_gemm_workspace_bytes_ex(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
+                                    int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k);
 /* number of MiaEpilogue.sqsum slots (doubles) of an M x N output */
 int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N);
 int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
@@ -102,23 +107,13 @@ int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int
  * B = the conv input as RC, M = Cout in {32,64}, split_k >= 2 partial slabs: blocks = KH x split),
  * 3 = single-channel tap weight gradient (conv1 pair view / 1-channel 8x8 conv3, M = 32, N = 64,
  * split_k >= 2 blocks), 4 = single-channel tap conv forward (the same two convs, N = 32, K = 64),
- * 5 = dense bf16 GEMM with LDS-DMA staging (bf16 DENSE operands, K % 64 == 0, M, N >= 64). */
+ * 5 = dense bf16 GEMM with LDS-DMA staging, 128x128 tiles (bf16 DENSE operands, K % 64 == 0,
+ * M, N >= 64: EnvNet FC layers, small token counts), 7 = dense bf16 GEMM, 256x256 tiles, 8 waves
+ * (M >= 1024 rows, N >= 256: the AST block linears at training batch sizes; its own split-K for the
+ * weight gradients, fused bias / GELU / GELU_SAVE / residual / dGELU + colsum epilogues).  Path 7
+ * is taken only for an epilogue it implements; E may be NULL here (plain epilogue assumed). */
 int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
                   int32_t compute_dtype, int32_t split_k);
-/* Dense bf16 GEMMs (DENSE bf16 operands, no pre-op, >= 10 GFLOP) whose epilogue is an optional f32
- * bias + ReLU, a residual add, GELU_SAVE or dGELU (bf16), with bf16/f32 output, may run on hipBLASLt
- * (path 6 above) instead of the tile kernel -- the GELU forms as the library GEMM plus one exact-erf
- * elementwise pass: TILE = always the hand-written kernel, LIB = always hipBLASLt, AUTO (default) =
- * the first call per (shape, layouts, epilogue) times both on the stream and keeps the faster.
- * The other fused epilogues (GELU, ReLU-mask, row maps, accumulate) and the implicit convolutions
- * always run on the tile kernels. */
-enum { MIA_GEMM_POLICY_TILE = 0, MIA_GEMM_POLICY_LIB = 1, MIA_GEMM_POLICY_AUTO = 2 };
-int mia_gemm_set_policy(int32_t policy);
-/* Library path, weight-gradient shapes (both operands RC, K >= 65536, no bias/activation): besides
- * the plain matmul, split-K variants (a strided batch over S = 4, 8, 16 contiguous K-slices into f32
- * partials, then a fixed-order sum of the S partials) are timed on the first call and the fastest is
- * kept.  split = 0 (default) uses that choice; 1, 4, 8, 16 force the plain / split-S variant (tests). */
-int mia_gemm_lib_split(int32_t split);
 
 /* Fused log-mel: frame gather + 1024-pt real FFT (LDS) + |X|^2 + htk mel (sparse bands)
  * + 10log10 + per-clip top_db clamp + per-clip mean/unbiased-std normalisation.

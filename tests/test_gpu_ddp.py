@@ -2,7 +2,7 @@
 
 Two ranks share the one GPU (gloo carries the GPU tensors: RCCL refuses two ranks on one device, and
 the 8-GPU RCCL run is the driver's).  Each rank runs EnvNetV2(compute_dtype="bf16") on its own clips:
-a warm-up step (the auto GEMM policy measures its first calls), a plain step whose gradients are the
+a warm-up step, a plain step whose gradients are the
 reference, then the same step under GradAllReducer (src/training/ddp.py), whose buckets leave from
 inside EnvNetFunction.backward through ``_grad_ready`` on the side stream (the FC gradients; FC1's
 weight gradient as 16 row chunks through ``_grad_chunk_ready``, one all-reduce per chunk GEMM) and

@@ -418,13 +418,6 @@ def test_conv1ch_dgrad_bf16(cuda, n, oh, ow):
     assert rel(out.float().cpu(), ref) < 1e-2
 
 
-@pytest.fixture
-def policy():
-    """Set the plain-GEMM policy for one test and restore the default (auto) afterwards."""
-    yield K.gemm_policy
-    K.gemm_policy(L.GEMM_POLICY_AUTO)
-
-
 def _big_operands(cuda, la, lb, M, N, Kd, seed):
     g = torch.Generator(device=cuda).manual_seed(seed)
     a = torch.randn(M, Kd, generator=g, device=cuda).to(torch.bfloat16)
@@ -436,42 +429,37 @@ def _big_operands(cuda, la, lb, M, N, Kd, seed):
     return a, b, A, Bo, g
 
 
-@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB, L.GEMM_POLICY_AUTO])
 @pytest.mark.parametrize("la,lb", [(L.KC, L.KC), (L.KC, L.RC), (L.RC, L.KC), (L.RC, L.RC)])
-@pytest.mark.parametrize("M,N,Kd,split", [(4096, 3072, 512, 1), (4000, 3000, 512, 1), (3840, 3584, 1024, 3)])
-def test_plain_gemm_policies(cuda, policy, pol, la, lb, M, N, Kd, split):
-    """Plain dense bf16 GEMM (bias + ReLU, bf16 out) on the tile kernel, on hipBLASLt and under the
-    timed auto choice vs a PyTorch fp32 matmul of the same bf16 operands: every layout pair, ragged
-    M/N edges, split-K slabs (tile path)."""
-    policy(pol)
-    a, b, A, Bo, g = _big_operands(cuda, la, lb, M, N, Kd, M + N + Kd)
-    path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, split)
-    assert path == (6 if pol == L.GEMM_POLICY_LIB else 5)
+@pytest.mark.parametrize("M,N,Kd", [(4096, 768, 768), (4136, 2304, 512), (8192, 264, 3072), (8200, 520, 1024)])
+def test_mgemm_layouts(cuda, la, lb, M, N, Kd):
+    """The 256x256 8-wave kernel (path 7, csrc/mgemm.hip) on every layout pair -- k-contiguous operands
+    read with ds_read_b128, k-by-m operands with ds_read_b64_tr_b16 -- ragged M (rows past M read as
+    zeros through the buffer range) and N (a 264-wide output: a partial column tile), bias + bf16 out,
+    vs a PyTorch fp32 matmul of the same bf16 operands.  Nothing is written outside the output."""
+    a, b, A, Bo, g = _big_operands(cuda, la, lb, M, N, Kd, M + N + Kd + 7 * la + 3 * lb)
+    assert L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1) == 7
     bias = torch.randn(N, generator=g, device=cuda)
-    ref = torch.relu(a.float() @ b.float().t() + bias)
-    for _ in range(2):  # auto: the first call measures both paths, the second runs the cached winner
-        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=cuda)
-        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_RELU, bias=bias), M, N, Kd, L.BF16, split_k=split)
-        torch.cuda.synchronize()
-        assert rel(out.float(), ref) < 1e-2
+    ref = a.float() @ b.float().t() + bias
+    full = torch.full((M + 3, N + 8), float("nan"), dtype=torch.bfloat16, device=cuda)
+    out = full[:M, :N]
+    K.gemm(A, Bo, K.epilogue(out, N + 8, bias=bias), M, N, Kd, L.BF16)
+    torch.cuda.synchronize()
+    assert torch.isnan(full[M:].float()).all() and torch.isnan(full[:, N:].float()).all()
+    assert rel(out.float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB])
-@pytest.mark.parametrize("case", ["wgrad_f32", "residual_f32", "bias_bf16", "gelu_save", "dact_gelu"])
-def test_plain_gemm_epilogues_both_paths(cuda, policy, pol, case):
-    """The epilogues the library path takes over, identical semantics on either path: f32 output of a
-    weight gradient (RC x RC), residual add into f32 with bias (AST proj/fc2 forward), bias only (qkv
-    forward), GELU_SAVE with bias (fc1 forward: erf GELU + saved pre-activation) and dGELU (fc2
-    backward-data: times gelu'(u), u = the saved pre-activation)."""
-    policy(pol)
-    if case == "wgrad_f32":
-        M, N, Kd, la, lb = 768, 2304, 8192, L.RC, L.RC
-    else:
-        M, N, Kd, la, lb = 8192, 768, 1024, L.KC, L.KC
-    a, b, A, Bo, g = _big_operands(cuda, la, lb, M, N, Kd, 11)
+@pytest.mark.parametrize("case", ["plain_f32", "residual_f32", "bias_bf16", "gelu", "gelu_save", "dact_gelu"])
+def test_mgemm_epilogues(cuda, case):
+    """The fused epilogues of the AST linears on the 256x256 kernel: f32 output, residual add into f32
+    with bias (proj / fc2 forward), bias only (qkv forward), exact-erf GELU, GELU_SAVE with bias (fc1
+    forward: gelu(u) and the saved u) and dGELU with the column sums of the stored values (fc2
+    backward-data: times gelu'(u); the sums are fc1's bias gradient) -- vs float64 / fp32 torch."""
+    M, N, Kd = 8192 + 37, 768 if case != "dact_gelu" else 3072, 768
+    a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 11)
     z = a.float() @ b.float().t()
     bias = torch.randn(N, generator=g, device=cuda)
-    if case == "wgrad_f32":
+    cs = None
+    if case == "plain_f32":
         out = torch.empty(M, N, dtype=torch.float32, device=cuda)
         K.gemm(A, Bo, K.epilogue(out, N), M, N, Kd, L.BF16)
         ref = z
@@ -484,6 +472,10 @@ def test_plain_gemm_epilogues_both_paths(cuda, policy, pol, case):
         out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
         K.gemm(A, Bo, K.epilogue(out, N, bias=bias), M, N, Kd, L.BF16)
         ref = z + bias
+    elif case == "gelu":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_GELU, bias=bias), M, N, Kd, L.BF16)
+        ref = F.gelu(z + bias)
     elif case == "gelu_save":
         u = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
@@ -494,56 +486,27 @@ def test_plain_gemm_epilogues_both_paths(cuda, policy, pol, case):
     else:
         u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
-        K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N), M, N, Kd, L.BF16)
+        cs = torch.full((N,), float("nan"), device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs), M, N, Kd, L.BF16)
         x = u.double().requires_grad_(True)
         F.gelu(x).backward(torch.ones_like(x))
         ref = z.double() * x.grad
     torch.cuda.synchronize()
     tol = 1e-4 if out.dtype == torch.float32 else 1e-2
     assert rel(out.float(), ref) < tol
-
-
-@pytest.mark.parametrize("pol", [L.GEMM_POLICY_TILE, L.GEMM_POLICY_LIB, L.GEMM_POLICY_AUTO])
-@pytest.mark.parametrize("case", ["dact_gelu", "plain"])
-def test_gemm_output_colsum(cuda, policy, pol, case):
-    """MiaEpilogue.colsum: the column sums of the stored output (the next linear's bias gradient) --
-    fused into the library path's dGELU pass (AST fc1 bias behind the fc2 dgrad), a column-sum pass
-    otherwise -- equal to float64 sums of what was stored, on every path (the auto policy's first
-    call runs both paths)."""
-    policy(pol)
-    M, N, Kd = 8192 + 37, 3072, 768
-    a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 13)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
-    for it in range(2 if pol == L.GEMM_POLICY_AUTO else 1):  # auto: the measuring call, then the chosen path
-        cs = torch.full((N,), float("nan"), device=cuda)
-        if case == "dact_gelu":
-            u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
-            K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs), M, N, Kd, L.BF16)
-        else:
-            K.gemm(A, Bo, K.epilogue(out, N, colsum=cs), M, N, Kd, L.BF16)
-        torch.cuda.synchronize()
-        ref = out.double().sum(0)
-        assert rel(cs, ref) < 1e-5, it
-
-
-@pytest.fixture
-def lib_split():
-    """Force one library weight-gradient variant for a test, restore the timed choice afterwards."""
-    yield lambda s: L.check(L.load().mia_gemm_lib_split(s), "mia_gemm_lib_split")
-    L.check(L.load().mia_gemm_lib_split(0), "mia_gemm_lib_split")
+    if cs is not None:
+        assert rel(cs, out.double().sum(0)) < 1e-5  # the sums of exactly what was stored
 
 
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("split", [1, 4, 8, 16, 0])
-def test_wgrad_lib_split_k(cuda, policy, lib_split, odt, split):
-    """Library weight-gradient shapes (RC x RC, K = tokens >= 65536): the plain matmul and the split-K
-    variants (strided batch over S K-slices into f32 partials + the fixed-order partial sum), forced one
-    by one, and the timed choice (0) -- vs a PyTorch fp32 matmul of the same bf16 operands, into a
-    strided output (ldc > N), bit-identical from call to call."""
-    policy(L.GEMM_POLICY_LIB)
-    lib_split(split)
-    M, N, Kd = 768, 1152, 69632
+@pytest.mark.parametrize("M,N,Kd", [(768, 2304, 69632 + 100), (2304, 768, 16384), (768, 768, 421120 // 8)])
+def test_mgemm_wgrad_split_k(cuda, odt, M, N, Kd):
+    """Weight-gradient shapes (both operands k-by-m, K = tokens, few output tiles): the kernel's own
+    split-K (a fixed function of the shape) into f32 slabs, summed in slice order -- vs a PyTorch fp32
+    matmul of the same bf16 operands; a K tail that is not a multiple of 64 (k-rows past K read as
+    zeros), a strided output (ldc > N, nothing written past N), bit-identical from call to call."""
     a, b, A, Bo, g = _big_operands(cuda, L.RC, L.RC, M, N, Kd, 17)
+    assert L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1) == 7
     ref = a.float() @ b.float().t()
     full = torch.full((M, N + 64), float("nan"), dtype=odt, device=cuda)
     out = full[:, :N]
@@ -552,9 +515,29 @@ def test_wgrad_lib_split_k(cuda, policy, lib_split, odt, split):
         K.gemm(A, Bo, K.epilogue(out, N + 64), M, N, Kd, L.BF16)
         torch.cuda.synchronize()
         outs.append(out.clone())
-    assert torch.isnan(full[:, N:].float()).all()  # nothing written past N
+    assert torch.isnan(full[:, N:].float()).all()
     assert torch.equal(outs[0], outs[1])
     assert rel(out.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("case", ["dact_gelu", "plain"])
+def test_mgemm_output_colsum(cuda, case):
+    """MiaEpilogue.colsum on both routes: fused into the 256x256 kernel's dGELU epilogue (AST fc1 bias
+    behind the fc2 dgrad) and, for an epilogue it does not fuse it into (the 128x128 dense kernel at a
+    small token count), a column-sum pass over the output in the caller's workspace -- equal to float64
+    sums of what was stored."""
+    M, N, Kd = (8192 + 37, 3072, 768) if case == "dact_gelu" else (900, 640, 256)
+    a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 13)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    cs = torch.full((N,), float("nan"), device=cuda)
+    if case == "dact_gelu":
+        u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs), M, N, Kd, L.BF16)
+    else:
+        assert L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1) == 5
+        K.gemm(A, Bo, K.epilogue(out, N, colsum=cs), M, N, Kd, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(cs, out.double().sum(0)) < 1e-5
 
 
 def test_wgrad8_many_items(cuda):

@@ -1,5 +1,6 @@
-"""Time the dense bf16 GEMM paths on the AST linear shapes (one process, interleaved rounds).
-    TOKENS=421120 python tools/bench_gemm.py   (each shape on the tile kernel and on hipBLASLt)"""
+"""Time mia_gemm on the AST linear shapes with the epilogues the AST step uses (one process).
+    TOKENS=421120 python tools/bench_gemm.py [name ...]
+Prints ms and TFLOP/s per shape (random bf16 operands; HIP events on the launch stream)."""
 import os
 import sys
 from pathlib import Path
@@ -11,38 +12,70 @@ import torch  # noqa: E402
 from src.miaudio import kernels as K  # noqa: E402
 from src.miaudio import lib as L  # noqa: E402
 
-T = int(os.environ.get("TOKENS", 105280))
-SHAPES = [  # (name, M, N, K, la, lb)
-    ("qkv.fwd", T, 2304, 768, L.KC, L.KC), ("fc1.fwd", T, 3072, 768, L.KC, L.KC),
-    ("fc2.fwd", T, 768, 3072, L.KC, L.KC), ("proj.fwd", T, 768, 768, L.KC, L.KC),
-    ("fc2.dgrad", T, 3072, 768, L.KC, L.RC), ("qkv.dgrad", T, 768, 2304, L.KC, L.RC),
-    ("fc1.wgrad", 3072, 768, T, L.RC, L.RC), ("qkv.wgrad", 2304, 768, T, L.RC, L.RC),
-    ("proj.dgrad", T, 768, 768, L.KC, L.RC), ("fc1.dgrad", T, 768, 3072, L.KC, L.RC),
-    ("proj.wgrad", 768, 768, T, L.RC, L.RC), ("fc2.wgrad", 768, 3072, T, L.RC, L.RC),
-    ("envfc1.fwd", 256, 4096, 84480, L.KC, L.KC), ("envfc1.dgrad", 256, 84480, 4096, L.KC, L.RC),
-    ("envfc1.wgrad", 4096, 84480, 256, L.RC, L.RC),
+T = int(os.environ.get("TOKENS", 421120))
+REPS = int(os.environ.get("REPS", 10))
+# (name, M, N, K, la, lb, epilogue kind)
+SHAPES = [
+    ("qkv.fwd", T, 2304, 768, L.KC, L.KC, "bias"), ("proj.fwd", T, 768, 768, L.KC, L.KC, "residual"),
+    ("fc1.fwd", T, 3072, 768, L.KC, L.KC, "gelu_save"), ("fc2.fwd", T, 768, 3072, L.KC, L.KC, "residual"),
+    ("fc2.dgrad", T, 3072, 768, L.KC, L.RC, "dgelu"), ("fc1.dgrad", T, 768, 3072, L.KC, L.RC, "plain"),
+    ("proj.dgrad", T, 768, 768, L.KC, L.RC, "plain"), ("qkv.dgrad", T, 768, 2304, L.KC, L.RC, "plain"),
+    ("fc2.wgrad", 768, 3072, T, L.RC, L.RC, "f32"), ("fc1.wgrad", 3072, 768, T, L.RC, L.RC, "f32"),
+    ("proj.wgrad", 768, 768, T, L.RC, L.RC, "f32"), ("qkv.wgrad", 2304, 768, T, L.RC, L.RC, "f32"),
 ]
-dev = torch.device("cuda:0")
-g = torch.Generator(device=dev).manual_seed(0)
-for name, M, N, Kd, la, lb in SHAPES:
-    a = (torch.randn(M, Kd, generator=g, device=dev) if la == L.KC else torch.randn(Kd, M, generator=g, device=dev)).to(torch.bfloat16)
-    b = (torch.randn(N, Kd, generator=g, device=dev) if lb == L.KC else torch.randn(Kd, N, generator=g, device=dev)).to(torch.bfloat16)
-    A = K.dense(a, la, *a.shape)
-    Bo = K.dense(b, lb, *b.shape)
-    out = torch.empty(M, N, dtype=torch.float32 if "wgrad" in name else torch.bfloat16, device=dev)
-    E = K.epilogue(out, N)
-    for pol, pname in ((L.GEMM_POLICY_TILE, "tile"), (L.GEMM_POLICY_LIB, "lib")):
-        K.gemm_policy(pol)
+
+def main():
+    want = set(sys.argv[1:])
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    total = 0.0
+    for name, M, N, Kd, la, lb, epi in SHAPES:
+        if want and name not in want:
+            continue
+        a = (torch.randn(M, Kd, generator=g, device=dev) if la == L.KC else torch.randn(Kd, M, generator=g, device=dev))
+        a = a.to(torch.bfloat16)
+        b = (torch.randn(N, Kd, generator=g, device=dev) if lb == L.KC else torch.randn(Kd, N, generator=g, device=dev))
+        b = b.to(torch.bfloat16)
+        A = K.dense(a, la, *a.shape)
+        Bo = K.dense(b, lb, *b.shape)
+        bias = torch.randn(N, generator=g, device=dev)
+        if epi == "f32":
+            out = torch.empty(M, N, dtype=torch.float32, device=dev)
+            E = K.epilogue(out, N)
+        elif epi == "residual":
+            out = torch.empty(M, N, dtype=torch.float32, device=dev)
+            res = torch.randn(M, N, generator=g, device=dev)
+            E = K.epilogue(out, N, act=L.ACT_ADD_AUX, bias=bias, aux=res, ldaux=N)
+        elif epi == "gelu_save":
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            u = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            E = K.epilogue(out, N, act=L.ACT_GELU_SAVE, bias=bias, aux=u, ldaux=N)
+        elif epi == "dgelu":
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            u = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
+            cs = torch.empty(N, device=dev)
+            E = K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs)
+        else:
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            E = K.epilogue(out, N, bias=bias if epi == "bias" else None)
+        path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1)
         for _ in range(2):
             K.gemm(A, Bo, E, M, N, Kd, L.BF16)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(10):
+        for _ in range(REPS):
             K.gemm(A, Bo, E, M, N, Kd, L.BF16)
         e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 10
-        print(f"{pname:4s} {name:12s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  {2 * M * N * Kd / ms / 1e9:7.1f} TF/s",
-              flush=True)
-K.gemm_policy(L.GEMM_POLICY_AUTO)
+        ms = e0.elapsed_time(e1) / REPS
+        total += ms
+        print(f"path {path} {name:11s} {epi:9s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
+              f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
+        del a, b, A, Bo, E, out
+        torch.cuda.empty_cache()
+    print(f"total {total:.3f} ms per block (x12 per step)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,696 @@
+// EXPERIMENT COPY of dl-sound-classification_amd/csrc/mgemm.hip (tools/probe: never linked into the
+// product library): the same kernel with run-time flags that select epilogue / scheduling variants,
+// for A/B timing in one process (tools/bench_mgexp.py).
+//   F_NODELAY  no first-wave start stagger        F_LDSEPI  bf16 outputs staged through LDS (16-B rows)
+//   F_NOSTORE  no epilogue memory traffic         F_PAIR    bf16 outputs as 16-B stores via lane pairs
+//   F_NOMAIN   no main loop (epilogue traffic alone, accumulators = lane-dependent constants)
+// Dense bf16 GEMM for the AST block linears (timm Block qkv / proj / fc1 / fc2, reference
+// src/models/ast.py:38,60-61): forward (x W^T), backward-data (dy W) and weight gradient (dy^T x)
+// with their epilogues fused -- bias, exact-erf GELU (+ the pre-activation saved for the backward),
+// the f32 residual add, gelu'(u) applied to the fc2 backward-data output together with the column
+// sums of what it stores (fc1's bias gradient), and deterministic split-K slabs for the weight
+// gradients.  Hand-written for gfx950; no vendor library, no run-time tuning, no host sync.
+//
+// * one 512-thread workgroup (8 waves, 2 per SIMD) per CU owns a 256 x 256 output tile; wave w keeps
+//   the 128 x 64 sub-tile (rows 128 * (w >> 2), columns 64 * (w & 3)) in 32 accumulators of
+//   v_mfma_f32_16x16x32_bf16 (128 VGPRs), computed TRANSPOSED (C^T = B^T A^T) so each lane holds four
+//   consecutive columns of one row: the epilogue stores 16 B (f32) / 8 B (bf16) per lane straight from
+//   the accumulators and reads the aux tensors the same way, no LDS pass;
+// * operand tiles travel HBM/L2 -> LDS by buffer-load LDS-DMA (16 B per lane, 1 KB per wave
+//   instruction) into two 64 KB stages; rows/k-rows outside the operand read as zeros (descriptor
+//   range), the XOR swizzle rides the per-lane SOURCE offset so every fragment read is conflict-free
+//   (ds_read_b128 for k-contiguous operands, ds_read_b64_tr_b16 for k-by-m operands);
+// * each K-tile is two phases of 32 MFMAs; waves 4-7 run one barrier behind waves 0-3, so on every
+//   SIMD one wave issues its MFMAs while its partner reads its fragments and issues the next
+//   LDS-DMA (MI355X_MICROARCH.md, "Two waves per SIMD"); every LDS-DMA is retired by a counted
+//   vmcnt one phase after its issue and read one barrier later;
+// * the tiles are identical work, so the CUs would run their HBM-bound epilogues (residual stream,
+//   GELU's saved pre-activation: up to 512 KB per tile) all at the same moment; the first workgroup
+//   on each CU starts 0, 1/4, 2/4 or 3/4 of a tile period late (by CU group), which keeps the
+//   epilogues of the four groups apart for the whole launch.
+#include "../../dl-sound-classification_amd/csrc/common.h"
+#include "../../dl-sound-classification_amd/csrc/gemm_common.h"
+
+namespace {
+
+constexpr int MG_NT = 512;
+constexpr int MG_BM = 256, MG_BN = 256, MG_BK = 64;
+constexpr int MG_HALF = 16384;                 // bytes of one half-tile (128 x 64 bf16)
+constexpr int MG_STAGE = 4 * MG_HALF;          // A0 A1 B0 B1
+constexpr int MG_LDS = 8 * 64 * 68 * 4;  // the staged epilogue's images (>= the two stages)
+
+enum { MG_KC = MIA_LAYOUT_KC, MG_RC = MIA_LAYOUT_RC };
+enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_GELU_SAVE = 2, EPI_ADD_AUX = 3, EPI_DGELU = 4, EPI_SLAB = 5 };
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_vp;
+
+struct MArgs {
+  const bf16* a;
+  const bf16* b;
+  int64_t lda, ldb, M, N, K, kper;
+  int nbm, nbn, split;
+  void* out;
+  int64_t ldc;
+  int out_f32;
+  const float* bias;
+  const void* aux;
+  int64_t ldaux;
+  float* ws;          // EPI_SLAB: [split][M][N] f32
+  float* colsum_part; // EPI_DGELU with colsum: [nbm][N] f32
+  int64_t delay;      // realtime ticks (100 MHz) of one quarter tile period: first-wave start stagger
+  int ncu;            // workgroups in the first wave (one per CU)
+  int flags;
+};
+enum { F_NODELAY = 1, F_LDSEPI = 2, F_NOSTORE = 4, F_PAIR = 8, F_NOMAIN = 16 };
+constexpr int MG_EPI_ROW = 68;
+constexpr int MG_EPI_WAVE = 64 * MG_EPI_ROW * 4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int64_t bytes) {
+  const uint32_t n = bytes <= 0 ? 0u : (bytes >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
+}
+
+// 32-byte chunk swizzle of the k-by-m images (RC): the 8 k-rows one 32-lane half of a transposed
+// fragment read touches ({k0..k0+3} and {k0+8..k0+11}) land on 8 different chunks
+__device__ __forceinline__ int rc_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// One operand (A or B) of the tile: its buffer descriptor, the four per-lane source offsets of this
+// wave's DMA instructions (2 per half-tile) and the byte step per K-tile.
+template <int L>
+struct Loader {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff[4];
+  uint32_t kstep;
+  // KC: rows [r0, r0 + 256) of a row-major [rows][K] operand, k from kbeg; RC: k-rows [kbeg, kend)
+  // of a row-major [K][cols] operand, columns [r0, r0 + 256)
+  __device__ __forceinline__ void init(const bf16* p, int64_t ld, int64_t rows, int64_t r0, int64_t kbeg,
+                                       int64_t kend, int wave, int lane) {
+    if constexpr (L == MG_KC) {
+      const bf16* base = p + r0 * ld + kbeg;
+      const int64_t nrows = rows - r0 < 256 ? rows - r0 : 256;
+      rsrc = rsrc_of(base, ((nrows - 1) * ld + (kend - kbeg)) * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hh = i >> 1, j = 2 * wave + (i & 1);
+        const int r = hh * 128 + 8 * j + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        voff[i] = (uint32_t)(((int64_t)r * ld + c * 8) * 2);
+      }
+      kstep = 128;
+    } else {
+      const bf16* base = p + kbeg * ld + r0;
+      const int64_t ncols = rows - r0 < 256 ? rows - r0 : 256;
+      rsrc = rsrc_of(base, ((kend - kbeg - 1) * ld + ncols) * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hh = i >> 1, j = 2 * wave + (i & 1);
+        const int k = 4 * j + (lane >> 4);
+        const int s = lane & 15;
+        const int c = (s >> 1) ^ rc_swz(k);
+        voff[i] = (uint32_t)(((int64_t)k * ld + hh * 128 + c * 16 + (s & 1) * 8) * 2);
+      }
+      kstep = (uint32_t)(64 * ld * 2);
+    }
+  }
+  // both half-tiles of K-tile kt into the stage at `tile` (this wave's 4 instructions)
+  __device__ __forceinline__ void issue(char* tile, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + (i >> 1) * MG_HALF + (2 * wave + (i & 1)) * 1024),
+                                               16, voff[i], kt * kstep, 0, 0);
+  }
+};
+
+// fragment of 16 rows (KC: operand rows; RC: operand columns) at `r0` inside a half-tile image, k-step ks
+template <int L>
+__device__ __forceinline__ bf16x8 frag(const char* half, int r0, int ks, int lane) {
+  if constexpr (L == MG_KC) {
+    const int r = r0 + (lane & 15);
+    const int c = 4 * ks + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(half + r * 128 + ((c ^ (r & 7)) << 4));
+  } else {
+    const int i = lane & 15, g = lane >> 4;
+    const int k = 32 * ks + 8 * g + (i >> 2);
+    const int ch = r0 >> 4;
+    const char* p0 = half + k * 256 + ((ch ^ rc_swz(k)) << 5) + (i & 3) * 8;
+    const char* p1 = half + (k + 4) * 256 + ((ch ^ rc_swz(k + 4)) << 5) + (i & 3) * 8;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
+    const s16x8 cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, cc);
+  }
+}
+
+// transposed product: lane (l & 15) = row of C, 4 (l >> 4) + r = its columns
+__device__ __forceinline__ f32x4 mfma_t(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint2 pack4(f32x4 v) {
+  const bf16 a = (bf16)v[0], b = (bf16)v[1], c = (bf16)v[2], d = (bf16)v[3];
+  return make_uint2((uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16),
+                    (uint32_t)__builtin_bit_cast(unsigned short, c) | ((uint32_t)__builtin_bit_cast(unsigned short, d) << 16));
+}
+__device__ __forceinline__ f32x4 unpack4(uint2 u) {
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+
+template <int LA, int LB, int EPI>
+__global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[MG_LDS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-aware tile order: the blocks one XCD runs (b, b + 8, ...) take consecutive logical tiles,
+  // N fastest, so a row block of A is read by all its column tiles from that XCD's L2
+  const int nwg = (int)gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_z = g.nbm * g.nbn;
+  const int z = lid / per_z;
+  const int rem = lid - z * per_z;
+  const int bm = rem / g.nbn, bn = rem - (rem / g.nbn) * g.nbn;
+  const int64_t m0 = (int64_t)bm * MG_BM, n0 = (int64_t)bn * MG_BN;
+  const int64_t kbeg = (int64_t)z * g.kper;
+  const int64_t kend = kbeg + g.kper < g.K ? kbeg + g.kper : g.K;
+  const int nk = kend > kbeg ? (int)((kend - kbeg + 63) >> 6) : 0;
+
+  // first wave: CU group (orig / 8) % 4 starts that many quarter tile periods late (see header)
+  if (g.delay > 0 && orig < g.ncu && !(g.flags & F_NODELAY)) {
+    const int64_t wait = g.delay * ((orig >> 3) & 3);
+    if (wait > 0) {
+      const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+      while ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(32);
+    }
+  }
+
+  Loader<LA> la;
+  Loader<LB> lb;
+  la.init(g.a, g.lda, g.M, m0, kbeg, kend, wave, lane);
+  lb.init(g.b, g.ldb, g.N, n0, kbeg, kend, wave, lane);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (g.flags & F_NOMAIN) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{(float)lane, (float)i, (float)j, 1.f};
+  }
+  const int nk_run = (g.flags & F_NOMAIN) ? 0 : nk;
+  char* const st0 = smem;
+  char* const st1 = smem + MG_STAGE;
+  // prologue: K-tile 0 (A and B) -> stage 0, K-tile 1's B -> stage 1
+  if (nk_run > 0) {
+    la.issue(st0, 0, wave);
+    lb.issue(st0 + 2 * MG_HALF, 0, wave);
+  }
+  if (nk_run > 1) {
+    lb.issue(st1 + 2 * MG_HALF, 1, wave);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int bhalf = wc >> 1;  // B half-tile holding this wave's 64 columns, at column 64 * (wc & 1)
+  const int bcol = 64 * (wc & 1);
+  bf16x8 af[2][4], bfr[2][4];
+  for (int t = 0; t < nk_run; ++t) {
+    const char* cur = (t & 1) ? st1 : st0;
+    const char* ah = cur + wr * MG_HALF;  // the wave's 128 rows are A half-tile wr
+    const char* bh = cur + (2 + bhalf) * MG_HALF;
+    // ---------------- phase 0: rows 0..63 of the wave's 128, all 64 columns
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag<LA>(ah, 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[ks][j] = frag<LB>(bh, bcol + 16 * j, ks, lane);
+    }
+    if (t + 1 < nk_run) {  // K-tile t+1's A -> the other stage (its previous contents, K-tile t-1, are read)
+      la.issue((t & 1) ? st0 : st1, t + 1, wave);
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_t(af[ks][i], bfr[ks][j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---------------- phase 1: rows 64..127, the same B fragments
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag<LA>(ah, 64 + 16 * i, ks, lane);
+    if (t + 2 < nk_run) {  // K-tile t+2's B -> this stage (K-tile t's B fragments are all in registers)
+      lb.issue(const_cast<char*>(cur) + 2 * MG_HALF, t + 2, wave);
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma_t(af[ks][i], bfr[ks][j], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two halves
+
+  // ---------------------------------------------------------------- epilogue variants
+  if (g.flags & F_NOSTORE) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+    if (sum == 1234.5678f && g.out) reinterpret_cast<float*>(g.ws ? (void*)g.ws : g.out)[0] = sum;
+    return;
+  }
+  const int64_t mb = m0 + wr * 128 + (lane & 15);
+  const int64_t nb = n0 + wc * 64 + 4 * (lane >> 4);
+  f32x4 bias4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = nb + 16 * j;
+    if (EPI != EPI_SLAB && EPI != EPI_DGELU && g.bias && n < g.N)
+      bias4[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
+    else
+      bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr bool BF_OUT = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU || EPI == EPI_PLAIN;
+  float* red = reinterpret_cast<float*>(smem);
+  if (BF_OUT && !g.out_f32 && (g.flags & F_LDSEPI)) {
+    // ---- staged: per-wave [64][68] f32 image, two passes, 8 columns per lane in the row pass
+    float* img = reinterpret_cast<float*>(smem + wave * MG_EPI_WAVE);
+    float cs8[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cs8[c] = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(img + (16 * i + (lane & 15)) * MG_EPI_ROW + 16 * j + 4 * (lane >> 4)) =
+              acc[4 * h + i][j] + bias4[j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) {
+        const int rr = 8 * it + (lane >> 3), cc = 8 * (lane & 7);
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(img + rr * MG_EPI_ROW + cc);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(img + rr * MG_EPI_ROW + cc + 4);
+        f32x4 v0 = lo, v1 = hi;
+        const int64_t m = m0 + wr * 128 + 64 * h + rr, n = n0 + wc * 64 + cc;
+        if (m >= g.M || n >= g.N) continue;
+        if constexpr (EPI == EPI_GELU_SAVE) {
+          const uint2 a0 = pack4(v0), a1 = pack4(v1);
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) =
+              make_uint4(a0.x, a0.y, a1.x, a1.y);
+        }
+        if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) { v0[c] = gelu_erf(v0[c]); v1[c] = gelu_erf(v1[c]); }
+        }
+        if constexpr (EPI == EPI_DGELU) {
+          const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n);
+          const f32x4 u0 = unpack4(make_uint2(u.x, u.y)), u1 = unpack4(make_uint2(u.z, u.w));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) { v0[c] *= gelu_erf_grad(u0[c]); v1[c] *= gelu_erf_grad(u1[c]); }
+        }
+        const uint2 p0 = pack4(v0), p1 = pack4(v1);
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = make_uint4(p0.x, p0.y, p1.x, p1.y);
+        if constexpr (EPI == EPI_DGELU) {
+          const f32x4 q0 = unpack4(p0), q1 = unpack4(p1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) { cs8[c] += q0[c]; cs8[4 + c] += q1[c]; }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      if (g.colsum_part) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float v = cs8[c];
+          v += __shfl_xor(v, 8, 64);
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          cs8[c] = v;
+        }
+        __syncthreads();
+        if (lane < 8) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) red[wr * 256 + wc * 64 + 8 * lane + c] = cs8[c];
+        }
+        __syncthreads();
+        if (threadIdx.x < 256) {
+          const int64_t n = n0 + threadIdx.x;
+          if (n < g.N) g.colsum_part[(int64_t)bm * g.N + n] = red[threadIdx.x] + red[256 + threadIdx.x];
+        }
+      }
+    }
+    return;
+  }
+  f32x4 cs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cs[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool pair = BF_OUT && !g.out_f32 && (g.flags & F_PAIR);
+  const int gq = lane >> 4;
+  const bool even = (gq & 1) == 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t m = mb + 16 * i;
+    const bool mok = m < g.M;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      uint2 pk[2], ax[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * jp + jj;
+        const int64_t n = nb + 16 * j;
+        const bool ok = mok && n < g.N;
+        f32x4 v = acc[i][j] + bias4[j];
+        if constexpr (EPI == EPI_SLAB) {
+          if (ok) *reinterpret_cast<f32x4*>(g.ws + ((int64_t)z * g.M + m) * g.N + n) = v;
+        } else if constexpr (EPI == EPI_ADD_AUX) {
+          if (ok) {
+            v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g.aux) + m * g.ldaux + n);
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + m * g.ldc + n) = v;
+          }
+        } else {
+          if (EPI == EPI_PLAIN && g.out_f32) {
+            if (ok) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + m * g.ldc + n) = v;
+            continue;
+          }
+          if constexpr (EPI == EPI_GELU_SAVE) ax[jj] = pack4(v);
+          if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = gelu_erf(v[c]);
+          }
+          if constexpr (EPI == EPI_DGELU) {
+            const f32x4 u = ok ? unpack4(*reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n))
+                               : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] *= gelu_erf_grad(u[c]);
+          }
+          pk[jj] = pack4(v);
+          if constexpr (EPI == EPI_DGELU) { if (ok) cs[j] += unpack4(pk[jj]); }
+          if (!pair && ok) {
+            *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = pk[jj];
+            if constexpr (EPI == EPI_GELU_SAVE)
+              *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) = ax[jj];
+          }
+        }
+      }
+      if constexpr (BF_OUT) {
+        if (pair) {
+          // lanes l, l ^ 16 hold columns 4g..4g+3 (g = l >> 4) of fragments j0 = 2jp, j1 = 2jp + 1:
+          // the even one stores j0's 8 columns from 4g, the odd one j1's 8 columns from 4(g - 1)
+          auto swap = [&](uint2 a, uint2 b) {
+            const uint2 send = even ? b : a;
+            uint2 recv;
+            recv.x = __shfl_xor(send.x, 16, 64);
+            recv.y = __shfl_xor(send.y, 16, 64);
+            const uint2 lo = even ? a : recv, hi = even ? recv : b;
+            return make_uint4(lo.x, lo.y, hi.x, hi.y);
+          };
+          const int64_t n = n0 + wc * 64 + 16 * (2 * jp + (even ? 0 : 1)) + 4 * (even ? gq : gq - 1);
+          const uint4 o = swap(pk[0], pk[1]);
+          if (mok && n < g.N) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = o;
+          if constexpr (EPI == EPI_GELU_SAVE) {
+            const uint4 q = swap(ax[0], ax[1]);
+            if (mok && n < g.N) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) = q;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    if (g.colsum_part) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v = cs[j][c];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          v += __shfl_xor(v, 8, 64);
+          cs[j][c] = v;
+        }
+      __syncthreads();
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(red + wr * 256 + wc * 64 + 16 * j + 4 * (lane >> 4)) = cs[j];
+      }
+      __syncthreads();
+      if (threadIdx.x < 256) {
+        const int64_t n = n0 + threadIdx.x;
+        if (n < g.N) g.colsum_part[(int64_t)bm * g.N + n] = red[threadIdx.x] + red[256 + threadIdx.x];
+      }
+    }
+  }
+}
+
+// Every instantiation explicitly: with implicit instantiation from launch_epi, hipcc (ROCm 7.2)
+// emitted the host-side launch stub of the first instantiation only (the others stayed undefined
+// symbols of the shared library).
+template __global__ void mgemm_kernel<0, 0, 0>(MArgs);
+template __global__ void mgemm_kernel<0, 0, 1>(MArgs);
+template __global__ void mgemm_kernel<0, 0, 2>(MArgs);
+template __global__ void mgemm_kernel<0, 0, 3>(MArgs);
+template __global__ void mgemm_kernel<0, 0, 4>(MArgs);
+template __global__ void mgemm_kernel<0, 0, 5>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 0>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 1>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 2>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 3>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 4>(MArgs);
+template __global__ void mgemm_kernel<0, 1, 5>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 0>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 1>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 2>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 3>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 4>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 5>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 0>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 1>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 2>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 3>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 4>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 5>(MArgs);
+
+// fixed-order split-K reduction of the f32 slabs into the epilogue's output (f32 or bf16, +bias)
+__global__ __launch_bounds__(256) void mg_splitk_reduce_kernel(const float* __restrict__ ws, int split, int64_t M,
+                                                               int64_t N, void* out, int64_t ldc, int out_f32,
+                                                               const float* __restrict__ bias) {
+  const int64_t n4 = N >> 2;
+  const int64_t total = M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / n4, n = (i - m * n4) * 4;
+    f32x4 s = *reinterpret_cast<const f32x4*>(ws + m * N + n);
+    for (int zz = 1; zz < split; ++zz) s += *reinterpret_cast<const f32x4*>(ws + ((int64_t)zz * M + m) * N + n);
+    if (bias) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] += bias[n + c];
+    }
+    if (out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + m * ldc + n) = s;
+    else *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + m * ldc + n) = pack4(s);
+  }
+}
+
+__global__ __launch_bounds__(256) void mg_colsum_final_kernel(const double* __restrict__ part2, int N, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) out[c] = (float)colsum_slices(part2, N, c);
+}
+
+template <int LA, int LB>
+hipError_t launch_epi(const MArgs& a, int epi, hipStream_t s) {
+  const unsigned grid = (unsigned)((int64_t)a.nbm * a.nbn * a.split);
+  switch (epi) {
+    case EPI_PLAIN: mgemm_kernel<LA, LB, EPI_PLAIN><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_GELU: mgemm_kernel<LA, LB, EPI_GELU><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_GELU_SAVE: mgemm_kernel<LA, LB, EPI_GELU_SAVE><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_ADD_AUX: mgemm_kernel<LA, LB, EPI_ADD_AUX><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_DGELU: mgemm_kernel<LA, LB, EPI_DGELU><<<grid, MG_NT, 0, s>>>(a); break;
+    default: mgemm_kernel<LA, LB, EPI_SLAB><<<grid, MG_NT, 0, s>>>(a); break;
+  }
+  return hipGetLastError();
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+namespace mgexp {
+
+// Which epilogue kind the kernel would run for E (-1: not this kernel)
+static int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
+  if (E.accumulate || E.rm_inner || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
+  const bool bf = E.dtype == MIA_BF16, f32 = E.dtype == MIA_F32;
+  if ((E.ldc & 3) || E.ldc < N || (reinterpret_cast<uintptr_t>(E.ptr) & (bf ? 7 : 15)) != 0) return -1;
+  if (E.bias && (reinterpret_cast<uintptr_t>(E.bias) & 15)) return -1;
+  const bool aux_ok = E.aux && aligned16(E.aux) && (E.ldaux & 3) == 0 && E.ldaux >= N;
+  switch (E.act) {
+    case MIA_ACT_NONE: return (bf || f32) && !E.colsum ? EPI_PLAIN : -1;
+    case MIA_ACT_GELU: return bf && !E.colsum ? EPI_GELU : -1;
+    case MIA_ACT_GELU_SAVE: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.colsum ? EPI_GELU_SAVE : -1;
+    case MIA_ACT_ADD_AUX: return f32 && aux_ok && E.aux_dtype == MIA_F32 && !E.colsum ? EPI_ADD_AUX : -1;
+    case MIA_DACT_GELU: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.bias ? EPI_DGELU : -1;
+    default: return -1;
+  }
+}
+
+// This kernel takes dense bf16 GEMMs big enough to fill the chip with 256 x 256 tiles (AST token
+// counts, or a weight gradient over them): A/B without pre-op, 16-B aligned, ld % 8 == 0, N % 4 == 0,
+// K % 64 == 0 where K is the contiguous dimension (KC), any K where it is the row index (RC).
+bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+           int compute) {
+  if (compute != MIA_BF16 || M < 256 || N < 256 || N % 4 || K < 64) return false;
+  if (cdiv(M, MG_BM) * cdiv(N, MG_BN) < 32 && K < 16384) return false;  // small: the 128 x 128 kernel
+  if (A.kind != MIA_OP_DENSE || B.kind != MIA_OP_DENSE || A.dtype != MIA_BF16 || B.dtype != MIA_BF16) return false;
+  if (A.pre != MIA_PRE_NONE || B.pre != MIA_PRE_NONE || A.ld % 8 || B.ld % 8 || !aligned16(A.ptr) || !aligned16(B.ptr))
+    return false;
+  if (A.layout == MIA_LAYOUT_KC) { if (A.rows != M || A.cols < K || K % MG_BK) return false; }
+  else if (A.rows < K || A.cols != M || M % 8) return false;
+  if (B.layout == MIA_LAYOUT_KC) { if (B.rows != N || B.cols < K || K % MG_BK) return false; }
+  else if (B.rows < K || B.cols != N || N % 8) return false;
+  if (cdiv(M, MG_BM) * cdiv(N, MG_BN) >= (1ll << 24)) return false;
+  return mg_epi_kind(E, N) >= 0;
+}
+
+// split-K width for the weight gradients (few output tiles, K = tokens): about 3 workgroups per
+// CU, K-slices of at least 1024; a fixed function of the shape (no timing)
+int mg_split(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = cdiv(M, MG_BM) * cdiv(N, MG_BN);
+  if (tiles >= 512 || K < 4096) return 1;
+  int64_t s = cdiv(768, tiles);
+  const int64_t smax = K / 1024;
+  if (s > smax) s = smax;
+  return (int)(s < 1 ? 1 : s);
+}
+
+static void mg_geometry(int64_t M, int64_t N, int64_t K, int& split, int64_t& kper) {
+  split = mg_split(M, N, K);
+  kper = cdiv(cdiv(K, split), 64) * 64;
+  split = (int)cdiv(K, kper);
+}
+
+int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum) {
+  int split;
+  int64_t kper;
+  mg_geometry(M, N, K, split, kper);
+  int64_t b = split > 1 ? (int64_t)split * M * N * 4 : 0;
+  b = cdiv(b, 256) * 256;
+  if (colsum) b += cdiv(cdiv(M, MG_BM) * N * 4, 256) * 256 + colsum_part2_bytes((int)N);
+  return b;
+}
+
+int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
+           void* workspace, hipStream_t s, int flags) {
+  const int epi = mg_epi_kind(E, N);
+  MArgs a;
+  memset(&a, 0, sizeof(a));
+  a.a = reinterpret_cast<const bf16*>(A.ptr);
+  a.b = reinterpret_cast<const bf16*>(B.ptr);
+  a.lda = A.ld; a.ldb = B.ld; a.M = M; a.N = N; a.K = K;
+  mg_geometry(M, N, K, a.split, a.kper);
+  a.nbm = (int)cdiv(M, MG_BM); a.nbn = (int)cdiv(N, MG_BN);
+  a.out = E.ptr; a.ldc = E.ldc; a.out_f32 = E.dtype == MIA_F32;
+  a.bias = E.bias; a.aux = E.aux; a.ldaux = E.ldaux;
+  // first-wave stagger: a quarter of the estimated tile period (MFMA time at ~4.6 TFLOP/s per CU plus
+  // the epilogue), only when the launch runs several waves of tiles
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      ncu = n > 0 ? n : 256;
+    else
+      ncu = 256;
+  }
+  a.ncu = ncu;
+  a.flags = flags;
+  const int64_t tiles = (int64_t)a.nbm * a.nbn * a.split;
+  const double tile_us = 2.0 * MG_BM * MG_BN * (double)a.kper / 4.6e6 + 4.0;
+  a.delay = tiles >= 3 * ncu ? (int64_t)(tile_us * 100.0 / 4.0) : 0;  // s_memrealtime: 100 MHz
+  const int need_ws = a.split > 1 || E.colsum;
+  MIA_CHECK_ARG(!need_ws || workspace, "gemm: the 256x128 path needs the workspace of mia_gemm_workspace_bytes_ex");
+  char* ws = reinterpret_cast<char*>(workspace);
+  int kind = epi;
+  if (a.split > 1) {
+    MIA_CHECK_ARG(epi == EPI_PLAIN && !E.colsum, "gemm: split-K weight gradients take a plain epilogue");
+    a.ws = reinterpret_cast<float*>(ws);
+    a.bias = nullptr;  // added by the reduction
+    kind = EPI_SLAB;
+    ws += cdiv((int64_t)a.split * M * N * 4, 256) * 256;
+  }
+  if (E.colsum) {
+    a.colsum_part = reinterpret_cast<float*>(ws);
+    ws += cdiv((int64_t)a.nbm * N * 4, 256) * 256;
+  }
+  hipError_t err;
+  const int la = A.layout, lb = B.layout;
+  if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = launch_epi<MG_KC, MG_KC>(a, kind, s);
+  else if (la == MIA_LAYOUT_KC) err = launch_epi<MG_KC, MG_RC>(a, kind, s);
+  else if (lb == MIA_LAYOUT_RC) err = launch_epi<MG_RC, MG_RC>(a, kind, s);
+  else err = launch_epi<MG_RC, MG_KC>(a, kind, s);
+  if (err != hipSuccess) return mia::fail(-(int)err, "mgemm launch: %s", hipGetErrorString(err));
+  if (a.split > 1) {
+    const int64_t total = M * (N / 4);
+    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+    mg_splitk_reduce_kernel<<<blocks, 256, 0, s>>>(a.ws, a.split, M, N, E.ptr, E.ldc, E.dtype == MIA_F32, E.bias);
+    MIA_LAUNCH_CHECK("mgemm splitk reduce");
+  }
+  if (E.colsum && kind == EPI_DGELU) {
+    double* part2 = reinterpret_cast<double*>(ws);
+    colsum_pass1(a.colsum_part, a.nbm, (int)N, N, part2, s);
+    mg_colsum_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, s>>>(part2, (int)N, E.colsum);
+    MIA_LAUNCH_CHECK("mgemm colsum");
+  }
+  return 0;
+}
+
+}  // namespace mgexp
+
+extern "C" int64_t mgexp_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum) {
+  return mgexp::mg_workspace_bytes(M, N, K, colsum);
+}
+extern "C" int mgexp_ok(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M, int64_t N, int64_t K) {
+  return mgexp::mg_ok(*A, *B, *E, M, N, K, MIA_BF16) ? 1 : 0;
+}
+extern "C" int mgexp_gemm(int flags, const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
+                          int64_t N, int64_t K, void* ws, void* stream) {
+  return mgexp::mg_run(*A, *B, *E, M, N, K, ws, reinterpret_cast<hipStream_t>(stream), flags);
+}
