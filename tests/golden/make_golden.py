@@ -4,6 +4,7 @@
 Run in this container only (the reference is not present on the GPU box):
     python tests/golden/make_golden.py        # golden.npz
     python tests/golden/make_golden.py aug    # golden_aug.npz (augmentations + pad/crop)
+    python tests/golden/make_golden.py split  # golden_split.npz (DataModule split + multi-crop)
 
 What runs from /root/reference (imported as-is, never copied):
   * src/models/envnet_v2.py::EnvNetV2                    (needs only torch)
@@ -13,7 +14,9 @@ What runs from /root/reference (imported as-is, never copied):
         synthetic weights because the pretrained DeiT checkpoint needs the network)
   * src/datasets/preprocessing.py::BCMixingDataset, ASTPreprocessor.apply_specaugment,
         EnvNetPreprocessor.apply_augmentation, and src/datasets/esc50.py::MixupDataset /
-        ESC50Dataset (through a two-line lightning stub), with Python's `random` seeded per case
+        ESC50Dataset (through a small lightning stub), with Python's `random` seeded per case
+  * src/datasets/esc50.py::ESC50DataModule.setup (the fold / stratified validation split) and
+        EnvNetPreprocessor.multi_crop_test
 Inputs/weights come from oracle/synth.py (splitmix64 counters) so the GPU tests can
 regenerate them bit-identically; only outputs and checksums are committed.
 The script also cross-checks oracle/ against these outputs and prints the errors.
@@ -294,8 +297,57 @@ def golden_aug(out):
                 out[f"{tag}__y"] = y.numpy()
 
 
+# --------------------------------------------------------------------------- data split + multi-crop
+def golden_split(out):
+    """The reference's own ESC50DataModule.setup (esc50.py:501-592: four train folds, stratified
+    validation split with StratifiedShuffleSplit(random_state=42), held-out test fold) on a synthetic
+    five-fold layout, and EnvNetPreprocessor.multi_crop_test (preprocessing.py:857-884) on padded
+    clips; the file lists are recorded as fold_k/name strings, the crops as checksums."""
+    import tempfile
+
+    from src.datasets.esc50 import ESC50DataModule
+    from src.datasets.preprocessing import EnvNetPreprocessor, PreprocessingConfig
+    from tests.golden._layout import (MCROP_CASES, SPLIT_CLASSES, SPLIT_FOLD_CLIPS, SPLIT_TEST_FOLD, mcrop_clip,
+                                      split_label)
+    with tempfile.TemporaryDirectory() as td:
+        root = Path(td) / "esc50"
+        for f in range(5):
+            (root / f"fold_{f}").mkdir(parents=True)
+            for i in range(SPLIT_FOLD_CLIPS):
+                torch.save({"waveform": torch.zeros(1, 64), "label": split_label(f, i)},
+                           root / f"fold_{f}" / f"c{i:03d}.pt")
+        dm = ESC50DataModule(root=str(root), fold=SPLIT_TEST_FOLD, val_split=0.1, batch_size=4, num_workers=0,
+                             num_classes=SPLIT_CLASSES, preprocessing_config={"window_length": 0.001})
+        dm.setup("fit")
+
+        def names(ds):
+            return np.array([f"{Path(f).parent.name}/{Path(f).name}" for f in ds.files])
+
+        out["split_train"] = names(dm._train_set)
+        out["split_val"] = names(dm._val_set)
+        out["split_test"] = names(dm._test_set)
+        print(f"[split] train {len(out['split_train'])} val {len(out['split_val'])} test {len(out['split_test'])}")
+    # multi-crop: crops of the T/2-padded clip at linspace(0, max_start, test_crops) starts
+    for s, (win, n, crops) in enumerate(MCROP_CASES):
+        pre = EnvNetPreprocessor(PreprocessingConfig(sample_rate=44100, window_length=win, test_crops=crops,
+                                                     multi_crop_test=True))
+        w = torch.from_numpy(mcrop_clip(s))
+        cs = pre.multi_crop_test(pre.preprocess(w, 44100))
+        out[f"mcrop{s}__n"] = np.array(len(cs))
+        for k, c in enumerate(cs):
+            pack(f"mcrop{s}_{k}", checksum(c.numpy(), 32), out)
+            out[f"mcrop{s}_{k}__shape"] = np.array(c.shape)
+
+
 def main():
     only = sys.argv[1:]
+    if only == ["split"]:
+        out = {}
+        golden_split(out)
+        dst = HERE / "golden_split.npz"
+        np.savez_compressed(dst, **out)
+        print(f"wrote {dst} ({dst.stat().st_size / 1e6:.2f} MB, {len(out)} arrays)")
+        return
     if only == ["aug"]:
         out = {}
         golden_aug(out)

@@ -4,6 +4,7 @@ BCMixingUtils / BCMixingDataset / ASTPreprocessor.apply_specaugment / MixupDatas
 EnvNetPreprocessor.apply_augmentation / ESC50Dataset with Python's `random` seeded per case), and
 the product ESC50Dataset's pad + crop (CPU host code) draws the same crops as the reference."""
 import random
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -116,3 +117,54 @@ def test_product_dataset_pad_crop_matches_reference(tmp_path, golden_aug):
             assert tuple(x.shape) == tuple(golden_aug[f"{tag}__shape"])
             _check(x.numpy(), golden_aug, tag, 0)
             assert int(np.argmax(golden_aug[f"{tag}__y"])) == label
+
+
+# ------------------------------------------------------------------ data split + multi-crop (reference-pinned)
+GOLDEN_SPLIT = np.load(Path(__file__).resolve().parent / "golden" / "golden_split.npz")
+
+
+def test_esc50_split_matches_reference_setup(tmp_path):
+    """ESC50DataModule.setup reproduces the reference's own split (tests/golden/golden_split.npz, written
+    by running reference esc50.py:501-592 on the same synthetic five-fold layout): identical train /
+    validation / test file lists, in the same order."""
+    from src.datasets.esc50 import ESC50DataModule
+    from tests.golden._layout import SPLIT_CLASSES, SPLIT_FOLD_CLIPS, SPLIT_TEST_FOLD, split_label
+    root = tmp_path / "esc50"
+    for f in range(5):
+        (root / f"fold_{f}").mkdir(parents=True)
+        for i in range(SPLIT_FOLD_CLIPS):
+            torch.save({"waveform": torch.zeros(1, 64), "label": split_label(f, i)}, root / f"fold_{f}" / f"c{i:03d}.pt")
+    dm = ESC50DataModule(root=str(root), fold=SPLIT_TEST_FOLD, val_split=0.1, batch_size=4, num_workers=0,
+                         num_classes=SPLIT_CLASSES, preprocessing_config={"window_length": 0.001})
+    dm.setup("fit")
+
+    def names(ds):
+        return [f"{Path(f).parent.name}/{Path(f).name}" for f in ds.files]
+
+    assert names(dm._train_set) == list(GOLDEN_SPLIT["split_train"])
+    assert names(dm._val_set) == list(GOLDEN_SPLIT["split_val"])
+    assert names(dm._test_set) == list(GOLDEN_SPLIT["split_test"])
+
+
+@pytest.mark.parametrize("s", [0, 1, 2])
+def test_multi_crop_matches_reference(tmp_path, s):
+    """Multi-crop test items = the reference's EnvNetPreprocessor.multi_crop_test of the T/2-padded clip
+    (preprocessing.py:814-827,857-884): crop count, shapes and contents (checksums of the reference's
+    crops).  The reference's dataset path (esc50.py:208-214) applies multi_crop_test BEFORE the
+    padding, which turns every 5 s ESC-50 clip into one 10 s crop the model cannot take; the padded
+    order pinned here is the one that yields `test_crops` window-length crops."""
+    from src.datasets.esc50 import ESC50Dataset
+    from tests.golden._layout import MCROP_CASES, checksum, mcrop_clip
+    win, n, crops = MCROP_CASES[s]
+    w = torch.from_numpy(mcrop_clip(s))
+    f = tmp_path / "clip.pt"
+    torch.save({"waveform": w, "label": 0}, f)
+    ds = ESC50Dataset(tmp_path, files=[f], window_length=win, pad_crop=True, training=False, multi_crop_test=True,
+                      test_crops=crops)
+    got, _ = ds[0]
+    assert len(got) == int(GOLDEN_SPLIT[f"mcrop{s}__n"])
+    for k, c in enumerate(got):
+        assert tuple(c.shape) == tuple(GOLDEN_SPLIT[f"mcrop{s}_{k}__shape"])
+        cs = checksum(c.numpy(), 32)
+        assert cs["sum"] == GOLDEN_SPLIT[f"mcrop{s}_{k}__sum"] and cs["sumsq"] == GOLDEN_SPLIT[f"mcrop{s}_{k}__sumsq"]
+        assert np.array_equal(cs["vals"], GOLDEN_SPLIT[f"mcrop{s}_{k}__vals"])
