@@ -765,8 +765,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
     sum += p;
   }
   sum = wave_sum(sum);
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   float o = 0.f;
   for (int k = 0; k < N; ++k) o = fmaf(sc[wave][k], base[(int64_t)k * ldt + 2 * H * D + lane], o);
   out[((int64_t)b * N + q) * H * D + hd * D + lane] = o / sum;
@@ -813,8 +812,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_f32_kernel(const float* __res
     const float p = expf(s - L);
     sc[wave][k] = p * (dp - dl);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   float a = 0.f;
   for (int k = 0; k < N; ++k) a = fmaf(sc[wave][k], base[(int64_t)k * ldt + H * D + lane], a);
   dqkv[((int64_t)b * N + q) * ldt + hd * D + lane] = a * scale;
@@ -849,8 +847,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_kernel(const float* __r
     sp[wave][q] = p;
     sd[wave][q] = p * (dp - delta[(int64_t)bh * N + q]);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   float dv = 0.f, dk = 0.f;
   for (int q = 0; q < N; ++q) {
     dv = fmaf(sp[wave][q], dout[((int64_t)b * N + q) * ldo + hd * D + lane], dv);

@@ -42,6 +42,16 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// Lanes of ONE wave exchanging data through LDS with no s_barrier.  The hardware runs a wave's LDS
+// instructions in order, but the compiler reasons per lane: another lane's store is a data race to
+// it, so without this fence it may reuse a load from the previous iteration or move loads/stores
+// across the exchange (seen: eval-mode fe_conv3 read stale B fragments in its second pipeline half).
+// Place it between the writes and the other lanes' reads, and between those reads and the next writes.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <typename T> __device__ __forceinline__ float to_f(T x);
 template <> __device__ __forceinline__ float to_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ float to_f<bf16>(bf16 x) { return (float)x; }

@@ -76,9 +76,9 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
   const int i16 = lane & 15, gq = lane >> 4, h = lane >> 5;
   const int n = lane & 31;  // tap within an N tile: ky = 4*nt + (n >> 3), kx = n & 7
   auto run = [&](const Raw& R) __attribute__((always_inline)) {
+    wave_sync();  // the previous item's fragment reads are done (common.h)
     {
-      // every lane writes (lanes 40..63 the same bytes as lanes 0..23): a branch on lane < 40 let the
-      // compiler sink the B-fragment reads below into the masked region (lanes >= 40 read nothing)
+      // every lane writes (lanes 40..63 the same bytes as lanes 0..23): no divergent staging
       const int l = lane < 40 ? lane : lane - 40;
       const int r = l / 5, q = l % 5;
       const uint32_t d[6] = {R.v[0][0], R.v[0][1], R.v[1][0], R.v[1][1], R.v[2][0], R.v[2][1]};
@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
       const int qq = lane + 64 * s;
       *reinterpret_cast<u32x4*>(dt + (qq >> 2) * 64 + (qq & 3) * 16) = R.d[s];
     }
+    wave_sync();
     const int kx = n & 7, cp = kx & 3;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {

@@ -188,7 +188,11 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
       constexpr int P = decltype(PC)::value;
       const int iy = r - g.ph;
       const bool live = iy >= 0 && iy < g.h;  // wave-uniform: padding rows contribute nothing
-      if (live) store_row();
+      if (live) {
+        wave_sync();  // the previous row's fragment reads are done (common.h)
+        store_row();
+        wave_sync();
+      }
       if (r + 1 < r_hi) load_row(r + 1);
       if (live) {
         // (kx, c) blocks of 16 MFMAs; the 10 fragments of block j+1 are read while block j computes

@@ -307,8 +307,10 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
   auto run = [&](int it, f32x2 xr) __attribute__((always_inline)) {
     const bf16 lo = (bf16)xr[0], hi = (bf16)xr[1];
     const uint32_t d = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    wave_sync();  // the previous item's fragment reads are done
     sg[lane] = d;
     if (lane >= 1) sg[96 + lane - 1] = d;
+    wave_sync();
     f32x16 acc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -450,6 +452,7 @@ __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
     return R;
   };
   auto run = [&](int it, const Raw& R) __attribute__((always_inline)) {
+    wave_sync();  // the previous item's fragment reads are done
     if (lane < 40) {
       const int r = lane / 5, q = lane % 5;
       const uint32_t d[6] = {R.v[0][0], R.v[0][1], R.v[1][0], R.v[1][1], R.v[2][0], R.v[2][1]};
@@ -465,6 +468,7 @@ __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
         *reinterpret_cast<u32x4*>(sg + c * CPYB + r * ROWB + 16 * q) = u32x4{o[0], o[1], o[2], o[3]};
       }
     }
+    wave_sync();
     f32x16 acc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;

@@ -60,12 +60,6 @@ __device__ __forceinline__ void dft8(float2 (&v)[8]) {
   v[3] = cadd(b6, b7); v[7] = csub(b6, b7);
 }
 
-// orders this wave's LDS writes before its later LDS reads by other lanes
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 __device__ __forceinline__ int reflect_idx(int n, int T) {
   if (n < 0) n = -n;
   if (n >= T) n = 2 * (T - 1) - n;

@@ -204,7 +204,7 @@ class ASTFunction(torch.autograd.Function):
             dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj", db=db_proj)
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
             work = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8, device=dev)
-            with K.probe("attn.bwd", 10.0 * B * Hh * N * N * (D // Hh),
+            with K.probe("attn.bwd", 8.0 * B * Hh * N * N * (D // Hh),  # 2x fwd, recompute not credited
                          (2 * dqkv.numel() + 2 * da.numel()) * dqkv.element_size()):
                 L.check(L.load().mia_attn_bwd(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
                                               sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), cd, B, N, Hh,

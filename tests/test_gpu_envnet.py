@@ -144,3 +144,33 @@ def test_cpu_input_fails_loudly():
     m = EnvNetV2()
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1, 220_500))
+
+
+def test_bf16_eval_with_running_statistics_tracks_autocast(cuda):
+    """bf16 eval mode (BN from running statistics, the stats-free launches of the wave-persistent
+    convs) on the seeded default init, running statistics populated by training-mode forwards of
+    other clips: logits as close to the f32 oracle as the oracle under autocast(bf16) gets, argmax
+    equal where f32 is decided.  (Regression: the eval-mode fe_conv3 launch read stale LDS fragments
+    in half of its items, 0.39 rel. vs autocast's 0.07, unseen by the hash-weight tests.)"""
+    from oracle import envnet as oenv
+    from src.models.envnet_v2 import EnvNetV2
+    torch.manual_seed(4321)
+    m = EnvNetV2(num_classes=50, dropout=0.0, compute_dtype="bf16").to(cuda).train()
+    with torch.no_grad():
+        for s in range(3):
+            m(torch.from_numpy(synth_waveform(500 + s, 4, 220_500)[:, None, :]).to(cuda))
+    m.eval()
+    x = torch.from_numpy(synth_waveform(77, 8, 220_500)[:, None, :]).to(cuda)
+    with torch.no_grad():
+        z = m(x).float()
+        q = {k: v.detach().clone() for k, v in m.state_dict().items() if not k.endswith("num_batches_tracked")}
+        z32 = oenv.forward(q, x, training=False, dropout_p=0.0).float()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            za = oenv.forward(q, x, training=False, dropout_p=0.0).float()
+    e_hip = float((z - z32).norm() / z32.norm())
+    e_ac = float((za - z32).norm() / z32.norm())
+    print(f"eval logits rel vs f32: hip bf16 {e_hip:.4f} autocast {e_ac:.4f}")
+    assert e_hip <= 1.5 * e_ac + 0.02, (e_hip, e_ac)
+    top2 = z32.topk(2, dim=1).values
+    decided = (top2[:, 0] - top2[:, 1]) > 2 * (z - z32).abs().max(1).values
+    assert torch.equal(z.argmax(1)[decided], z32.argmax(1)[decided])

@@ -410,3 +410,44 @@ def test_pool_fwd_raw_winners_feed_gather_bit_identical(cuda, geom, dtype):
     torch.cuda.synchronize()
     for u, v in zip(got, ref):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("kind", ["conv1", "conv3", "conv8"])
+def test_wave_conv_eval_mode_equals_training_mode(cuda, kind):
+    """The eval-mode launches (no BN statistics) of the wave-persistent EnvNet convs write the same
+    output, bit for bit, as their training-mode launches on the same operands."""
+    g = torch.Generator(device=cuda).manual_seed(77)
+    bias = torch.randn(32, generator=g, device=cuda) * 0.5
+    if kind == "conv1":
+        n, t = 3, 9000
+        x = torch.randn(n, t, generator=g, device=cuda) * 0.1
+        wp = K.pack_weight(torch.randn(32, 1, 1, 64, generator=g, device=cuda) * 0.1, L.BF16, 0)
+        P = n * ((t - 64) // 2 + 1)
+
+        def run(y, stats):
+            return K.fe_conv1_fwd(x, wp, bias, y, n, t, stats=stats)
+    elif kind == "conv3":
+        n, h, wd = 3, 64, 860
+        x = (torch.randn(n, h, wd, generator=g, device=cuda) * 0.5).to(torch.bfloat16)
+        wp = K.pack_weight(torch.randn(32, 1, 8, 8, generator=g, device=cuda) * 0.1, L.BF16, 0)
+        P = n * (h - 7) * (wd - 7)
+
+        def run(y, stats):
+            return K.fe_conv3_fwd(x, wp, bias, y, n, h, wd, stats=stats)
+    else:
+        n, h, wd = 2, 57, 853
+        x = (torch.randn(n, h, wd, 32, generator=g, device=cuda) * 0.7 + 0.1).to(torch.bfloat16)
+        scale = torch.rand(32, generator=g, device=cuda) + 0.5
+        shift = torch.randn(32, generator=g, device=cuda) * 0.3
+        wp = K.pack_weight(torch.randn(32, 32, 8, 8, generator=g, device=cuda) * 0.03, L.BF16, 0)
+        P = n * (h - 7) * (wd - 7)
+
+        def run(y, stats):
+            return K.trunk_conv8(x, wp, y, n, h, wd, scale=scale, shift=shift, bias=bias, stats=stats)
+    ya = torch.full((P, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    yb = torch.full((P, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    run(ya, True)
+    run(yb, False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(yb.float()).all()
+    assert torch.equal(ya, yb), float((ya.float() - yb.float()).abs().max())

@@ -24,7 +24,6 @@ from oracle import ast as oast
 from oracle import envnet as oenv
 from oracle import logmel as olog
 from oracle import train as otrain
-from tests._util import envnet_with_hash_params, hash_params
 
 pytestmark = pytest.mark.gpu
 
@@ -52,8 +51,8 @@ def _onehot(lbl, C):
     return torch.nn.functional.one_hot(lbl.long(), C).float()
 
 
-def _oracle_run(fwd, params, names, batches, steps, autocast, eval_fn):
-    opt = torch.optim.Adam([params[n] for n in names], lr=1e-4, weight_decay=1e-4)
+def _oracle_run(fwd, params, names, batches, steps, autocast, eval_fn, lr=1e-4):
+    opt = torch.optim.Adam([params[n] for n in names], lr=lr, weight_decay=1e-4)
     losses = []
     for it in range(steps):
         x, y = batches[it % len(batches)]
@@ -70,10 +69,10 @@ def _oracle_run(fwd, params, names, batches, steps, autocast, eval_fn):
     return np.array(losses), acc
 
 
-def _hip_run(model, batches, steps, eval_fn, input_sigmoid=False):
+def _hip_run(model, batches, steps, eval_fn, input_sigmoid=False, lr=1e-4):
     from src.miaudio import kernels as K
     from src.training.optim import FusedAdam
-    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
+    opt = FusedAdam(model.parameters(), lr=lr, weight_decay=1e-4, clip=1.0)
     losses = []
     for it in range(steps):
         x, y = batches[it % len(batches)]
@@ -107,33 +106,49 @@ def _compare(tag, hip, auto, f32, floor, acc_tol, min_drop):
 
 
 def test_envnet_bf16_multistep_training_parity(cuda):
-    C, B, steps = 10, 8, 60
-    xtr, ytr = tone_set(64, C, seed=1)
+    """EnvNet: 100 steps, batch 16 of 128 clips, Adam lr 1e-5.  At the reference's lr 1e-4 this small
+    set from the default init is chaotic -- Adam's first steps move every weight by ~lr*sign(g), the
+    logits blow up to losses of ~10 and two f32 runs that differ only in summation order end up on
+    unrelated trajectories (tools/diag/envnet_curves.py: per seed, the oracle's own autocast and f32
+    runs landed 3 nats apart) -- so a curve comparison there measures noise.  At 1e-5 all runs
+    converge and stay comparable; the held-out accuracy (eval mode: BN running statistics) is where
+    the eval-mode fe_conv3 defect showed (bf16 0.75 vs f32 0.91)."""
+    C, B, steps, n = 10, 16, 100, 128
+    xtr, ytr = tone_set(n, C, seed=1)
     xte, yte = tone_set(32, C, seed=2)
-    batches = [(xtr[i:i + B, None, :].to(cuda), _onehot(ytr[i:i + B], 50).to(cuda)) for i in range(0, 64, B)]
+    batches = [(xtr[i:i + B, None, :].to(cuda), _onehot(ytr[i:i + B], 50).to(cuda)) for i in range(0, n, B)]
     xte, yte = xte[:, None, :].to(cuda), yte.to(cuda)
+    lr = 1e-5
+
+    # the reference's own initialisation (envnet_v2.py:63-73 + replace_head), seeded
+    from src.models.envnet_v2 import EnvNetV2
+    torch.manual_seed(1234)
+    init = {k: v.clone() for k, v in EnvNetV2(num_classes=50, dropout=0.0, compute_dtype="bf16").state_dict().items()
+            if not k.endswith("num_batches_tracked")}
 
     def oracle(autocast):
-        p = {k: torch.from_numpy(v.copy()).to(cuda) for k, v in hash_params(100).items()}
+        p = {k: v.to(cuda) for k, v in init.items()}
         names = oenv.trainable_names(p)
-        for n in names:
-            p[n].requires_grad_(True)
+        for n_ in names:
+            p[n_].requires_grad_(True)
 
         def ev(q):
             z = torch.cat([oenv.forward(q, xte[i:i + 8], training=False, dropout_p=0.0) for i in range(0, 32, 8)])
             return float((z.float().argmax(1) == yte).float().mean())
 
         return _oracle_run(lambda q, x: oenv.forward(q, x, training=True, dropout_p=0.0), p, names, batches, steps,
-                           autocast, ev)
+                           autocast, ev, lr=lr)
 
-    m = envnet_with_hash_params(cuda, compute_dtype="bf16").train()
+    m = EnvNetV2(num_classes=50, dropout=0.0, compute_dtype="bf16")
+    m.load_state_dict(init, strict=False)
+    m = m.to(cuda).train()
 
     def ev_hip(model):
         z = torch.cat([model(xte[i:i + 8]) for i in range(0, 32, 8)])
         return float((z.float().argmax(1) == yte).float().mean())
 
-    hip = _hip_run(m, batches, steps, ev_hip)
-    _compare("envnet", hip, oracle(True), oracle(False), floor=0.01, acc_tol=2 / 32, min_drop=0.2)
+    hip = _hip_run(m, batches, steps, ev_hip, lr=lr)
+    _compare("envnet", hip, oracle(True), oracle(False), floor=0.02, acc_tol=2 / 32, min_drop=0.5)
 
 
 def test_ast_depth2_bf16_multistep_training_parity(cuda):

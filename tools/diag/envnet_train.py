@@ -44,7 +44,7 @@ for it in range(8):
     lo.backward()
     no = float(torch.nn.utils.clip_grad_norm_([p[n] for n in names], 1.0))
     zh = m(x)
-    lh, dz, _ = K.soft_ce(zh.detach().float().contiguous(), y)
+    lh, dz, _ = K.soft_ce(zh.detach().float().contiguous(), y, False)
     zh.backward(dz)
     nh = float(torch.sqrt(sum((q.grad.double() ** 2).sum() for q in m.parameters() if q.grad is not None)))
     print(f"step {it}: loss oracle {float(lo):.4f} hip {float(lh):.4f}  logits rel {float((zh.float()-z).norm()/z.norm()):.4f}"
