@@ -61,7 +61,8 @@ def parse():
                     help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=["both", "envnet", "ast"], default="both")
+    ap.add_argument("--model", choices=["both", "envnet", "ast", "ast-fp8"], default="both",
+                    help="both = EnvNet-v2 leg + AST bf16 leg + AST fp8-mixed leg (config 5's linears)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU EnvNet batch (default 256)")
     ap.add_argument("--ast-batch", type=int, default=None, help="per-GPU AST batch (default 256)")
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
@@ -316,7 +317,7 @@ def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_c
     ks = {k: v for k, v in kstats.items() if k not in regions}
     peak_tf = BF16_MFMA_PEAK_TF if args.dtype == "bf16" else F32_PEAK_TF
     dom = max(ks, key=lambda k: ks[k]["ms"] * ks[k]["launches_per_step"]) if ks else None
-    name = "EnvNet-v2" if model == "envnet" else "AST"
+    name = {"envnet": "EnvNet-v2", "ast": "AST", "ast_fp8": "AST fp8-mixed"}[model]
     out = {
         "metric": f"training clips/sec ({name}, ESC-50 shape)",
         "value": round(B * world * steps / elapsed, 2), "unit": "clips/s", "n_gpus": world, "steps": steps,
@@ -479,10 +480,28 @@ def main():
         log(f"AST: {results['ast']['value']} clips/s")
         del step
         free_leg()
-    out = results.get("envnet") or results["ast"]
+    if args.model in ("both", "ast-fp8"):
+        sys.path.insert(0, str(REPO))
+        from bench_ast import build_ast_step
+        log("AST fp8-mixed leg: building")
+        B = args.ast_batch or 256
+        step, fpc, tags, workload = build_ast_step(args, dev, rank, world, B, compute="fp8")
+        tags = args.probe.split(",") if args.probe else tags
+        el, loss, ks = time_leg(step, tags, args, world, dev, args.warmup, args.steps)
+        results["ast_fp8"] = leg_result("ast_fp8", B, world, args.steps, args.warmup, el, loss, ks, fpc, args,
+                                        workload, roof_tag="attn.fwd")
+        results["ast_fp8"]["config"]["model"] = "ast"
+        results["ast_fp8"]["config"]["precision"] = "fp8-mixed"
+        results["ast_fp8"]["dtype"] = "mxfp8-e4m3 (block linears fwd) + bf16"
+        log(f"AST fp8-mixed: {results['ast_fp8']['value']} clips/s")
+        del step
+        free_leg()
+    out = results.get("envnet") or results.get("ast") or results["ast_fp8"]
     if "envnet" in results and "ast" in results:
         out = dict(results["envnet"])
         out["ast"] = results["ast"]
+    if "ast_fp8" in results and out is not results["ast_fp8"]:
+        out["ast_fp8"] = results["ast_fp8"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads, why = cpu_threads()
         log(f"CPU baseline threads: {threads} ({why})")

@@ -14,7 +14,7 @@ import torch
 AST_FLOP_PER_CLIP = 1139.7e9  # fwd+bwd at 1645 tokens (flop_counter)
 
 
-def build_ast_step(args, dev, rank, world, B):
+def build_ast_step(args, dev, rank, world, B, compute=None):
     os.environ.setdefault("MIA_QUIET", "1")
     from src.datasets.augment import spec_augment_mixup
     from src.datasets.features import GpuLogMel
@@ -24,7 +24,7 @@ def build_ast_step(args, dev, rank, world, B):
     from src.training.optim import FusedAdam
 
     torch.manual_seed(42)
-    model = ASTModel(num_classes=50, compute_dtype=args.dtype).to(dev).train()
+    model = ASTModel(num_classes=50, compute_dtype=compute or args.dtype).to(dev).train()
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
     ddp = GradAllReducer(model, world) if world > 1 else None
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -51,4 +51,7 @@ def build_ast_step(args, dev, rank, world, B):
             "fc1.wgrad", "fc1.dgrad", "fc2.wgrad", "fc2.dgrad", "logmel.fwd", "optim.step"]
     workload = ("AST train step (log-mel, SpecAugment+Mixup, fwd, soft-CE, bwd, clip, Adam), "
                 "5 s @ 44.1 kHz -> 128x1379 log-mel -> 1645 tokens, DeiT-base/384 geometry")
+    if (compute or args.dtype) == "fp8":
+        workload += ("; trainer.precision=fp8-mixed: block linears' forward GEMMs on MX-fp8 operands "
+                     "(e4m3 + E8M0 per 32, v_mfma_scale_f32_16x16x128_f8f6f4), the rest bf16")
     return step, AST_FLOP_PER_CLIP, tags, workload

@@ -298,9 +298,14 @@ __device__ __forceinline__ void fwd_pv(FwdAcc& a, const bf16* V_, const bf16x8 (
   }
 }
 
+// MX (fp8-mixed): the bf16 output is also written as OCP MX-fp8 (e4m3 q8 [B*N][H*64], E8M0 s8
+// [B*N][H*2]) -- the proj MX GEMM's A operand.  Lanes l and l ^ 32 hold the 32 d of one block of one
+// query (16 each), so a block's amax is one lane-pair exchange.
+template <bool MX>
 __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                           float* __restrict__ lse, int N, int H, int nqb,
-                                                          float scale_log2) {
+                                                          float scale_log2, uint8_t* __restrict__ q8,
+                                                          uint8_t* __restrict__ s8) {
   __shared__ __attribute__((aligned(1024))) bf16 Ks[2][64 * 64];
   __shared__ __attribute__((aligned(1024))) bf16 Vs[2][64 * 64];
   const int t = threadIdx.x, lane = t & 63;
@@ -376,8 +381,29 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     }
   }
   const float lt = half_exchange_sum(a.l);
+  const float inv = 1.f / lt;
+  if constexpr (MX) {
+    // every lane takes part in the pair exchange; queries past the end store nothing
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      float v[16], am = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { v[r] = (float)(bf16)(a.o[dh][r] * inv); am = fmaxf(am, fabsf(v[r])); }
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const int e = mx_exponent(am);
+      if (q < N) {
+        uint8_t* qrow = q8 + ((int64_t)b * N + q) * H * D + hd * D + 32 * dh;
+#pragma unroll
+        for (int g2 = 0; g2 < 2; ++g2) {  // registers 8 g2 .. 8 g2 + 7 = d runs 16 g2 + {0..3, 8..11} (+4 high lanes)
+          const uint2 p = mx_pack8(v + 8 * g2, e);
+          *reinterpret_cast<uint32_t*>(qrow + 16 * g2 + 4 * (lane >> 5)) = p.x;
+          *reinterpret_cast<uint32_t*>(qrow + 16 * g2 + 8 + 4 * (lane >> 5)) = p.y;
+        }
+        if (lane < 32) s8[((int64_t)b * N + q) * H * 2 + hd * 2 + dh] = (uint8_t)(e + 127);
+      }
+    }
+  }
   if (q < N) {
-    const float inv = 1.f / lt;
     bf16* orow = out + ((int64_t)b * N + q) * H * D + hd * D;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {  // registers 4g4..4g4+3 = 4 consecutive d
@@ -391,6 +417,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     if (lane < 32) lse[(int64_t)bh * N + q] = (a.mb + log2f(lt)) / LOG2E;
   }
 }
+template __global__ void attn_fwd_kernel<false>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*);
+template __global__ void attn_fwd_kernel<true>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*);
 
 // ------------------------------------------------------------------------------ backward
 // Both backward kernels recompute P from the SAME MFMA operands the forward used (Q' = bf16(q * scale
@@ -874,9 +902,23 @@ extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtyp
   MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_fwd: one sequence must span < 2 GiB");
   const int nqb = (int)cdiv(N, FWD_Q);
   MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd: grid too large");
-  attn_fwd_kernel<<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>((const bf16*)qkv, (bf16*)out, lse, N, H, nqb,
-                                                                        scale * LOG2E);
+  attn_fwd_kernel<false><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
+      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, nullptr, nullptr);
   MIA_LAUNCH_CHECK("attn_fwd");
+  return 0;
+}
+
+extern "C" int mia_attn_fwd_mx(const void* qkv, void* out, float* lse, void* q8, void* s8, int32_t B, int32_t N,
+                               int32_t H, float scale, mia_stream_t stream) {
+  MIA_CHECK_ARG(qkv && out && lse && q8 && s8, "attn_fwd_mx: null pointer");
+  MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_fwd_mx: bad shape");
+  MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_fwd_mx: one sequence must span < 2 GiB");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(q8) & 3) == 0, "attn_fwd_mx: q8 must be 4-B aligned");
+  const int nqb = (int)cdiv(N, FWD_Q);
+  MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd_mx: grid too large");
+  attn_fwd_kernel<true><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
+      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, (uint8_t*)q8, (uint8_t*)s8);
+  MIA_LAUNCH_CHECK("attn_fwd_mx");
   return 0;
 }
 

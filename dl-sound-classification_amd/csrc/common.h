@@ -129,6 +129,38 @@ __device__ __forceinline__ double colsum_slices(const double* __restrict__ part2
   return v;
 }
 
+// ---------------------------------------------------------------- OCP MX-fp8 (see mia_mx_quantize)
+// shared exponent of a 32-element block from its amax: floor(log2(amax)) - 8 (e4m3 emax), clamped to
+// [-127, 127]; a zero / subnormal amax takes -127 (scale byte 0)
+__device__ __forceinline__ int mx_exponent(float amax) {
+  const int be = (int)((__float_as_uint(amax) >> 23) & 0xff);
+  const int e = be == 0 ? -127 : be - 127 - 8;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+// 8 values -> 8 e4m3fn bytes of x * 2^-e (v_ldexp_f32: exact, subnormal results included), saturated
+// to +-448 (v_med3_f32), round-to-nearest-even (v_cvt_pk_fp8_f32, OCP format on gfx950)
+__device__ __forceinline__ uint2 mx_pack8(const float* v, int e) {
+  float y[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) y[k] = __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(v[k], -e), -448.f, 448.f);
+  int p0 = 0, p1 = 0;
+  p0 = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], p0, false);
+  p0 = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], p0, true);
+  p1 = __builtin_amdgcn_cvt_pk_fp8_f32(y[4], y[5], p1, false);
+  p1 = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], p1, true);
+  return make_uint2((uint32_t)p0, (uint32_t)p1);
+}
+// 8 consecutive values held by each of 4 adjacent lanes (lane & 3 = quarter of the block): the block's
+// exponent from the 4 lanes' amax (every lane of the wave must execute this)
+__device__ __forceinline__ int mx_exponent_4lanes(const float* v) {
+  float am = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) am = fmaxf(am, fabsf(v[k]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  return mx_exponent(am);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

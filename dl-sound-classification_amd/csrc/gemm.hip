@@ -2071,6 +2071,8 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
   MIA_CHECK_ARG(A && B && E, "gemm: null descriptor");
   if (E->ptr && M > 0 && N > 0 && K > 0 && mgemm::mg_ok(*A, *B, *E, M, N, K, compute_dtype))
     return mgemm::mg_run(*A, *B, *E, M, N, K, workspace, as_stream(stream));
+  MIA_CHECK_ARG(!E->mx_q, "gemm: an MX-fp8 output copy needs the 256x256 kernel (bf16 dense operands, "
+                "plain / GELU / GELU_SAVE bf16 output, ldc == N, N %% 32 == 0)");
   if (E->colsum) {
     MIA_CHECK_ARG(!E->sqsum && !E->accumulate && !E->rm_inner && E->ldc >= N &&
                       (E->dtype == MIA_BF16 || E->dtype == MIA_F32),

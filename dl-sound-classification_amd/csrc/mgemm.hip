@@ -50,6 +50,8 @@ struct MArgs {
   int64_t ldaux;
   float* ws;          // EPI_SLAB: [split][M][N] f32
   float* colsum_part; // EPI_DGELU with colsum: [nbm][N] f32
+  uint8_t* mxq;       // optional MX-fp8 copy of a bf16 output: e4m3 [M][N] (row stride N) ...
+  uint8_t* mxs;       // ... and its scales [M][N / 32]
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int64_t bytes) {
@@ -158,6 +160,52 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x * 0.39894228040143268f, __expf(-0.5f * x * x), gelu_cdf(x));
 }
 
+// The same two functions on element pairs for the epilogues, which are VALU-bound: the polynomial and
+// the products run as packed f32 (v_pk_fma_f32 / v_pk_mul_f32, two lanes' worth per instruction), log2 e
+// is folded into the polynomial so the exponential is a bare v_exp_f32.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+constexpr float L2E = 1.4426950408889634f;
+// Phi(x) of a pair and z^2 = x^2 / 2
+__device__ __forceinline__ f2 gelu_cdf2(f2 x, f2& zz) {
+  const f2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f2 d = pfma(z, f2{0.5f, 0.5f}, f2{1.f, 1.f});
+  const f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f2 p = f2{0.17087277f * L2E, 0.17087277f * L2E};
+  p = pfma(p, t, f2{-0.82215223f * L2E, -0.82215223f * L2E});
+  p = pfma(p, t, f2{1.48851587f * L2E, 1.48851587f * L2E});
+  p = pfma(p, t, f2{-1.13520398f * L2E, -1.13520398f * L2E});
+  p = pfma(p, t, f2{0.27886807f * L2E, 0.27886807f * L2E});
+  p = pfma(p, t, f2{-0.18628806f * L2E, -0.18628806f * L2E});
+  p = pfma(p, t, f2{0.09678418f * L2E, 0.09678418f * L2E});
+  p = pfma(p, t, f2{0.37409196f * L2E, 0.37409196f * L2E});
+  p = pfma(p, t, f2{1.00002368f * L2E, 1.00002368f * L2E});
+  p = pfma(p, t, f2{-1.26551223f * L2E, -1.26551223f * L2E});
+  zz = z * z;
+  const f2 a = pfma(-zz, f2{L2E, L2E}, p);
+  const f2 he = t * f2{0.5f * __builtin_amdgcn_exp2f(a.x), 0.5f * __builtin_amdgcn_exp2f(a.y)};
+  return f2{x.x >= 0.f ? 1.f - he.x : he.x, x.y >= 0.f ? 1.f - he.y : he.y};
+}
+__device__ __forceinline__ f2 gelu2(f2 x) {
+  f2 zz;
+  return x * gelu_cdf2(x, zz);
+}
+__device__ __forceinline__ f2 gelu_grad2(f2 x) {
+  f2 zz;
+  const f2 c = gelu_cdf2(x, zz);
+  const f2 a = -zz * L2E;  // exp(-x^2 / 2)
+  return pfma(x * 0.39894228040143268f, f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, c);
+}
+// v * gelu'(u) / gelu(v) on 4 values in place
+__device__ __forceinline__ void gelu4(f32x4& v) {
+  const f2 a = gelu2(f2{v[0], v[1]}), b = gelu2(f2{v[2], v[3]});
+  v = f32x4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ void dgelu4(f32x4& v, f32x4 u) {
+  const f2 a = gelu_grad2(f2{u[0], u[1]}), b = gelu_grad2(f2{u[2], u[3]});
+  v = f32x4{v[0] * a.x, v[1] * a.y, v[2] * b.x, v[3] * b.y};
+}
+
 __device__ __forceinline__ uint2 pack4(f32x4 v) {
   const bf16 a = (bf16)v[0], b = (bf16)v[1], c = (bf16)v[2], d = (bf16)v[3];
   return make_uint2((uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16),
@@ -166,6 +214,138 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 __device__ __forceinline__ f32x4 unpack4(uint2 u) {
   return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                __uint_as_float(u.y & 0xffff0000u)};
+}
+
+// Epilogue shared by the bf16 and the MX-fp8 kernels: lane holds C[m][n .. n+3] of fragment (i, j):
+// m = m0 + 128 wr + 16 i + (lane & 15), n = n0 + 64 wc + 16 j + 4 (lane >> 4).  f32 outputs (residual
+// stream, slabs) are stored from the registers (16 B per lane); bf16 outputs are rounded, staged in a
+// per-wave [128][64] bf16 image and stored as 16-B pieces of whole 128-B rows, with the aux tensors read
+// the same way.
+template <int EPI>
+__device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], char* smem, int wave, int lane,
+                                            int bm, int z, int64_t m0, int64_t n0) {
+  const int wr = wave >> 2, wc = wave & 3;
+  f32x4 bias4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+    if (EPI != EPI_SLAB && EPI != EPI_DGELU && g.bias && n < g.N)
+      bias4[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
+    else
+      bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool bf_out = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU || (EPI == EPI_PLAIN && !g.out_f32);
+  if (!bf_out) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+        if (n >= g.N) continue;
+        f32x4 v = acc[i][j] + bias4[j];
+        if constexpr (EPI == EPI_ADD_AUX)
+          v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g.aux) + m * g.ldaux + n);
+        float* dst = EPI == EPI_SLAB ? g.ws + ((int64_t)z * g.M + m) * g.N + n
+                                     : reinterpret_cast<float*>(g.out) + m * g.ldc + n;
+        *reinterpret_cast<f32x4*>(dst) = v;
+      }
+    }
+    return;
+  }
+  if constexpr (EPI != EPI_SLAB && EPI != EPI_ADD_AUX) {
+    // all waves are past their last fragment read and every DMA has landed (vmcnt(0) in the last
+    // step): the ring is free.  Image row r, 16-B chunk c at chunk c ^ (r & 7) ^ ((r >> 3) & 1):
+    // conflict-free 8-B writes (16 rows of one column group) and 16-B row reads.
+    __syncthreads();
+    char* img = smem + wave * 16384;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * i + (lane & 15), g4 = lane >> 4;
+        const int c = 2 * j + (g4 >> 1);
+        *reinterpret_cast<uint2*>(img + r * 128 + ((c ^ (r & 7) ^ ((r >> 3) & 1)) << 4) + (g4 & 1) * 8) =
+            pack4(acc[i][j] + bias4[j]);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    float cs[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cs[c] = 0.f;
+    const int cc = lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int r = 8 * it + (lane >> 3);
+      const uint4 q = *reinterpret_cast<const uint4*>(img + r * 128 + ((cc ^ (r & 7) ^ ((r >> 3) & 1)) << 4));
+      const int64_t m = m0 + wr * 128 + r, n = n0 + wc * 64 + 8 * cc;
+      const bool ok = m < g.M && n < g.N;  // no early exit: the MX block exponent is a 4-lane exchange
+      uint4 o = q;
+      if constexpr (EPI == EPI_GELU_SAVE) {
+        if (ok) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) = q;
+      }
+      if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
+        f32x4 v0 = unpack4(make_uint2(q.x, q.y)), v1 = unpack4(make_uint2(q.z, q.w));
+        if constexpr (EPI == EPI_DGELU) {
+          const uint4 u = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)
+                             : make_uint4(0, 0, 0, 0);
+          const f32x4 u0 = unpack4(make_uint2(u.x, u.y)), u1 = unpack4(make_uint2(u.z, u.w));
+          dgelu4(v0, u0);
+          dgelu4(v1, u1);
+        } else {
+          gelu4(v0);
+          gelu4(v1);
+        }
+        const uint2 p0 = pack4(v0), p1 = pack4(v1);
+        o = make_uint4(p0.x, p0.y, p1.x, p1.y);
+        if constexpr (EPI == EPI_DGELU) {
+          if (ok) {
+            const f32x4 w0 = unpack4(p0), w1 = unpack4(p1);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { cs[k] += w0[k]; cs[4 + k] += w1[k]; }
+          }
+        }
+      }
+      if constexpr (EPI != EPI_DGELU) {
+        if (g.mxq) {  // MX-fp8 copy of the stored bf16 values (the next MX GEMM's A operand)
+          const f32x4 w0 = unpack4(make_uint2(o.x, o.y)), w1 = unpack4(make_uint2(o.z, o.w));
+          const float v8[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+          const int e = mx_exponent_4lanes(v8);
+          const uint2 p = mx_pack8(v8, e);
+          if (ok) {
+            *reinterpret_cast<uint2*>(g.mxq + m * g.N + n) = p;
+            if ((cc & 3) == 0) g.mxs[m * (g.N >> 5) + (n >> 5)] = (uint8_t)(e + 127);
+          }
+        }
+      }
+      if (ok) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = o;
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      if (g.colsum_part) {
+        // column sums of the stored values: lanes with equal (lane & 7) hold the same 8 columns
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float v = cs[c];
+          v += __shfl_xor(v, 8, 64);
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          cs[c] = v;
+        }
+        __syncthreads();  // every wave is done with its image
+        float* red = reinterpret_cast<float*>(smem);  // [2 row halves][256 columns]
+        if (lane < 8) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) red[wr * 256 + wc * 64 + 8 * lane + c] = cs[c];
+        }
+        __syncthreads();
+        if (threadIdx.x < 256) {
+          const int64_t n = n0 + threadIdx.x;
+          if (n < g.N) g.colsum_part[(int64_t)bm * g.N + n] = red[threadIdx.x] + red[256 + threadIdx.x];
+        }
+      }
+    }
+  }
 }
 
 template <int LA, int LB, int EPI>
@@ -280,117 +460,7 @@ __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two halves
-
-  // ---------------------------------------------------------------- epilogue
-  // lane holds C[m][n .. n+3] of fragment (i, j): m = m0 + 128 wr + 16 i + (lane & 15),
-  // n = n0 + 64 wc + 16 j + 4 (lane >> 4).  f32 outputs (residual stream, slabs) are stored from the
-  // registers (16 B per lane); bf16 outputs are rounded, staged in a per-wave [128][64] bf16 image
-  // and stored as 16-B pieces of whole 128-B rows, with the aux tensors read the same way.
-  f32x4 bias4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
-    if (EPI != EPI_SLAB && EPI != EPI_DGELU && g.bias && n < g.N)
-      bias4[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
-    else
-      bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const bool bf_out = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU || (EPI == EPI_PLAIN && !g.out_f32);
-  if (!bf_out) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
-        if (n >= g.N) continue;
-        f32x4 v = acc[i][j] + bias4[j];
-        if constexpr (EPI == EPI_ADD_AUX)
-          v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g.aux) + m * g.ldaux + n);
-        float* dst = EPI == EPI_SLAB ? g.ws + ((int64_t)z * g.M + m) * g.N + n
-                                     : reinterpret_cast<float*>(g.out) + m * g.ldc + n;
-        *reinterpret_cast<f32x4*>(dst) = v;
-      }
-    }
-    return;
-  }
-  if constexpr (EPI != EPI_SLAB && EPI != EPI_ADD_AUX) {
-    // all waves are past their last fragment read and every DMA has landed (vmcnt(0) in the last
-    // step): the ring is free.  Image row r, 16-B chunk c at chunk c ^ (r & 7) ^ ((r >> 3) & 1):
-    // conflict-free 8-B writes (16 rows of one column group) and 16-B row reads.
-    __syncthreads();
-    char* img = smem + wave * 16384;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 16 * i + (lane & 15), g4 = lane >> 4;
-        const int c = 2 * j + (g4 >> 1);
-        *reinterpret_cast<uint2*>(img + r * 128 + ((c ^ (r & 7) ^ ((r >> 3) & 1)) << 4) + (g4 & 1) * 8) =
-            pack4(acc[i][j] + bias4[j]);
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    float cs[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) cs[c] = 0.f;
-    const int cc = lane & 7;
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int r = 8 * it + (lane >> 3);
-      const uint4 q = *reinterpret_cast<const uint4*>(img + r * 128 + ((cc ^ (r & 7) ^ ((r >> 3) & 1)) << 4));
-      const int64_t m = m0 + wr * 128 + r, n = n0 + wc * 64 + 8 * cc;
-      if (m >= g.M || n >= g.N) continue;
-      uint4 o = q;
-      if constexpr (EPI == EPI_GELU_SAVE)
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) = q;
-      if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
-        f32x4 v0 = unpack4(make_uint2(q.x, q.y)), v1 = unpack4(make_uint2(q.z, q.w));
-        if constexpr (EPI == EPI_DGELU) {
-          const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n);
-          const f32x4 u0 = unpack4(make_uint2(u.x, u.y)), u1 = unpack4(make_uint2(u.z, u.w));
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { v0[k] *= gelu_grad_f(u0[k]); v1[k] *= gelu_grad_f(u1[k]); }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { v0[k] = gelu_f(v0[k]); v1[k] = gelu_f(v1[k]); }
-        }
-        const uint2 p0 = pack4(v0), p1 = pack4(v1);
-        o = make_uint4(p0.x, p0.y, p1.x, p1.y);
-        if constexpr (EPI == EPI_DGELU) {
-          const f32x4 w0 = unpack4(p0), w1 = unpack4(p1);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { cs[k] += w0[k]; cs[4 + k] += w1[k]; }
-        }
-      }
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = o;
-    }
-    if constexpr (EPI == EPI_DGELU) {
-      if (g.colsum_part) {
-        // column sums of the stored values: lanes with equal (lane & 7) hold the same 8 columns
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          float v = cs[c];
-          v += __shfl_xor(v, 8, 64);
-          v += __shfl_xor(v, 16, 64);
-          v += __shfl_xor(v, 32, 64);
-          cs[c] = v;
-        }
-        __syncthreads();  // every wave is done with its image
-        float* red = reinterpret_cast<float*>(smem);  // [2 row halves][256 columns]
-        if (lane < 8) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) red[wr * 256 + wc * 64 + 8 * lane + c] = cs[c];
-        }
-        __syncthreads();
-        if (threadIdx.x < 256) {
-          const int64_t n = n0 + threadIdx.x;
-          if (n < g.N) g.colsum_part[(int64_t)bm * g.N + n] = red[threadIdx.x] + red[256 + threadIdx.x];
-        }
-      }
-    }
-  }
+  mg_epilogue<EPI>(g, acc, smem, wave, lane, bm, z, m0, n0);
 }
 
 // Every instantiation explicitly: with implicit instantiation from launch_epi, hipcc (ROCm 7.2)
@@ -420,6 +490,188 @@ template __global__ void mgemm_kernel<1, 1, 2>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 3>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 4>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 5>(MArgs);
+
+// ---------------------------------------------------------------- MX-fp8 (OCP e4m3fn, E8M0 per 32 K)
+// Forward block linears under trainer.precision=fp8-mixed (north_star config 5; the reference has no fp8
+// path).  A [M][K] and B [N][K] are e4m3 bytes, K contiguous, with one E8M0 scale byte per 32 K-elements
+// ([rows][K / 32]).  The tile, LDS ring, phase structure and epilogue are the bf16 kernel's: a K-tile is
+// 128 e4m3 = 128 B per row (the bf16 kernel's 64 elements), so the loaders move the same bytes, and each
+// phase is 16 v_mfma_scale_f32_16x16x128_f8f6f4 (twice the cycles of a 16x16x32 bf16 MFMA for four
+// times the K: 2x the bf16 rate).  Operand lane map (tools/probe/mx16_layout.cpp, measured): lane group
+// g = lane >> 4 of row (lane & 15) holds k [16g, 16g + 16) and [64 + 16g, 64 + 16g + 16) of the K-tile,
+// i.e. 16-B chunks g and 4 + g of the row; the scale of (row, k-block b) comes from lane row + 16 b.
+// The per-K-tile scale dwords ([256 rows][4 blocks] for A and for B, 1 KB each) arrive by 4-B-per-lane
+// LDS-DMA with the A tile (waves 0-3: A rows 64w.., waves 4-7: B rows), double-buffered after the ring.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+constexpr int MX_SC = MG_LDS;  // scale ring: [2 stages][A 1 KB | B 1 KB]
+
+struct MxArgs {
+  const uint8_t* sa;  // [M][K / 32]
+  const uint8_t* sb;  // [N][K / 32]
+};
+
+__device__ __forceinline__ i32x8 mx_frag(const char* half, int r0, int lane) {
+  const int r = r0 + (lane & 15), g = lane >> 4;
+  const i32x4v lo = *reinterpret_cast<const i32x4v*>(half + r * 128 + ((g ^ (r & 7)) << 4));
+  const i32x4v hi = *reinterpret_cast<const i32x4v*>(half + r * 128 + (((4 + g) ^ (r & 7)) << 4));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+__device__ __forceinline__ int mx_scale(const char* sbuf, int r0, int lane) {
+  return *reinterpret_cast<const uint8_t*>(sbuf + (r0 + (lane & 15)) * 4 + (lane >> 4));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(MG_NT, 2) void mxgemm_kernel(MArgs g, MxArgs x) {
+  __shared__ __attribute__((aligned(1024))) char smem[MG_LDS + 4096];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nwg = (int)gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bm = lid / g.nbn, bn = lid - (lid / g.nbn) * g.nbn;
+  const int64_t m0 = (int64_t)bm * MG_BM, n0 = (int64_t)bn * MG_BN;
+  const int nk = (int)(g.K >> 7);
+  // e4m3 rows seen as bf16 pairs: the bf16 loaders move 128-B K-tiles unchanged
+  Loader<MG_KC> la, lb;
+  la.init(g.a, g.lda, g.M, m0, 0, g.K >> 1, wave, lane);
+  lb.init(g.b, g.ldb, g.N, n0, 0, g.K >> 1, wave, lane);
+  // scale DMA: one 4-B-per-lane piece per wave and K-tile (waves 0-3: A rows, 4-7: B rows)
+  const int64_t kb32 = g.K >> 5;
+  const int srow = 64 * (wave & 3) + lane;
+  const uint8_t* sbase = wr == 0 ? x.sa + m0 * kb32 : x.sb + n0 * kb32;
+  const int64_t srows = wr == 0 ? g.M - m0 : g.N - n0;
+  const __amdgpu_buffer_rsrc_t srsrc = rsrc_of(sbase, (srows < 256 ? srows : 256) * kb32);
+  const uint32_t svoff = (uint32_t)(srow * kb32);
+  char* const sdst0 = smem + MX_SC + wr * 1024 + (wave & 3) * 256;
+  auto sissue = [&](int kt) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(srsrc, (lds_vp)(sdst0 + (kt & 1) * 2048), 4, svoff, kt * 4, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  char* const st0 = smem;
+  char* const st1 = smem + MG_STAGE;
+  if (nk > 0) {
+    la.issue(st0, 0, wave);
+    sissue(0);
+    lb.issue(st0 + 2 * MG_HALF, 0, wave);
+  }
+  if (nk > 1) {
+    lb.issue(st1 + 2 * MG_HALF, 1, wave);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int bhalf = wc >> 1;
+  const int bcol = 64 * (wc & 1);
+  i32x8 af[4], bfr[4];
+  int sa[4], sb[4];
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = (t & 1) ? st1 : st0;
+    const char* ah = cur + wr * MG_HALF;
+    const char* bh = cur + (2 + bhalf) * MG_HALF;
+    const char* scur = smem + MX_SC + (t & 1) * 2048;
+    // ---------------- phase 0: rows 0..63 of the wave's 128
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { af[i] = mx_frag(ah, 16 * i, lane); sa[i] = mx_scale(scur, 128 * wr + 16 * i, lane); }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bfr[j] = mx_frag(bh, bcol + 16 * j, lane);
+      sb[j] = mx_scale(scur + 1024, 128 * bhalf + bcol + 16 * j, lane);
+    }
+    if (t + 1 < nk) {
+      la.issue((t & 1) ? st0 : st1, t + 1, wave);
+      sissue(t + 1);
+      asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, sb[j], 0, sa[i]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---------------- phase 1: rows 64..127, the same B fragments
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i] = mx_frag(ah, 64 + 16 * i, lane);
+      sa[i] = mx_scale(scur, 128 * wr + 64 + 16 * i, lane);
+    }
+    if (t + 2 < nk) {
+      lb.issue(const_cast<char*>(cur) + 2 * MG_HALF, t + 2, wave);
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] =
+            __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[4 + i][j], 0, 0, 0, sb[j], 0, sa[i]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+  mg_epilogue<EPI>(g, acc, smem, wave, lane, bm, 0, m0, n0);
+}
+template __global__ void mxgemm_kernel<0>(MArgs, MxArgs);
+template __global__ void mxgemm_kernel<1>(MArgs, MxArgs);
+template __global__ void mxgemm_kernel<2>(MArgs, MxArgs);
+template __global__ void mxgemm_kernel<3>(MArgs, MxArgs);
+
+// MX quantiser: 8 values per thread, 4 threads per 32-element block (a block never straddles a row:
+// cols % 32 == 0).  OCP MX rule: shared exponent e = floor(log2(amax)) - 8 (e4m3 emax), clamped to
+// [-127, 127], scale byte e + 127; elements x * 2^-e saturated to +-448 and rounded to nearest-even
+// e4m3fn (v_cvt_pk_fp8_f32, OCP format on gfx950); an all-zero block gets scale byte 0.
+template <typename T>
+__global__ __launch_bounds__(256) void mx_quant_kernel(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
+                                                       uint8_t* __restrict__ q, int64_t ldq, uint8_t* __restrict__ sc) {
+  const int64_t per_row = cols >> 3;
+  const int64_t total = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row, c = (i - r * per_row) * 8;
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      const uint4 u = *reinterpret_cast<const uint4*>(x + r * ldx + c);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[2 * k] = __uint_as_float(w[k] << 16); v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(x + r * ldx + c);
+      const float4 b = *reinterpret_cast<const float4*>(x + r * ldx + c + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    const int e = mx_exponent_4lanes(v);
+    *reinterpret_cast<uint2*>(q + r * ldq + c) = mx_pack8(v, e);
+    if ((c & 31) == 0) sc[r * (cols >> 5) + (c >> 5)] = (uint8_t)(e + 127);
+  }
+}
 
 // fixed-order split-K reduction of the f32 slabs into the epilogue's output (f32 or bf16, +bias)
 __global__ __launch_bounds__(256) void mg_splitk_reduce_kernel(const float* __restrict__ ws, int split, int64_t M,
@@ -466,8 +718,11 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 namespace mgemm {
 
 // Which epilogue kind the kernel would run for E (-1: not this kernel)
-static int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
+int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
   if (E.accumulate || E.rm_inner || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
+  if (E.mx_q && (!E.mx_scales || E.dtype != MIA_BF16 || E.ldc != N || N % 32 || E.colsum ||
+                 !(E.act == MIA_ACT_NONE || E.act == MIA_ACT_GELU || E.act == MIA_ACT_GELU_SAVE)))
+    return -1;
   const bool bf = E.dtype == MIA_BF16, f32 = E.dtype == MIA_F32;
   if ((E.ldc & 3) || E.ldc < N || (reinterpret_cast<uintptr_t>(E.ptr) & (bf ? 7 : 15)) != 0) return -1;
   if (E.bias && (reinterpret_cast<uintptr_t>(E.bias) & 15)) return -1;
@@ -539,6 +794,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   a.nbm = (int)cdiv(M, MG_BM); a.nbn = (int)cdiv(N, MG_BN);
   a.out = E.ptr; a.ldc = E.ldc; a.out_f32 = E.dtype == MIA_F32;
   a.bias = E.bias; a.aux = E.aux; a.ldaux = E.ldaux;
+  a.mxq = reinterpret_cast<uint8_t*>(E.mx_q); a.mxs = reinterpret_cast<uint8_t*>(E.mx_scales);
   const int need_ws = a.split > 1 || E.colsum;
   MIA_CHECK_ARG(!need_ws || workspace, "gemm: the 256x128 path needs the workspace of mia_gemm_workspace_bytes_ex");
   char* ws = reinterpret_cast<char*>(workspace);
@@ -577,3 +833,60 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
 }
 
 }  // namespace mgemm
+
+// ---------------------------------------------------------------- MX-fp8 C ABI
+extern "C" int mia_mx_quantize(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ldx, void* q,
+                               int64_t ldq, void* scales, mia_stream_t stream) {
+  MIA_CHECK_ARG(x_dtype == MIA_BF16 || x_dtype == MIA_F32, "mx_quantize: input must be bf16 or f32");
+  MIA_CHECK_ARG(rows >= 0 && cols >= 0 && cols % 32 == 0, "mx_quantize: cols must be a multiple of 32");
+  MIA_CHECK_ARG(ldx >= cols && ldq >= cols && ldq % 8 == 0 && ldx % 8 == 0, "mx_quantize: bad leading dimension");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 7) == 0,
+                "mx_quantize: x must be 16-B and q 8-B aligned");
+  if (rows == 0 || cols == 0) return 0;
+  const int64_t total = rows * (cols / 8);
+  const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 16384);
+  hipStream_t s = as_stream(stream);
+  if (x_dtype == MIA_BF16)
+    mx_quant_kernel<bf16><<<blocks, 256, 0, s>>>(reinterpret_cast<const bf16*>(x), rows, cols, ldx,
+                                                 reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(scales));
+  else
+    mx_quant_kernel<float><<<blocks, 256, 0, s>>>(reinterpret_cast<const float*>(x), rows, cols, ldx,
+                                                  reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(scales));
+  MIA_LAUNCH_CHECK("mx_quantize");
+  return 0;
+}
+
+extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales,
+                              int64_t ldb, const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, mia_stream_t stream) {
+  MIA_CHECK_ARG(a && b && a_scales && b_scales && E && E->ptr, "gemm_mxfp8: null operand");
+  MIA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mxfp8: K must be a positive multiple of 128");
+  MIA_CHECK_ARG(lda >= K && ldb >= K && lda % 16 == 0 && ldb % 16 == 0, "gemm_mxfp8: lda / ldb (bytes) must be >= K and 16-B multiples");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(a) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(a_scales) & 3) == 0 && (reinterpret_cast<uintptr_t>(b_scales) & 3) == 0,
+                "gemm_mxfp8: operands 16-B and scales 4-B aligned");
+  MIA_CHECK_ARG(N % 4 == 0 && cdiv(M, MG_BM) * cdiv(N, MG_BN) < (1ll << 24), "gemm_mxfp8: N must be a multiple of 4");
+  const int epi = mgemm::mg_epi_kind(*E, N);
+  MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_ADD_AUX,
+                "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE / f32 residual (row-major, aligned)");
+  MArgs g;
+  memset(&g, 0, sizeof(g));
+  g.a = reinterpret_cast<const bf16*>(a);
+  g.b = reinterpret_cast<const bf16*>(b);
+  g.lda = lda / 2; g.ldb = ldb / 2;  // e4m3 rows seen as bf16 pairs by the loaders
+  g.M = M; g.N = N; g.K = K; g.kper = K; g.split = 1;
+  g.nbm = (int)cdiv(M, MG_BM); g.nbn = (int)cdiv(N, MG_BN);
+  g.out = E->ptr; g.ldc = E->ldc; g.out_f32 = E->dtype == MIA_F32;
+  g.bias = E->bias; g.aux = E->aux; g.ldaux = E->ldaux;
+  g.mxq = reinterpret_cast<uint8_t*>(E->mx_q); g.mxs = reinterpret_cast<uint8_t*>(E->mx_scales);
+  MxArgs x{reinterpret_cast<const uint8_t*>(a_scales), reinterpret_cast<const uint8_t*>(b_scales)};
+  const unsigned grid = (unsigned)((int64_t)g.nbm * g.nbn);
+  hipStream_t s = as_stream(stream);
+  switch (epi) {
+    case EPI_PLAIN: mxgemm_kernel<EPI_PLAIN><<<grid, MG_NT, 0, s>>>(g, x); break;
+    case EPI_GELU: mxgemm_kernel<EPI_GELU><<<grid, MG_NT, 0, s>>>(g, x); break;
+    case EPI_GELU_SAVE: mxgemm_kernel<EPI_GELU_SAVE><<<grid, MG_NT, 0, s>>>(g, x); break;
+    default: mxgemm_kernel<EPI_ADD_AUX><<<grid, MG_NT, 0, s>>>(g, x); break;
+  }
+  MIA_LAUNCH_CHECK("gemm_mxfp8");
+  return 0;
+}

@@ -245,11 +245,15 @@ int check_bn(const void* x, int dtype, int64_t P, int C) {
 }
 
 // ---------------------------------------------------------------- LayerNorm (rows x D), one wave per row
-template <int PER>
+// MX (fp8-mixed): the bf16 output row is also written as OCP MX-fp8 (e4m3 bytes q [rows][D], E8M0
+// scales [rows][D / 32]) -- the qkv / fc1 MX GEMM's A operand without a quantisation pass.  Lane l holds
+// d = l + 64 i, so lanes 0-31 / 32-63 hold 32-blocks 2i / 2i + 1: the block amax is a 32-lane max.
+template <int PER, bool MX = false>
 __global__ __launch_bounds__(NT) void ln_fwd_kernel(const void* __restrict__ x, int xdt, const float* __restrict__ g,
                                                     const float* __restrict__ b, void* y, int ydt,
                                                     float* __restrict__ mean_o, float* __restrict__ rstd_o,
-                                                    int64_t rows, int D, float eps) {
+                                                    int64_t rows, int D, float eps, uint8_t* __restrict__ q = nullptr,
+                                                    uint8_t* __restrict__ qs = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -273,7 +277,20 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const void* __restrict__ x, 
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int d = lane + 64 * i;
-    if (d < D) st_elem(y, ydt, row * D + d, (v[i] - mean) * rstd * g[d] + b[d]);
+    if constexpr (MX) {  // D % 64 == 0 (d < D is wave-uniform), bf16 output: quantise the stored value
+      if (64 * i >= D) break;
+      const float yb = (float)(bf16)((v[i] - mean) * rstd * g[d] + b[d]);
+      reinterpret_cast<bf16*>(y)[row * D + d] = (bf16)yb;
+      float am = fabsf(yb);
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+      const int e = mx_exponent(am);
+      const float t = __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(yb, -e), -448.f, 448.f);
+      q[row * D + d] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(t, 0.f, 0, false) & 0xff);
+      if ((lane & 31) == 0) qs[row * (D >> 5) + (d >> 5)] = (uint8_t)(e + 127);
+    } else {
+      if (d < D) st_elem(y, ydt, row * D + d, (v[i] - mean) * rstd * g[d] + b[d]);
+    }
   }
   if (lane == 0) { mean_o[row] = mean; rstd_o[row] = rstd; }
 }
@@ -576,6 +593,18 @@ extern "C" int mia_layernorm_fwd(const void* x, int32_t xdtype, const float* gam
   if (D <= 768) ln_fwd_kernel<12><<<nb, NT, 0, s>>>(x, xdtype, gamma, beta, y, ydtype, mean, rstd, rows, D, eps);
   else ln_fwd_kernel<16><<<nb, NT, 0, s>>>(x, xdtype, gamma, beta, y, ydtype, mean, rstd, rows, D, eps);
   MIA_LAUNCH_CHECK("layernorm_fwd");
+  return 0;
+}
+
+extern "C" int mia_layernorm_fwd_mx(const void* x, int32_t xdtype, const float* gamma, const float* beta, void* y,
+                                    void* q, void* scales, float* mean, float* rstd, int64_t rows, int32_t D, float eps,
+                                    mia_stream_t stream) {
+  MIA_CHECK_ARG(x && gamma && beta && y && q && scales && mean && rstd, "layernorm_fwd_mx: null pointer");
+  MIA_CHECK_ARG(D > 0 && D <= 768 && D % 64 == 0, "layernorm_fwd_mx: D must be a multiple of 64, <= 768");
+  const unsigned nb = (unsigned)cdiv(rows, 4);
+  ln_fwd_kernel<12, true><<<nb, NT, 0, as_stream(stream)>>>(x, xdtype, gamma, beta, y, MIA_BF16, mean, rstd, rows, D, eps,
+                                                             reinterpret_cast<uint8_t*>(q), reinterpret_cast<uint8_t*>(scales));
+  MIA_LAUNCH_CHECK("layernorm_fwd_mx");
   return 0;
 }
 

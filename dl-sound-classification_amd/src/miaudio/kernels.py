@@ -65,11 +65,12 @@ def conv(t: torch.Tensor, layout: int, n, h, w, c, oh, ow, kh, kw, sh=1, sw=1, p
 
 def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=None, ldaux: int = 0,
              accumulate: bool = False, alpha: float = 1.0, act_scale: float = 1.0,
-             rowmap=None, sqsum=None, colsum=None) -> L.MiaEpilogue:
+             rowmap=None, sqsum=None, colsum=None, mx=None) -> L.MiaEpilogue:
     """Output descriptor of a GEMM.  ``sqsum``: optional f64 tensor of ``mia_gemm_sqsum_slots(M, N)``
     entries that receives the per-tile sums of squares of a plain f32 output (see ``sqsum_slots``).
     ``colsum``: optional f32 (N,) tensor receiving the column sums of the stored output (the bias
-    gradient of the linear whose dy this output is)."""
+    gradient of the linear whose dy this output is).  ``mx``: optional MXTensor (mx_empty) receiving an
+    MX-fp8 copy of a bf16 output (256x256 kernels only)."""
     e = L.MiaEpilogue()
     e.ptr = out.data_ptr()
     e.dtype = L.dtype_code(out)
@@ -87,7 +88,9 @@ def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=
     e.act_scale = act_scale
     e.sqsum = L.ptr(sqsum)
     e.colsum = L.ptr(colsum)
-    e._keep = (out, bias, aux, sqsum, colsum)
+    if mx is not None:  # MXTensor receiving the MX-fp8 copy of the bf16 output
+        e.mx_q, e.mx_scales = mx.q.data_ptr(), mx.scales.data_ptr()
+    e._keep = (out, bias, aux, sqsum, colsum, mx)
     return e
 
 
@@ -580,3 +583,50 @@ def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     L.check(L.load().mia_cast(src.data_ptr(), L.dtype_code(src), out.data_ptr(), L.dtype_code(out), src.numel(),
                               _s()), "mia_cast")
     return out
+
+
+# ------------------------------------------------------------------------------------ MX-fp8
+class MXTensor:
+    """An MX-fp8 operand: e4m3 bytes ``q`` [rows][cols] (torch.uint8) and E8M0 scales [rows][cols / 32]."""
+
+    def __init__(self, q: torch.Tensor, scales: torch.Tensor):
+        self.q, self.scales = q, scales
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+
+def mx_empty(rows: int, cols: int, device) -> MXTensor:
+    return MXTensor(torch.empty(rows, cols, dtype=torch.uint8, device=device),
+                    torch.empty(rows, cols // 32, dtype=torch.uint8, device=device))
+
+
+def mx_quantize(x: torch.Tensor) -> MXTensor:
+    """OCP MX-fp8 quantisation of a row-major [rows][cols] bf16/f32 tensor (mia_mx_quantize)."""
+    if not x.is_cuda:
+        raise RuntimeError("mx_quantize runs on the MI355X HIP kernels only (input is on CPU)")
+    x = x.contiguous()
+    rows, cols = x.shape
+    q = torch.empty(rows, cols, dtype=torch.uint8, device=x.device)
+    sc = torch.empty(rows, cols // 32, dtype=torch.uint8, device=x.device)
+    L.check(L.load().mia_mx_quantize(x.data_ptr(), L.dtype_code(x), rows, cols, cols, q.data_ptr(), cols,
+                                     sc.data_ptr(), _s()), "mia_mx_quantize")
+    return MXTensor(q, sc)
+
+
+def gemm_mxfp8(a: MXTensor, b: MXTensor, E: L.MiaEpilogue, tag: str | None = None):
+    """C = epilogue(A B^T) on MX-fp8 operands A [M][K], B [N][K] (mia_gemm_mxfp8)."""
+    M, K = a.q.shape
+    N = b.q.shape[0]
+    rec = PROBE is not None and tag in PROBE
+    if rec:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    L.check(L.load().mia_gemm_mxfp8(a.q.data_ptr(), a.scales.data_ptr(), a.q.stride(0), b.q.data_ptr(),
+                                    b.scales.data_ptr(), b.q.stride(0), E, M, N, K, _s()), "mia_gemm_mxfp8")
+    if rec:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        nb = (M + N) * K * (1 + 1 / 32) + M * N * (4 if E.dtype == L.F32 else 2)
+        PROBE[tag].append((e0, e1, 2 * M * N * K, nb))

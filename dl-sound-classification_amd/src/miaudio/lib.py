@@ -16,6 +16,9 @@ PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("MIAUDIO_LIB", PKG_ROOT / "lib" / "libmiaudio.so"))
 
 F32, BF16, U8 = 0, 1, 2
+# model compute mode (not a tensor dtype): bf16 compute with the AST block linears' forward GEMMs on MX-fp8
+# operands (trainer.precision=fp8-mixed)
+MXFP8 = 16
 OP_DENSE, OP_CONV, OP_CONVROW = 0, 1, 2
 KC, RC = 0, 1
 PRE_NONE, PRE_AFFINE, PRE_AFFINE_RELU, PRE_GELU = 0, 1, 2, 3
@@ -40,7 +43,8 @@ class MiaEpilogue(C.Structure):
     _fields_ = [("ptr", vp), ("dtype", i32), ("act", i32), ("accumulate", i32), ("aux_dtype", i32),
                 ("ldc", i64), ("rm_inner", i64), ("rm_outer", i64), ("rm_istride", i64),
                 ("rm_offset", i64), ("bias", vp), ("aux", vp), ("ldaux", i64),
-                ("alpha", f32), ("act_scale", f32), ("sqsum", vp), ("colsum", vp)]
+                ("alpha", f32), ("act_scale", f32), ("sqsum", vp), ("colsum", vp), ("mx_q", vp),
+                ("mx_scales", vp)]
 
 
 class MiaMelCfg(C.Structure):
@@ -57,6 +61,10 @@ SIGNATURES = {
     "mia_gemm_sqsum_slots": (i64, [i64, i64]),
     "mia_gemm": (C.c_int, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32, vp, vp]),
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
+    "mia_mx_quantize": (C.c_int, [vp, i32, i64, i64, i64, vp, i64, vp, vp]),
+    "mia_gemm_mxfp8": (C.c_int, [vp, vp, i64, vp, vp, i64, P(MiaEpilogue), i64, i64, i64, vp]),
+    "mia_layernorm_fwd_mx": (C.c_int, [vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
+    "mia_attn_fwd_mx": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_splitk_reduce": (C.c_int, [vp, i32, i64, i64, P(MiaEpilogue), vp]),
     "mia_logmel_workspace_bytes": (i64, [i64, i64]),
     "mia_logmel_fwd": (C.c_int, [vp, i64, i64, i64, P(MiaMelCfg), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

@@ -130,7 +130,8 @@ class ASTModel(nn.Module):
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 return L.BF16
             return L.F32
-        return {"bf16": L.BF16, "bfloat16": L.BF16, "f32": L.F32, "fp32": L.F32, "32": L.F32}[str(cd)]
+        return {"bf16": L.BF16, "bfloat16": L.BF16, "f32": L.F32, "fp32": L.F32, "32": L.F32,
+                "fp8": L.MXFP8}[str(cd)]
 
     def param_list(self):
         ps = [self.patch_embed.weight, self.patch_embed.bias, self.cls_token, self.pos_embed]

@@ -20,14 +20,21 @@ from ..miaudio import lib as L
 EPS = 1e-6
 
 
-def _ln(x, g, b, out_dtype, rows, D):
+def _ln(x, g, b, out_dtype, rows, D, mx: bool = False):
+    """LayerNorm forward -> (y, mean, rstd[, MX-fp8 copy of y when mx: mia_layernorm_fwd_mx])."""
     y = torch.empty(rows, D, dtype=out_dtype, device=x.device)
     mean = torch.empty(rows, dtype=torch.float32, device=x.device)
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    if mx:
+        yq = K.mx_empty(rows, D, x.device)
+        L.check(L.load().mia_layernorm_fwd_mx(x.data_ptr(), L.dtype_code(x), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                              yq.q.data_ptr(), yq.scales.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                              rows, D, EPS, L.stream_ptr()), "mia_layernorm_fwd_mx")
+        return y, mean, rstd, yq
     L.check(L.load().mia_layernorm_fwd(x.data_ptr(), L.dtype_code(x), g.data_ptr(), b.data_ptr(), y.data_ptr(),
                                        L.dtype_code(y), mean.data_ptr(), rstd.data_ptr(), rows, D, EPS, L.stream_ptr()),
             "mia_layernorm_fwd")
-    return y, mean, rstd
+    return y, mean, rstd, None
 
 
 def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool, dx2=None):
@@ -88,7 +95,8 @@ class ASTFunction(torch.autograd.Function):
     def forward(ctx, model, spec, compute: int, *params):
         if not spec.is_cuda:
             raise RuntimeError("ASTModel runs on the MI355X HIP kernels only (input is on CPU)")
-        cd = compute
+        mx = compute == L.MXFP8  # fp8-mixed: block linears' forward GEMMs on MX-fp8 operands
+        cd = L.BF16 if mx else compute
         tdt = L.torch_dtype(cd)
         dev = spec.device
         B, Fm, Tf = spec.shape
@@ -116,32 +124,51 @@ class ASTFunction(torch.autograd.Function):
         wcast = []
         for i in range(nb):
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = params[4 + 12 * i: 16 + 12 * i]
+            wmx = [K.mx_quantize(w) for w in (wqkv, wproj, w1, w2)] if mx else None  # from the f32 masters
             if cd == L.BF16:
                 wqkv, wproj, w1, w2 = (K.bf16_shadow(w) for w in (wqkv, wproj, w1, w2))
             wcast.append((wqkv, wproj, w1, w2))
-            h, m1, r1 = _ln(x, g1, b1, tdt, Tt, D)
+
+            def lin(xin, xq, wi, W, bias, out, tag, **kw):
+                """x W^T + bias (+ epilogue); fp8-mixed: on the MX copy xq the producer wrote beside the
+                bf16 activation (which the backward keeps using)."""
+                if mx:
+                    K.gemm_mxfp8(xq, wmx[wi], K.epilogue(out, W.shape[0], bias=bias, ldaux=W.shape[0], **kw), tag=tag)
+                else:
+                    kw.pop("mx", None)
+                    _linear(xin, W, bias, out, Tt, cd, tag=tag, **kw)
+
+            h, m1, r1, hq = _ln(x, g1, b1, tdt, Tt, D, mx=mx)
             qkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
-            _linear(h, wqkv, bqkv, qkv, Tt, cd, tag="qkv.fwd")
+            lin(h, hq, 0, wqkv, bqkv, qkv, "qkv.fwd")
             a = torch.empty(Tt, D, dtype=tdt, device=dev)
+            aq = K.mx_empty(Tt, D, dev) if mx else None
             lse = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
             with K.probe("attn.fwd", 4.0 * B * Hh * N * N * (D // Hh), (qkv.numel() + a.numel()) * qkv.element_size()):
-                L.check(L.load().mia_attn_fwd(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(), cd, B, N, Hh, scale,
-                                              L.stream_ptr()), "mia_attn_fwd")
+                if mx:
+                    L.check(L.load().mia_attn_fwd_mx(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(), aq.q.data_ptr(),
+                                                     aq.scales.data_ptr(), B, N, Hh, scale, L.stream_ptr()),
+                            "mia_attn_fwd_mx")
+                else:
+                    L.check(L.load().mia_attn_fwd(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(), cd, B, N, Hh, scale,
+                                                  L.stream_ptr()), "mia_attn_fwd")
             xm = torch.empty(Tt, D, dtype=torch.float32, device=dev)
-            _linear(a, wproj, bproj, xm, Tt, cd, act=L.ACT_ADD_AUX, aux=x, tag="proj.fwd")
-            h2, m2, r2 = _ln(xm, g2, b2, tdt, Tt, D)
+            lin(a, aq, 1, wproj, bproj, xm, "proj.fwd", act=L.ACT_ADD_AUX, aux=x)
+            h2, m2, r2, h2q = _ln(xm, g2, b2, tdt, Tt, D, mx=mx)
             u = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)   # fc1 pre-activation
             gu = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)  # gelu(u)
-            _linear(h2, w1, bb1, gu, Tt, cd, act=L.ACT_GELU_SAVE, aux=u, tag="fc1.fwd")
+            guq = K.mx_empty(Tt, w1.shape[0], dev) if mx else None
+            lin(h2, h2q, 2, w1, bb1, gu, "fc1.fwd", act=L.ACT_GELU_SAVE, aux=u, mx=guq)
             xo = torch.empty(Tt, D, dtype=torch.float32, device=dev)
-            _linear(gu, w2, bb2, xo, Tt, cd, act=L.ACT_ADD_AUX, aux=xm, tag="fc2.fwd")
+            lin(gu, guq, 3, w2, bb2, xo, "fc2.fwd", act=L.ACT_ADD_AUX, aux=xm)
+            del hq, aq, h2q, guq
             saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u,
                                      gu=gu))
             x = xo
         # final norm only matters for the CLS rows (ast.py:62-63 takes x[:, 0])
         gn, bn_, wh, bh = params[4 + 12 * nb: 8 + 12 * nb]
         xc = x.view(B, N, D)[:, 0].contiguous()
-        hc, mc, rc = _ln(xc, gn, bn_, torch.float32, B, D)
+        hc, mc, rc, _ = _ln(xc, gn, bn_, torch.float32, B, D)
         z = torch.empty(B, wh.shape[0], dtype=torch.float32, device=dev)
         _linear(hc, wh, bh, z, B, cd, tag="head.fwd")
         probs = torch.sigmoid(z)

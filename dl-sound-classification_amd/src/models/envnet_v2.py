@@ -70,7 +70,8 @@ class EnvNetV2(nn.Module):
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 return L.BF16
             return L.F32
-        return {"bf16": L.BF16, "bfloat16": L.BF16, "f32": L.F32, "fp32": L.F32, "32": L.F32}[str(cd)]
+        # fp8-mixed: EnvNet-v2 has no fp8 path (north_star config 5 names the AST linears); it runs bf16
+        return {"bf16": L.BF16, "bfloat16": L.BF16, "f32": L.F32, "fp32": L.F32, "32": L.F32, "fp8": L.BF16}[str(cd)]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.ndim == 3:

@@ -9,7 +9,8 @@ Data parallelism: with ``devices > 1`` the script is launched one process per GP
 (torch.distributed.run); the trainer joins the RCCL process group, shards the clips across ranks
 (DistributedSampler semantics) and exchanges gradients with ``GradAllReducer`` (ddp.py).
 Precision: "32" -> f32 kernels; "bf16-mixed" -> bf16 MFMA compute with f32 master weights, f32
-gradients and f32 Adam state (Lightning bf16-mixed semantics).
+gradients and f32 Adam state (Lightning bf16-mixed semantics); "fp8-mixed" -> the same, with the AST block
+linears' forward GEMMs on MX-fp8 operands (north_star config 5; EnvNet-v2 runs bf16).
 """
 from __future__ import annotations
 
@@ -199,11 +200,14 @@ class Trainer:
             return "f32"
         if p in ("bf16", "bf16-mixed", "bf16-true"):
             return "bf16"
+        if p in ("fp8", "fp8-mixed", "transformer-engine"):
+            # north_star config 5: AST block linears forward on MX-fp8 operands, everything else bf16
+            return "fp8"
         if p in ("16", "16-mixed", "16-true"):
             print(f"[lite] precision={precision!r}: fp16 runs as bf16 compute (f32 master weights, no loss "
                   "scaling needed) on the MI355X kernels", flush=True)
             return "bf16"
-        raise ValueError(f"unsupported trainer.precision {precision!r} (use 32, bf16-mixed or 16-mixed)")
+        raise ValueError(f"unsupported trainer.precision {precision!r} (use 32, bf16-mixed, 16-mixed or fp8-mixed)")
 
     def broadcast_object(self, obj):
         if self.world <= 1:

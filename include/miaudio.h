@@ -83,6 +83,12 @@ typedef struct MiaEpilogue {
    * fc2 dgrad); any other path gets a column-sum pass over the output.  Row-major output, no
    * accumulate / row map / sqsum.  Needs the workspace of mia_gemm_workspace_bytes_ex. */
   float* colsum;
+  /* Optional (NULL = off): an MX-fp8 copy of the stored bf16 output -- mx_q e4m3 [M][N] (row stride N
+   * bytes), mx_scales [M][N / 32] E8M0 (mia_mx_quantize's format, of the rounded bf16 values) -- the next
+   * MX GEMM's A operand, written in the same epilogue (fp8-mixed: fc1's gelu(u) for fc2).  256x256
+   * kernels (path 7, mia_gemm_mxfp8) with a plain / GELU / GELU_SAVE bf16 output, ldc == N, N % 32 == 0. */
+  void* mx_q;
+  void* mx_scales;
 } MiaEpilogue;
 
 /* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16 / 16x16x32; f32: v_mfma_f32_32x32x2_f32).
@@ -94,6 +100,33 @@ typedef struct MiaEpilogue {
  * Workspace: mia_gemm_workspace_bytes_ex(...) bytes for exactly this call (split-K slabs, column-sum
  * partials); mia_gemm_workspace_bytes(M, N, split_k) is the split-K part alone of paths 0-5. */
 int64_t mia_gemm_workspace_bytes(int64_t M, int64_t N, int32_t split_k);
+/* MX-fp8 (OCP e4m3fn elements, one E8M0 scale byte per 32 consecutive K-elements) for the AST block
+ * linears' forward GEMMs under trainer.precision=fp8-mixed (north_star config 5; the reference has no fp8
+ * path: it replaces the bf16 nn.Linear of timm's Block, ast.py:38,60-61, inside autocast).
+ * mia_mx_quantize: x [rows][cols] (bf16 or f32, row stride ldx elements, cols % 32 == 0) -> q [rows][cols]
+ * e4m3 bytes (row stride ldq bytes) and scales [rows][cols / 32] bytes.  OCP MX rule: e = floor(log2(amax
+ * of the 32-block)) - 8, clamped to [-127, 127], scale byte e + 127; elements x * 2^-e saturated to +-448
+ * and rounded to nearest even; an all-zero block gets scale byte 0.
+ * mia_gemm_mxfp8: C[M][N] = epilogue(A[M][K] B[N][K]^T) with A, B e4m3 (row strides lda / ldb bytes,
+ * multiples of 16, K % 128 == 0) and their scale arrays ([M][K/32], [N][K/32] bytes, 4-B aligned); the
+ * epilogue is mia_gemm's dense one restricted to plain / bias / GELU / GELU_SAVE (bf16 out) and the f32
+ * residual add (MIA_ACT_ADD_AUX); f32 accumulation; no workspace, no host sync. */
+int mia_mx_quantize(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ldx, void* q, int64_t ldq,
+                    void* scales, mia_stream_t stream);
+int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales, int64_t ldb,
+                   const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, mia_stream_t stream);
+/* Quantise-on-store producers of the fp8-mixed AST forward (the MX GEMMs' A operands without a
+ * separate pass; both also write their usual bf16 output, which the backward keeps using):
+ * mia_layernorm_fwd_mx: mia_layernorm_fwd with a bf16 y plus q [rows][D] e4m3 and scales [rows][D/32]
+ *   (D % 64 == 0, D <= 768) -- timm Block norm1 / norm2 feeding qkv / fc1;
+ * mia_attn_fwd_mx: mia_attn_fwd (bf16) plus the output as q8 [B*N][H*64] e4m3 and s8 [B*N][H*2] --
+ *   feeding proj.  Both quantise the rounded bf16 values exactly as mia_mx_quantize would. */
+int mia_layernorm_fwd_mx(const void* x, int32_t xdtype, const float* gamma, const float* beta, void* y, void* q,
+                         void* scales, float* mean, float* rstd, int64_t rows, int32_t D, float eps,
+                         mia_stream_t stream);
+int mia_attn_fwd_mx(const void* qkv, void* out, float* lse, void* q8, void* s8, int32_t B, int32_t N, int32_t H,
+                    float scale, mia_stream_t stream);
+
 int64_t mia_gemm_workspace_bytes_ex(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
                                     int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k);
 /* number of MiaEpilogue.sqsum slots (doubles) of an M x N output */

@@ -111,22 +111,23 @@ def model_params(deit_state, head_w, head_b, depth: int = DEPTH):
     return p
 
 
-def block(p, pre, x):
+def block(p, pre, x, lin=F.linear):
+    """timm Block; ``lin`` replaces the four block linears (tests: an MX-fp8 emulation for fp8-mixed)."""
     B, N, C = x.shape
     h = F.layer_norm(x, (C,), p[pre + "norm1.weight"], p[pre + "norm1.bias"], 1e-6)
-    qkv = F.linear(h, p[pre + "attn.qkv.weight"], p[pre + "attn.qkv.bias"])
+    qkv = lin(h, p[pre + "attn.qkv.weight"], p[pre + "attn.qkv.bias"])
     qkv = qkv.reshape(B, N, 3, HEADS, C // HEADS).permute(2, 0, 3, 1, 4)
     q, k, v = qkv.unbind(0)
     scale = (C // HEADS) ** -0.5
     a = torch.softmax((q * scale) @ k.transpose(-2, -1), dim=-1) @ v
     a = a.transpose(1, 2).reshape(B, N, C)
-    x = x + F.linear(a, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])
+    x = x + lin(a, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])
     h = F.layer_norm(x, (C,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], 1e-6)
-    h = F.gelu(F.linear(h, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"]))
-    return x + F.linear(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    h = F.gelu(lin(h, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"]))
+    return x + lin(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
 
 
-def forward(p, x, depth: int = DEPTH, return_logits: bool = False):
+def forward(p, x, depth: int = DEPTH, return_logits: bool = False, lin=F.linear):
     """ASTModel.forward (ast.py:50-63). x: (B, 128, F) or (B, 1, 128, F)."""
     if x.dim() == 3:
         x = x.unsqueeze(1)
@@ -136,7 +137,7 @@ def forward(p, x, depth: int = DEPTH, return_logits: bool = False):
     x = torch.cat((cls, x), dim=1)
     x = x + p["pos_embed"][:, :x.size(1)]
     for i in range(depth):
-        x = block(p, f"transformer.{i}.", x)
+        x = block(p, f"transformer.{i}.", x, lin)
     x = F.layer_norm(x, (x.shape[-1],), p["norm.weight"], p["norm.bias"], 1e-6)
     z = F.linear(x[:, 0], p["head.weight"], p["head.bias"])
     return z if return_logits else torch.sigmoid(z)

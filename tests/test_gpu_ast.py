@@ -126,7 +126,7 @@ def test_layernorm(cuda, D):
     dy = torch.randn(300, D, generator=g)
     y.backward(dy.double())
     tx, tw, tb = x.to(cuda), w.to(cuda), b.to(cuda)
-    yo, m, r = _ln(tx, tw, tb, torch.float32, 300, D)
+    yo, m, r, _ = _ln(tx, tw, tb, torch.float32, 300, D)
     dx = torch.ones(300, D, device=cuda)
     dg, db, cs = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx, 300, D, True)
     torch.cuda.synchronize()
@@ -149,7 +149,7 @@ def test_layernorm_bwd_colsum(cuda, rows):
     b = torch.randn(D, generator=g, device=cuda)
     dy = torch.randn(rows, D, generator=g, device=cuda).to(torch.bfloat16)
     acc0 = torch.randn(rows, D, generator=g, device=cuda)
-    _, m, r = _ln(x, w, b, torch.bfloat16, rows, D)
+    _, m, r, _ = _ln(x, w, b, torch.bfloat16, rows, D)
     dxa, dxb = acc0.clone(), acc0.clone()
     d2a = torch.empty(rows, D, dtype=torch.bfloat16, device=cuda)
     d2b = torch.empty_like(d2a)

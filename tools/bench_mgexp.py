@@ -1,8 +1,10 @@
-"""A/B timing of the GEMM epilogue / scheduling variants of tools/probe/libmgexp.so (an experiment
-copy of csrc/mgemm.hip with run-time flags) on the AST shapes, interleaved rounds in one process;
-each variant's output is checked against the product kernel's (mia_gemm) bit for bit.
-    make -C tools/probe && TOKENS=421120 python tools/bench_mgexp.py "0,1,2,3,9" [shape ...]
-flags: 1 no start stagger, 2 LDS-staged bf16 epilogue, 4 no epilogue traffic, 8 paired 16-B bf16 stores."""
+"""A/B timing of an experiment GEMM library in tools/probe (default libmgexp.so, entry points
+mgexp_gemm / mgexp_workspace_bytes; MGLIB=libmg2.so MGSYM=mg2 for the 2-workgroups-per-CU variant)
+against the product kernel (mia_gemm, variant "p") on the AST shapes, interleaved rounds in one process;
+each variant's output is checked against mia_gemm's (bit for bit, or the max relative difference when the
+K split differs).
+    make -C tools/probe && TOKENS=421120 python tools/bench_mgexp.py "p,0,1" [shape ...]
+mgexp flags: 1 no start stagger, 2 LDS-staged bf16 epilogue, 4 no epilogue traffic, 8 paired 16-B bf16 stores."""
 import ctypes as C
 import os
 import sys
@@ -21,14 +23,17 @@ from bench_gemm import SHAPES  # noqa: E402
 T = int(os.environ.get("TOKENS", 421120))
 REPS = int(os.environ.get("REPS", 5))
 ROUNDS = int(os.environ.get("ROUNDS", 3))
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1").split(",")]
+variants = [v if v == "p" else int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "p,0").split(",")]
 want = set(sys.argv[2:])
-X = C.CDLL(str(REPO / "tools" / "probe" / "libmgexp.so"))
+X = C.CDLL(str(REPO / "tools" / "probe" / os.environ.get("MGLIB", "libmgexp.so")))
+SYM = os.environ.get("MGSYM", "mgexp")
 P = C.POINTER
-X.mgexp_gemm.argtypes = [C.c_int, P(L.MiaOperand), P(L.MiaOperand), P(L.MiaEpilogue), C.c_int64, C.c_int64,
-                         C.c_int64, C.c_void_p, C.c_void_p]
-X.mgexp_workspace_bytes.restype = C.c_int64
-X.mgexp_workspace_bytes.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int]
+XG = getattr(X, SYM + "_gemm")
+XW = getattr(X, SYM + "_workspace_bytes")
+XG.argtypes = [C.c_int, P(L.MiaOperand), P(L.MiaOperand), P(L.MiaEpilogue), C.c_int64, C.c_int64, C.c_int64,
+               C.c_void_p, C.c_void_p]
+XW.restype = C.c_int64
+XW.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int]
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 for name, M, N, Kd, la, lb, epi in SHAPES:
@@ -56,22 +61,25 @@ for name, M, N, Kd, la, lb, epi in SHAPES:
     K.gemm(A, Bo, K.epilogue(ref, N, **extra), M, N, Kd, L.BF16)
     out = torch.empty(M, N, dtype=odt, device=dev)
     E = K.epilogue(out, N, **extra)
-    ws = torch.empty(max(256, X.mgexp_workspace_bytes(M, N, Kd, 1 if epi == "dgelu" else 0)), dtype=torch.uint8,
+    ws = torch.empty(max(256, XW(M, N, Kd, 1 if epi == "dgelu" else 0)), dtype=torch.uint8,
                      device=dev)
     st = torch.cuda.current_stream().cuda_stream
 
     def run(f):
-        rc = X.mgexp_gemm(f, A, Bo, E, M, N, Kd, ws.data_ptr(), st)
+        if f == "p":
+            K.gemm(A, Bo, E, M, N, Kd, L.BF16)
+            return
+        rc = XG(f, A, Bo, E, M, N, Kd, ws.data_ptr(), st)
         assert rc == 0, rc
 
     times = {f: [] for f in variants}
     for f in variants:
         run(f)
         torch.cuda.synchronize()
-        if not f & 4:
-            same = torch.equal(out, ref)
-            if not same:
-                print(f"  variant {f}: output differs from mia_gemm (max {float((out.float() - ref.float()).abs().max())})")
+        if f == "p" or not f & 4:
+            if not torch.equal(out, ref):
+                d = float((out.float() - ref.float()).abs().max() / ref.float().abs().max())
+                print(f"  variant {f}: output differs from mia_gemm (max rel {d:.3e})")
     for _ in range(ROUNDS):
         for f in variants:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

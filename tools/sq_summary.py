@@ -1,33 +1,100 @@
-"""Per-kernel SQ counter summary of a tools/attn_pmc.sh output directory: python tools/sq_summary.py gpurun_out/<tag>"""
+"""Per-kernel SQ counter summary of one tools/profile.sh 'sq' pass (or the older tools/attn_pmc.sh a/b
+directories).
+
+    python tools/sq_summary.py gpurun_out/prof_<tag> [profiles/r03_sq_<tag>.json] [marker]
+
+MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe busy cycles summed over every SIMD
+(MI355X_MICROARCH.md, constants table: 32 per v_mfma_f32_32x32x16_bf16), so
+util = MFMA_BUSY / (1024 SIMDs x duration x clock); the duration is the kernel-trace pass's (undisturbed
+by counter collection), and the clock is the one the counter run itself held, estimated as
+SQ_BUSY_CU_CYCLES x 4 (quad-cycles) / 256 CUs / its own duration.  SQ_WAVE_CYCLES / SQ_WAIT_* /
+SQ_ACTIVE_INST_* count quad-cycles per wave; they are reported as fractions of SQ_WAVE_CYCLES.
+Only the launches of the last complete step (marker: the Adam kernel) are used.
+"""
+from __future__ import annotations
+
 import collections
 import csv
+import json
 import re
 import sys
 from pathlib import Path
 
-res = collections.defaultdict(dict)
-for sub in ("a", "b"):
-    p = Path(sys.argv[1]) / sub / "run_counter_collection.csv"
-    if not p.exists():
-        continue
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in csv.DictReader(open(p)):
-        m = re.search(r"(\w+_kernel)", r["Kernel_Name"])
-        agg[m.group(1) if m else r["Kernel_Name"][:40]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for k, v in agg.items():
-        for c, x in v.items():
-            res[k][c] = sum(x) / len(x)
-for k, v in res.items():
-    wc = v.get("SQ_WAVE_CYCLES") or 1
-    line = [k]
-    for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
-        if c in v:
-            line.append(f"{c[3:]}={v[c] / wc:.3f}")
-    if v.get("SQ_INSTS_MFMA"):
-        line.append(f"valu/mfma={v['SQ_INSTS_VALU'] / v['SQ_INSTS_MFMA']:.2f} lds/mfma={v['SQ_INSTS_LDS'] / v['SQ_INSTS_MFMA']:.2f} "
-                    f"salu/mfma={v['SQ_INSTS_SALU'] / v['SQ_INSTS_MFMA']:.2f}")
-    if "SQ_LDS_BANK_CONFLICT" in v and v.get("SQ_ACTIVE_INST_LDS"):
-        line.append(f"bankconf/lds_active={v['SQ_LDS_BANK_CONFLICT'] / v['SQ_ACTIVE_INST_LDS']:.2f}")
-    if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
-        line.append(f"mfma_busy={v['SQ_VALU_MFMA_BUSY_CYCLES']:.3e}")
-    print("  ".join(line))
+NSIMD, NCU = 1024, 256
+
+
+def short(name: str) -> str:
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
+    return n[-60:]
+
+
+def last_step(rows, marker):
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows if marker in r["Kernel_Name"]})
+    if len(ids) < 2:
+        return rows
+    lo, hi = ids[-2], ids[-1]
+    return [r for r in rows if lo < int(r["Dispatch_Id"]) <= hi]
+
+
+def main():
+    root = Path(sys.argv[1])
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    marker = sys.argv[3] if len(sys.argv) > 3 else "adam_kernel"
+    res = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur_pmc = collections.defaultdict(float)
+    launches = collections.Counter()
+    for sub in ("sq", "a", "b"):
+        p = root / sub / "run_counter_collection.csv"
+        if not p.exists():
+            continue
+        rows = last_step(list(csv.DictReader(open(p))), marker)
+        seen = set()
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            res[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            d = r["Dispatch_Id"]
+            if (sub, d) not in seen:
+                seen.add((sub, d))
+                if sub in ("sq", "a"):
+                    dur_pmc[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+                    launches[k] += 1
+    # undisturbed durations from the kernel-trace pass
+    dur = collections.defaultdict(float)
+    tp = root / "trace" / "run_kernel_trace.csv"
+    if tp.exists():
+        rows = list(csv.DictReader(open(tp)))
+        idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+        if len(idx) >= 2:
+            rows = rows[idx[-2] + 1: idx[-1] + 1]
+        for r in rows:
+            dur[short(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    table = {}
+    for k, v in sorted(res.items(), key=lambda kv: -dur_pmc.get(kv[0], 0.0)):
+        wc = v.get("SQ_WAVE_CYCLES") or 1.0
+        row = {"launches": launches[k], "ms_pmc_run": round(dur_pmc[k] * 1e3, 4)}
+        if dur.get(k):
+            row["ms_trace"] = round(dur[k] * 1e3, 4)
+        if v.get("SQ_BUSY_CU_CYCLES") and dur_pmc[k] > 0:
+            clk = v["SQ_BUSY_CU_CYCLES"] * 4 / NCU / dur_pmc[k]
+            row["clock_ghz_pmc_run"] = round(clk / 1e9, 3)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
+                row["mfma_util"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * dur_pmc[k] * clk), 4)
+                row["mfma_util_at_2.4GHz_trace"] = (round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * dur[k] * 2.4e9), 4)
+                                                   if dur.get(k) else None)
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+            if c in v:
+                row[c[3:].lower() + "_frac"] = round(v[c] / wc, 4)
+        if v.get("SQ_ACTIVE_INST_LDS"):
+            row["lds_bank_conflict_per_lds_active"] = round(v.get("SQ_LDS_BANK_CONFLICT", 0.0) / v["SQ_ACTIVE_INST_LDS"], 4)
+        if v.get("SQ_INSTS_MFMA"):
+            row["valu_per_mfma"] = round(v.get("SQ_INSTS_VALU", 0) / v["SQ_INSTS_MFMA"], 3)
+            row["lds_per_mfma"] = round(v.get("SQ_INSTS_LDS", 0) / v["SQ_INSTS_MFMA"], 3)
+        table[k] = row
+    for k, row in list(table.items())[:30]:
+        print(f"{k:60s} " + " ".join(f"{a}={b}" for a, b in row.items()))
+    if out:
+        Path(out).write_text(json.dumps({"source": str(root), "marker": marker, "kernels": table}, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
