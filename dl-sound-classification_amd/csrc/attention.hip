@@ -175,6 +175,38 @@ __device__ __forceinline__ int xcd_work_item(int L, int total) {
   return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
 }
 
+// Tiles s0 .. ntiles - 1 of a 3-slot LDS ring (K/V or Q/dO tiles arrive by LDS-DMA two tiles ahead of
+// their use), slot = tile % 3 as a compile-time constant (tile s0's slot is S0 % 3, so every LDS address
+// is base + immediate); the last tile is the TAIL form when `tail`.  body(tail_t, slot_t, j).
+template <int S0, class Body>
+__device__ __forceinline__ void ring3(int s0, int ntiles, bool tail, Body&& body) {
+  using T = std::true_type;
+  using F = std::false_type;
+  using C0 = std::integral_constant<int, S0 % 3>;
+  using C1 = std::integral_constant<int, (S0 + 1) % 3>;
+  using C2 = std::integral_constant<int, (S0 + 2) % 3>;
+  int j = s0;
+  for (; j + 3 < ntiles; j += 3) {
+    body(F{}, C0{}, j);
+    body(F{}, C1{}, j + 1);
+    body(F{}, C2{}, j + 2);
+  }
+  const int r = ntiles - j;
+  if (r == 1) {
+    if (tail) body(T{}, C0{}, j);
+    else body(F{}, C0{}, j);
+  } else if (r == 2) {
+    body(F{}, C0{}, j);
+    if (tail) body(T{}, C1{}, j + 1);
+    else body(F{}, C1{}, j + 1);
+  } else if (r == 3) {
+    body(F{}, C0{}, j);
+    body(F{}, C1{}, j + 1);
+    if (tail) body(T{}, C2{}, j + 2);
+    else body(F{}, C2{}, j + 2);
+  }
+}
+
 // Forward structure (the loop is vector-issue bound at head dim 64, so the design is a VALU diet):
 //  * one wave = 32 queries (query on the lane), 4 waves = 128 queries per block, <= 168 registers so
 //    three waves share each SIMD and one wave's softmax issues beside the others' MFMAs;
@@ -306,8 +338,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
                                                           float* __restrict__ lse, int N, int H, int nqb,
                                                           float scale_log2, uint8_t* __restrict__ q8,
                                                           uint8_t* __restrict__ s8) {
-  __shared__ __attribute__((aligned(1024))) bf16 Ks[2][64 * 64];
-  __shared__ __attribute__((aligned(1024))) bf16 Vs[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Ks[3][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Vs[3][64 * 64];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
@@ -330,6 +362,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
   }
+  if (ntiles > 1) {
+    kdma.issue(Ks[1], tile_bytes, wave);
+    vdma.issue(Vs[1], tile_bytes, wave);
+  }
   bf16x8 one;
 #pragma unroll
   for (int j = 0; j < 8; ++j) one[j] = (bf16)0.f;
@@ -341,24 +377,27 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
   a.mrow[0] = (bf16)0.f;
   f32x16 s[2];
   bf16x8 pf[4];
-  // one tile; P = buffer parity (compile-time, so every LDS address is base + immediate)
-  auto tile = [&](auto first, auto tail, auto par, int j) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;
-    if (j + 1 < ntiles) {  // next tile's DMA flies under this tile's work
-      kdma.issue(Ks[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
-      vdma.issue(Vs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+  // one tile in slot P of the 3-slot ring: tile j + 2's DMA flies under this tile's work and tile j + 1's
+  auto tile = [&](auto first, auto tail, auto slot, int j) __attribute__((always_inline)) {
+    constexpr int P = decltype(slot)::value;
+    constexpr int PN = (P + 2) % 3;
+    const bool ahead = j + 2 < ntiles;
+    if (ahead) {
+      kdma.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
+      vdma.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
     }
     fwd_qk(s, Ks[P], qf, one, a.mrow, lane);
     fwd_softmax<decltype(first)::value, decltype(tail)::value>(s, a, pf, j * 64, N, lane);
     fwd_pv(a, Vs[P], pf, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j + 1's pieces have landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
   using T = std::true_type;
   using F = std::false_type;
   using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 and the Q fragments
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const bool tail = (ntiles * 64 != N);
   if (ntiles == 1) {
@@ -366,19 +405,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     else tile(T{}, F{}, P0{}, 0);
   } else {
     tile(T{}, F{}, P0{}, 0);
-    int j = 1;
-    for (; j + 2 < ntiles; j += 2) {
-      tile(F{}, F{}, P1{}, j);
-      tile(F{}, F{}, P0{}, j + 1);
-    }
-    if (j + 1 < ntiles) {  // tiles j (odd) and j + 1 = last remain
-      tile(F{}, F{}, P1{}, j);
-      if (tail) tile(F{}, T{}, P0{}, j + 1);
-      else tile(F{}, F{}, P0{}, j + 1);
-    } else {  // tile j (odd) is the last
-      if (tail) tile(F{}, T{}, P1{}, j);
-      else tile(F{}, F{}, P1{}, j);
-    }
+    ring3<1>(1, ntiles, tail, [&](auto tl, auto sl, int j) __attribute__((always_inline)) { tile(F{}, tl, sl, j); });
   }
   const float lt = half_exchange_sum(a.l);
   const float inv = 1.f / lt;
