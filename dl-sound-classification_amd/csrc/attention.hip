@@ -704,8 +704,8 @@ __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const 
 __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                              const bf16* __restrict__ frag, bf16* __restrict__ dqkv,
                                                              int N, int H, int nqb, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(1024))) bf16 Ks[2][64 * 64];
-  __shared__ __attribute__((aligned(1024))) bf16 Vs[2][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Ks[3][64 * 64];
+  __shared__ __attribute__((aligned(1024))) bf16 Vs[3][64 * 64];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int w = xcd_work_item(blockIdx.x, gridDim.x);
@@ -740,39 +740,31 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
       for (int j = 0; j < 8; ++j) { lf[j] = (bf16)0.f; dlf[j] = (bf16)0.f; }
     }
   }
+  if (ntiles > 1) {
+    kd.issue(Ks[1], tile_bytes, wave);
+    vd.issue(Vs[1], tile_bytes, wave);
+  }
   const bf16x8 one = ones3(lane);
   f32x16 acc[2];
   acc[0] = zero16(); acc[1] = zero16();
-  auto tile = [&](auto tail, auto par, int j) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;
-    if (j + 1 < ntiles) {
-      kd.issue(Ks[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
-      vd.issue(Vs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
+  // one tile in slot P of the 3-slot ring: tile j + 2's DMA flies under this tile's work and tile j + 1's
+  auto tile = [&](auto tail, auto slot, int j) __attribute__((always_inline)) {
+    constexpr int P = decltype(slot)::value;
+    constexpr int PN = (P + 2) % 3;
+    const bool ahead = j + 2 < ntiles;
+    if (ahead) {
+      kd.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
+      vd.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
     }
     dq_tile<decltype(tail)::value>(acc, Ks[P], Vs[P], qf, gf, one, lf, dlf, j * 64, N, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  using T = std::true_type;
-  using F = std::false_type;
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 and the Q / dO fragments
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const bool tail = (ntiles * 64 != N);
-  int j = 0;
-  for (; j + 2 < ntiles; j += 2) {
-    tile(F{}, P0{}, j);
-    tile(F{}, P1{}, j + 1);
-  }
-  if (j + 1 < ntiles) {
-    tile(F{}, P0{}, j);
-    if (tail) tile(T{}, P1{}, j + 1);
-    else tile(F{}, P1{}, j + 1);
-  } else {
-    if (tail) tile(T{}, P0{}, j);
-    else tile(F{}, P0{}, j);
-  }
+  ring3<0>(0, ntiles, ntiles * 64 != N, tile);
   if (!qv) return;
   bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
 #pragma unroll
