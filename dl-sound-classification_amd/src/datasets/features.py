@@ -72,7 +72,8 @@ class GpuLogMel:
             self._dev[key] = {k: v.to(device) for k, v in self._host.items()}
         return self._dev[key]
 
-    def __call__(self, wav: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def __call__(self, wav: torch.Tensor, out: torch.Tensor | None = None, lib=None) -> torch.Tensor:
+        """``lib``: another build of the C ABI (tools/bench_logmel.py A/B); default the product library."""
         L.require_device(wav, "GpuLogMel")
         if wav.dim() == 3:
             wav = wav.reshape(wav.shape[0], -1)
@@ -82,7 +83,7 @@ class GpuLogMel:
         if out is None:
             out = torch.empty(B, self.n_mels, frames, dtype=torch.float32, device=wav.device)
         t = self.tables(wav.device)
-        lib = L.load()
+        lib = lib or L.load()
         ws = K.workspace(lib.mia_logmel_workspace_bytes(B, frames), wav.device, "logmel")
         # algorithmic HBM bytes: waveform read once + log-mel written once, f32
         with K.probe("logmel.fwd", 0.0, B * T * 4 + out.numel() * 4):
