@@ -1596,9 +1596,10 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   // plain f32 output of a full tile (the wide weight-gradient GEMMs, e.g. EnvNet FC1: 1.38 GB of f32
   // per step): the whole 128x128 tile is staged in the (now idle) 64 KB of LDS and written as whole
   // 512-B rows, two rows per wave store instruction, non-temporal (read next by the optimizer pass)
-  const bool plain = g.split == 1 && g.e.dtype == MIA_F32 && g.e.act == MIA_ACT_NONE && !g.e.bias &&
-                     !g.e.accumulate && !g.e.rm_inner && g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N &&
-                     (g.e.ldc & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0;
+  const bool plain = g.mode != 0 ||
+                     (g.split == 1 && g.e.dtype == MIA_F32 && g.e.act == MIA_ACT_NONE && !g.e.bias &&
+                      !g.e.accumulate && !g.e.rm_inner && g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N &&
+                      (g.e.ldc & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0);
   if (plain) {
     float* tile = reinterpret_cast<float*>(smem);  // [128][128], 32-dword halves swapped on row bit 2
 #pragma unroll
@@ -1612,6 +1613,47 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
           tile[row * 128 + (col ^ (((row >> 2) & 1) << 5))] = acc[i][j][r];
         }
     __syncthreads();
+    if (g.mode == 2) {
+      // Adam on the parameter rows this tile is the gradient of (torch single-tensor Adam, exactly
+      // adam_kernel's arithmetic; the gradient is the f32 product itself, which is never stored).  Four
+      // 16-B groups per lane in flight: p / m / v loads of 4 rows issued before any use.
+      const DArgs::AdamEpi& A = g.adam;
+      const float coef = A.coef[0];
+      const int col = (lane & 31) * 4;
+#pragma unroll 1
+      for (int it0 = 0; it0 < 16; it0 += 4) {
+        f32x4 pv[4], mv[4], vv[4], gv[4];
+        int64_t off[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int row = wave * 32 + (it0 + u) * 2 + (lane >> 5);
+          off[u] = (m0 + row) * A.ld + n0 + col;
+          gv[u] = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
+          pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.p + off[u]));
+          mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.m + off[u]));
+          vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.v + off[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = fmaf(A.wd, pv[u][e], gv[u][e] * coef);
+            mv[u][e] = mv[u][e] + (1.f - A.beta1) * (gg - mv[u][e]);
+            vv[u][e] = fmaf((1.f - A.beta2) * gg, gg, vv[u][e] * A.beta2);
+            const float denom = sqrtf(vv[u][e]) / A.bc2_sqrt + A.eps;
+            pv[u][e] = pv[u][e] - A.lr_over_bc1 * (mv[u][e] / denom);
+          }
+          __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4*>(A.p + off[u]));
+          __builtin_nontemporal_store(mv[u], reinterpret_cast<f32x4*>(A.m + off[u]));
+          __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(A.v + off[u]));
+          if (A.shadow) {
+            const bf16x4 b4 = {(bf16)pv[u][0], (bf16)pv[u][1], (bf16)pv[u][2], (bf16)pv[u][3]};
+            __builtin_nontemporal_store(b4, reinterpret_cast<bf16x4*>(A.shadow + off[u]));
+          }
+        }
+      }
+      return;
+    }
     float* out = reinterpret_cast<float*>(g.e.ptr);
     float sq = 0.f;
 #pragma unroll 4
@@ -1619,8 +1661,10 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       const int row = wave * 32 + it * 2 + (lane >> 5);
       const int col = (lane & 31) * 4;
       const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
-      f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
-      __builtin_nontemporal_store(v, dst);
+      if (g.mode == 0) {
+        f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
+        __builtin_nontemporal_store(v, dst);
+      }
       if (g.e.sqsum) sq = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], sq))));
     }
     if (g.e.sqsum) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq, reinterpret_cast<double*>(smem));
@@ -1929,6 +1973,7 @@ static int gemm_tile(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue
     d.gm = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2ll << 20) / (128 * 2 * std::max<int64_t>(K, 64))));
     d.ws = reinterpret_cast<float*>(workspace);
     d.e = to_dev(*E);
+    d.mode = 0;
     hipStream_t s = as_stream(stream);
     hipError_t err;
     const int la = A->layout, lb = B->layout;
@@ -2049,6 +2094,54 @@ static int gemm_tile(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue
 }
 
 extern "C" int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N) { return cdiv(M, 128) * cdiv(N, 128); }
+
+// The dense 128 x 128 kernel in its norm-only / fused-Adam modes (DArgs::mode): full tiles, no split.
+static int dgemm_mode(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K, int mode,
+                      double* sqsum, const DArgs::AdamEpi* adam, mia_stream_t stream) {
+  MIA_CHECK_ARG(A && B, "gemm_wgrad: null descriptor");
+  MIA_CHECK_ARG(dgemm_ok(*A, *B, M, N, K, MIA_BF16) && M % 128 == 0 && N % 128 == 0,
+                "gemm_wgrad: needs bf16 dense operands, M and N multiples of 128, K a multiple of 64");
+  DArgs d;
+  memset(&d, 0, sizeof(d));
+  d.a = reinterpret_cast<const bf16*>(A->ptr); d.b = reinterpret_cast<const bf16*>(B->ptr);
+  d.lda = A->ld; d.ldb = B->ld; d.M = M; d.N = N; d.K = K;
+  d.split = 1; d.kper = K;
+  d.nbm = (int)(M / 128); d.nbn = (int)(N / 128);
+  d.nfast = 0; d.gm = 1;
+  d.e.dtype = MIA_F32; d.e.alpha = 1.f; d.e.sqsum = sqsum;
+  d.mode = mode;
+  if (adam) d.adam = *adam;
+  hipStream_t s = as_stream(stream);
+  hipError_t err;
+  const int la = A->layout, lb = B->layout;
+  if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
+  else if (la == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_RC>(d, s);
+  else if (lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_KC>(d, s);
+  else err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC>(d, s);
+  if (err != hipSuccess) return mia::fail(-(int)err, "gemm_wgrad launch: %s", hipGetErrorString(err));
+  return 0;
+}
+
+extern "C" int mia_gemm_sqsum_only(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K,
+                                   double* sqsum, mia_stream_t stream) {
+  MIA_CHECK_ARG(sqsum, "gemm_sqsum_only: null sqsum");
+  return dgemm_mode(A, B, M, N, K, 1, sqsum, nullptr, stream);
+}
+
+extern "C" int mia_gemm_adam(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K, float* param,
+                             float* exp_avg, float* exp_avg_sq, void* shadow_bf16, int64_t ld, const float* coef,
+                             float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps, float weight_decay,
+                             mia_stream_t stream) {
+  MIA_CHECK_ARG(param && exp_avg && exp_avg_sq && coef, "gemm_adam: null pointer");
+  MIA_CHECK_ARG(ld >= N && ld % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(exp_avg) |
+                      reinterpret_cast<uintptr_t>(exp_avg_sq)) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(shadow_bf16) & 7) == 0,
+                "gemm_adam: p / m / v must be 16-B aligned rows (ld %% 4 == 0), the shadow 8-B aligned");
+  DArgs::AdamEpi a{param, exp_avg, exp_avg_sq, reinterpret_cast<bf16*>(shadow_bf16), coef, lr_over_bc1, bc2_sqrt,
+                   beta1, beta2, eps, weight_decay, ld};
+  return dgemm_mode(A, B, M, N, K, 2, nullptr, &a, stream);
+}
 
 // workspace layout of one mia_gemm call on paths 0-5: [split-K slabs][column-sum partials]
 static int64_t colsum_ws_offset(int64_t M, int64_t N, int32_t split_k) {

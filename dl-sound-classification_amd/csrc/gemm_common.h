@@ -29,6 +29,19 @@ struct DArgs {
               // row block per XCD: ~8-11 GB per AST launch.)
   float* ws;
   EpiDev e;
+  // 0: store through e; 1: only the per-tile sums of squares of the f32 product (e.sqsum), nothing
+  // stored; 2: no store either -- the product is a weight gradient and the epilogue applies the Adam
+  // update of `adam` to the parameter it belongs to (full 128 x 128 tiles, split 1)
+  int mode;
+  struct AdamEpi {
+    float* p;
+    float* m;
+    float* v;
+    bf16* shadow;        // bf16 operand copy of p, rewritten (or null)
+    const float* coef;   // device clip coefficient (mia_clip_adam's)
+    float lr_over_bc1, bc2_sqrt, beta1, beta2, eps, wd;
+    int64_t ld;          // row stride of p / m / v / shadow (elements)
+  } adam;
 };
 
 // -------------------------------------------------------------------------- epilogue

@@ -192,6 +192,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(void* const* __restrict__ para
                                                   float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps,
                                                   float wd, const int32_t* __restrict__ steps, float lr) {
   const int tsr = blockIdx.y;
+  if (!grads[tsr]) return;  // a deferred weight gradient: its update runs in its GEMM (mia_gemm_adam)
   if (steps) {  // per-tensor step counts (a parameter that missed gradients keeps its own count, as torch's Adam)
     const double st = (double)steps[tsr];
     lr_over_bc1 = (float)(lr / (1.0 - pow((double)beta1, st)));
@@ -530,6 +531,9 @@ extern "C" int mia_soft_ce(const float* logits, const float* y, int32_t B, int32
 extern "C" int64_t mia_adam_workspace_bytes(int32_t ntensors) {
   return ((int64_t)ntensors * ADAM_PARTS + 2) * 8;
 }
+
+// byte offset of the clip coefficient (f32) inside mia_clip_adam's workspace
+extern "C" int64_t mia_adam_coef_offset(int32_t ntensors) { return (int64_t)ntensors * ADAM_PARTS * 8; }
 
 extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg, void* const* exp_avg_sq,
                              void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,

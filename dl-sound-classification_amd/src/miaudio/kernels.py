@@ -101,6 +101,34 @@ def sqsum_slots(out: torch.Tensor, M: int, N: int) -> torch.Tensor:
     return buf
 
 
+def gemm_sqsum_only(A: L.MiaOperand, B: L.MiaOperand, M: int, N: int, K: int, sq: torch.Tensor,
+                    tag: str | None = None):
+    """Per-tile sums of squares of the f32 product A^T B (mia_gemm_sqsum_only): nothing else stored."""
+    rec = PROBE is not None and tag in PROBE
+    if rec:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    L.check(L.load().mia_gemm_sqsum_only(A, B, M, N, K, sq.data_ptr(), _s()), "mia_gemm_sqsum_only")
+    if rec:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        PROBE[tag].append((e0, e1, 2 * M * N * K, _operand_bytes(A, M, K) + _operand_bytes(B, N, K)))
+
+
+def defer_weight_grad(param: torch.Tensor, A: L.MiaOperand, B: L.MiaOperand, M: int, N: int, K: int,
+                      keep, tag: str | None = None) -> None:
+    """Defer the f32 weight gradient ``A^T B`` (M x N, the parameter's shape) of ``param`` to the optimizer:
+    only its per-tile sums of squares are computed now (the clip norm's share); FusedAdam.step recomputes
+    the product inside the fused Adam GEMM (mia_gemm_adam), so the gradient is never written or re-read.
+    ``keep``: the operand tensors (kept alive until the step)."""
+    if getattr(param, "_mia_deferred", None) is not None:
+        raise RuntimeError("a deferred weight gradient is still pending: call the optimizer's step() "
+                           "(FusedAdam) between backward passes, or build the model's optimizer as torch.optim")
+    sq = torch.empty(int(L.load().mia_gemm_sqsum_slots(M, N)), dtype=torch.float64, device=param.device)
+    gemm_sqsum_only(A, B, M, N, K, sq, tag=tag)
+    param._mia_deferred = dict(A=A, B=B, M=M, N=N, K=K, sq=sq, keep=keep)
+
+
 def tag_sqsum(param: torch.Tensor, grad: torch.Tensor, buf: torch.Tensor) -> None:
     """Record on ``param`` that ``buf`` holds the per-tile sums of squares of the gradient ``grad``, so
     FusedAdam's clip-norm pass reads the slots instead of the tensor.  The tag lives on the parameter

@@ -59,6 +59,9 @@ SIGNATURES = {
     "mia_gemm_workspace_bytes": (i64, [i64, i64, i32]),
     "mia_gemm_workspace_bytes_ex": (i64, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32]),
     "mia_gemm_sqsum_slots": (i64, [i64, i64]),
+    "mia_gemm_sqsum_only": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, vp, vp]),
+    "mia_gemm_adam": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, vp, vp, vp, vp, i64, vp, f32, f32, f32,
+                                f32, f32, f32, vp]),
     "mia_gemm": (C.c_int, [P(MiaOperand), P(MiaOperand), P(MiaEpilogue), i64, i64, i64, i32, i32, vp, vp]),
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
     "mia_mx_quantize": (C.c_int, [vp, i32, i64, i64, i64, vp, i64, vp, vp]),
@@ -102,6 +105,7 @@ SIGNATURES = {
     "mia_dropout": (C.c_int, [vp, i32, i64, f32, C.c_uint64, vp]),
     "mia_soft_ce": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "mia_adam_workspace_bytes": (i64, [i32]),
+    "mia_adam_coef_offset": (i64, [i32]),
     "mia_clip_adam": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp, vp,
                                 vp, vp]),
     "mia_layernorm_fwd": (C.c_int, [vp, i32, vp, vp, vp, i32, vp, vp, i64, i32, f32, vp]),

@@ -318,6 +318,14 @@ class EnvNetFunction(torch.autograd.Function):
                     K.gemm(K.dense(dcur[:, lo:], L.RC, B, FC1_CHUNK_ROWS, ld=fout), K.dense(hin, L.RC, B, fin),
                            K.epilogue(part, fin), FC1_CHUNK_ROWS, fin, B, cd, tag="fc1.wgrad")
                     chunk_ready(p[40], dW, part, lo + FC1_CHUNK_ROWS == fout)
+            elif (li == 0 and ready is None and chunk_ready is None and cd == L.BF16 and p[40].grad is None
+                  and getattr(p[40], "_mia_fused_adam", False) and fout % 128 == 0 and fin % 128 == 0
+                  and B % 64 == 0):
+                # single GPU under FusedAdam: FC1's 1.38 GB weight gradient is never written -- its sums
+                # of squares now, the product recomputed inside the fused Adam GEMM at the step
+                K.defer_weight_grad(p[40], K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), fout, fin, B,
+                                    keep=(dcur, hin), tag="fc1.wgrad")
+                dW = None
             else:
                 # FC1/FC2: the GEMM epilogue also writes per-tile sums of squares of dW, so the clip-norm
                 # pass of FusedAdam does not re-read the 1.4 GB (K.sqsum_slots)

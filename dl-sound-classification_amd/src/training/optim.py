@@ -9,6 +9,9 @@ so the step never synchronises with the host.
 """
 from __future__ import annotations
 
+import math
+
+import numpy as np
 import torch
 
 from ..miaudio import kernels as K
@@ -39,6 +42,10 @@ class FusedAdam(torch.optim.Optimizer):
         self._table_key = None     # pointer table of the last step (host pinned + device copy)
         self._table = None
         self.table_builds = 0
+        self.last_deferred = 0     # weight gradients applied by their fused Adam GEMM (last step)
+        for p in self.param_groups[0]["params"]:
+            # models may defer a wide Linear's weight gradient to this optimizer (K.defer_weight_grad)
+            p._mia_fused_adam = True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -49,13 +56,16 @@ class FusedAdam(torch.optim.Optimizer):
         if len(self.param_groups) != 1:
             raise RuntimeError("FusedAdam drives one parameter group (the reference configures one)")
         grp = self.param_groups[0]
-        ps = [p for p in grp["params"] if p.grad is not None]
+        ps = [p for p in grp["params"] if p.grad is not None or getattr(p, "_mia_deferred", None) is not None]
         if not ps:
             return loss
         dev = ps[0].device
         L.require_device(ps[0], "FusedAdam")
-        for p in ps:
-            if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+        deferred = [getattr(p, "_mia_deferred", None) for p in ps]
+        for p, d in zip(ps, deferred):
+            if d is not None and p.grad is not None:
+                raise RuntimeError("a parameter has both a gradient and a deferred weight gradient")
+            if p.dtype != torch.float32 or (d is None and p.grad.dtype != torch.float32):
                 raise TypeError("FusedAdam keeps f32 master parameters and gradients")
             st = self.state[p]
             if not st:
@@ -68,15 +78,18 @@ class FusedAdam(torch.optim.Optimizer):
         steps = [int(self.state[p]["step"].item()) for p in ps]
         step = steps[0]
         per_tensor_steps = any(v != step for v in steps)
-        gs = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
+        gs = [None if d is not None else (p.grad if p.grad.is_contiguous() else p.grad.contiguous())
+              for p, d in zip(ps, deferred)]
         # parameters with a live bf16 operand copy (K.bf16_shadow) get it rewritten in the update pass
         shadows = [getattr(p, "_mia_bf16", None) if getattr(p, "_mia_bf16_ver", None) == p._version else None
                    for p in ps]
-        # gradients whose producing GEMM left per-tile sums of squares (K.sqsum_slots) skip the norm read
-        pre = [K.valid_sqsum(p, g) for p, g in zip(ps, gs)]
+        # gradients whose producing GEMM left per-tile sums of squares (K.sqsum_slots) skip the norm read;
+        # a deferred one is in the table with a NULL gradient: norm from its sums, update by its GEMM
+        pre = [d["sq"] if d is not None else K.valid_sqsum(p, g) for p, g, d in zip(ps, gs, deferred)]
         self.last_precomputed = sum(q is not None for q in pre)
+        self.last_deferred = sum(d is not None for d in deferred)
         have_pre = self.last_precomputed > 0
-        rows = [[p.data_ptr() for p in ps], [g.data_ptr() for g in gs],
+        rows = [[p.data_ptr() for p in ps], [0 if g is None else g.data_ptr() for g in gs],
                 [self.state[p]["exp_avg"].data_ptr() for p in ps],
                 [self.state[p]["exp_avg_sq"].data_ptr() for p in ps],
                 [0 if sh is None else sh.data_ptr() for sh in shadows],
@@ -103,7 +116,10 @@ class FusedAdam(torch.optim.Optimizer):
         # p, m, v written (28 B/param) + the bf16 operand copies rewritten (2 B/param where shadowed)
         nel = sum(p.numel() for p in ps)
         nbytes = 32 * nel + 2 * sum(p.numel() for p, sh in zip(ps, shadows) if sh is not None)
-        nbytes -= 4 * sum(g.numel() for g, q in zip(gs, pre) if q is not None)
+        nbytes -= 4 * sum(p.numel() for p, q in zip(ps, pre) if q is not None)  # no norm read of those
+        for p, d in zip(ps, deferred):  # no gradient read either; the GEMM reads its two bf16 operands
+            if d is not None:
+                nbytes += -4 * p.numel() + 2 * d["K"] * (d["M"] + d["N"])
         with K.probe("optim.step", 0.0, nbytes):
             L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
                                       table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
@@ -114,11 +130,25 @@ class FusedAdam(torch.optim.Optimizer):
                                       table[7].data_ptr() if have_pre else None,
                                       steps_dev.data_ptr() if per_tensor_steps else None,
                                       L.stream_ptr()), "mia_clip_adam")
+            coef = ws.data_ptr() + int(lib.mia_adam_coef_offset(n))
+            for p, d, sh, st in zip(ps, deferred, shadows, steps):
+                if d is None:
+                    continue
+                # the bias corrections exactly as mia_clip_adam forms them: f32 lr / betas, double pow
+                lr32, b1_32, b2_32 = (float(np.float32(v)) for v in (grp["lr"], b1, b2))
+                lr_bc1 = lr32 / (1.0 - math.pow(b1_32, st))
+                bc2_sqrt = math.sqrt(1.0 - math.pow(b2_32, st))
+                L.check(lib.mia_gemm_adam(d["A"], d["B"], d["M"], d["N"], d["K"], p.data_ptr(),
+                                          self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr(),
+                                          L.ptr(sh), d["N"], coef, lr_bc1, bc2_sqrt, float(b1), float(b2),
+                                          float(grp["eps"]), float(grp["weight_decay"]), L.stream_ptr()),
+                        "mia_gemm_adam")
         self.last_total_norm = tot
         for p, sh in zip(ps, shadows):
             if sh is not None:
                 p._mia_bf16_ver = p._version  # the copy now matches the updated parameter
         for p in ps:
             p._mia_sqsum = None  # consumed (or stale): the next step's gradient brings its own
-        self._keep = (gs, pre, steps_host, steps_dev)  # alive until the next step (async copies, table targets)
+            p._mia_deferred = None
+        self._keep = (gs, pre, steps_host, steps_dev, deferred)  # alive until the next step (async use)
         return loss

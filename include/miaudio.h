@@ -131,6 +131,21 @@ int64_t mia_gemm_workspace_bytes_ex(const MiaOperand* A, const MiaOperand* B, co
                                     int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k);
 /* number of MiaEpilogue.sqsum slots (doubles) of an M x N output */
 int64_t mia_gemm_sqsum_slots(int64_t M, int64_t N);
+/* Deferred weight gradient of a wide nn.Linear (EnvNet-v2 FC1, envnet_v2.py:51: dW = dY^T X, 4096 x 84480
+ * f32 = 1.38 GB per step), so the gradient is never written: in the backward mia_gemm_sqsum_only leaves only
+ * its per-tile sums of squares (mia_gemm_sqsum_slots(M, N) doubles, the clip norm's share), and after the
+ * norm is known mia_gemm_adam recomputes the product (K = the batch: cheap) and applies torch's
+ * single-tensor Adam to the parameter rows in the epilogue -- exactly mia_clip_adam's arithmetic, the
+ * clip coefficient read from `coef` (mia_clip_adam's workspace + mia_adam_coef_offset(ntensors)), the
+ * bias corrections as lr / bc1 and sqrt(bc2); p / m / v (and the optional bf16 shadow) rows of stride ld.
+ * Full 128 x 128 tiles (M, N multiples of 128), bf16 dense operands, K a multiple of 64.  Replaces the
+ * gradient write + re-read of the Linear backward + torch.optim.Adam (engine.py:299-310). */
+int mia_gemm_sqsum_only(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K, double* sqsum,
+                        mia_stream_t stream);
+int mia_gemm_adam(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N, int64_t K, float* param,
+                  float* exp_avg, float* exp_avg_sq, void* shadow_bf16, int64_t ld, const float* coef,
+                  float lr_over_bc1, float bc2_sqrt, float beta1, float beta2, float eps, float weight_decay,
+                  mia_stream_t stream);
 int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue* E, int64_t M,
              int64_t N, int64_t K, int32_t compute_dtype, int32_t split_k, void* workspace,
              mia_stream_t stream);
@@ -400,6 +415,9 @@ int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32
  * each tensor its own 1-based step for the bias corrections (torch.optim.Adam keeps a step count per
  * parameter; a parameter that had no gradient in some step is behind the others). */
 int64_t mia_adam_workspace_bytes(int32_t ntensors);
+/* byte offset of the device clip coefficient (f32) inside that workspace; a tensor whose grads[] entry is
+ * NULL is counted in the norm through pre_sq only and not updated (its update is mia_gemm_adam's) */
+int64_t mia_adam_coef_offset(int32_t ntensors);
 int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
                   void* const* exp_avg_sq, void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors,
                   int64_t max_numel, float lr, float beta1, float beta2, float eps,
