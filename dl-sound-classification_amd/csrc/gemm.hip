@@ -1518,7 +1518,7 @@ __device__ __forceinline__ bf16x8 dfrag(const char* tile, int rbase, int ks, int
 }
 
 
-template <int LA, int LB>
+template <int LA, int LB, bool ADAM = false>
 __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   constexpr int TILE = 128 * 64 * 2;
   __shared__ __attribute__((aligned(1024))) char smem[4 * TILE];
@@ -1560,6 +1560,22 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // fused Adam (mode 2): the parameter rows of the tile's first 16-B group per lane -- p / m / v -- are
+  // fetched before the main loop, so their HBM latency hides under it; later groups are fetched one
+  // group ahead of their use in the epilogue
+  f32x4 pv[2][4], mv[2][4], vv[2][4];
+  const int acol = (lane & 31) * 4;
+  auto adam_fetch = [&](int it0, int b) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t off = (m0 + wave * 32 + (it0 + u) * 2 + (lane >> 5)) * g.adam.ld + n0 + acol;
+      pv[b][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g.adam.p + off));
+      mv[b][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g.adam.m + off));
+      vv[b][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g.adam.v + off));
+    }
+  };
+  if constexpr (ADAM) adam_fetch(0, 0);
+
   if (nk > 0) {
     la.issue(smem, wave);
     lb.issue(smem + TILE, wave);
@@ -1596,11 +1612,26 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   // plain f32 output of a full tile (the wide weight-gradient GEMMs, e.g. EnvNet FC1: 1.38 GB of f32
   // per step): the whole 128x128 tile is staged in the (now idle) 64 KB of LDS and written as whole
   // 512-B rows, two rows per wave store instruction, non-temporal (read next by the optimizer pass)
-  const bool plain = g.mode != 0 ||
+  const bool plain = ADAM || g.mode != 0 ||
                      (g.split == 1 && g.e.dtype == MIA_F32 && g.e.act == MIA_ACT_NONE && !g.e.bias &&
                       !g.e.accumulate && !g.e.rm_inner && g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N &&
                       (g.e.ldc & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0);
   if (plain) {
+    // the tile's sum of squares straight from the accumulators (one fixed order shared by the stored
+    // and the sums-only forms, so a deferred gradient's norm equals the materialised one's bit for bit)
+    float sq = 0.f;
+    if (g.e.sqsum) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sq = fmaf(acc[i][j][r], acc[i][j][r], sq);
+    }
+    if (g.mode == 1) {  // sums only: nothing staged, nothing stored
+      tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq, reinterpret_cast<double*>(smem));
+      return;
+    }
     float* tile = reinterpret_cast<float*>(smem);  // [128][128], 32-dword halves swapped on row bit 2
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1613,59 +1644,47 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
           tile[row * 128 + (col ^ (((row >> 2) & 1) << 5))] = acc[i][j][r];
         }
     __syncthreads();
-    if (g.mode == 2) {
+    if constexpr (ADAM) {
       // Adam on the parameter rows this tile is the gradient of (torch single-tensor Adam, exactly
-      // adam_kernel's arithmetic; the gradient is the f32 product itself, which is never stored).  Four
-      // 16-B groups per lane in flight: p / m / v loads of 4 rows issued before any use.
+      // adam_kernel's arithmetic; the gradient is the f32 product itself, which is never stored)
       const DArgs::AdamEpi& A = g.adam;
       const float coef = A.coef[0];
-      const int col = (lane & 31) * 4;
-#pragma unroll 1
-      for (int it0 = 0; it0 < 16; it0 += 4) {
-        f32x4 pv[4], mv[4], vv[4], gv[4];
-        int64_t off[4];
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        const int b = grp & 1;
+        if (grp + 1 < 4) adam_fetch((grp + 1) * 4, b ^ 1);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int row = wave * 32 + (it0 + u) * 2 + (lane >> 5);
-          off[u] = (m0 + row) * A.ld + n0 + col;
-          gv[u] = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
-          pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.p + off[u]));
-          mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.m + off[u]));
-          vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(A.v + off[u]));
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
+          const int row = wave * 32 + (grp * 4 + u) * 2 + (lane >> 5);
+          const int64_t off = (m0 + row) * A.ld + n0 + acol;
+          const f32x4 gv = *reinterpret_cast<const f32x4*>(tile + row * 128 + (acol ^ (((row >> 2) & 1) << 5)));
+          f32x4 p4 = pv[b][u], m4 = mv[b][u], v4 = vv[b][u];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float gg = fmaf(A.wd, pv[u][e], gv[u][e] * coef);
-            mv[u][e] = mv[u][e] + (1.f - A.beta1) * (gg - mv[u][e]);
-            vv[u][e] = fmaf((1.f - A.beta2) * gg, gg, vv[u][e] * A.beta2);
-            const float denom = sqrtf(vv[u][e]) / A.bc2_sqrt + A.eps;
-            pv[u][e] = pv[u][e] - A.lr_over_bc1 * (mv[u][e] / denom);
+            const float gg = fmaf(A.wd, p4[e], gv[e] * coef);
+            m4[e] = m4[e] + (1.f - A.beta1) * (gg - m4[e]);
+            v4[e] = fmaf((1.f - A.beta2) * gg, gg, v4[e] * A.beta2);
+            const float denom = sqrtf(v4[e]) / A.bc2_sqrt + A.eps;
+            p4[e] = p4[e] - A.lr_over_bc1 * (m4[e] / denom);
           }
-          __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4*>(A.p + off[u]));
-          __builtin_nontemporal_store(mv[u], reinterpret_cast<f32x4*>(A.m + off[u]));
-          __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(A.v + off[u]));
+          __builtin_nontemporal_store(p4, reinterpret_cast<f32x4*>(A.p + off));
+          __builtin_nontemporal_store(m4, reinterpret_cast<f32x4*>(A.m + off));
+          __builtin_nontemporal_store(v4, reinterpret_cast<f32x4*>(A.v + off));
           if (A.shadow) {
-            const bf16x4 b4 = {(bf16)pv[u][0], (bf16)pv[u][1], (bf16)pv[u][2], (bf16)pv[u][3]};
-            __builtin_nontemporal_store(b4, reinterpret_cast<bf16x4*>(A.shadow + off[u]));
+            const bf16x4 b4 = {(bf16)p4[0], (bf16)p4[1], (bf16)p4[2], (bf16)p4[3]};
+            __builtin_nontemporal_store(b4, reinterpret_cast<bf16x4*>(A.shadow + off));
           }
         }
       }
       return;
     }
     float* out = reinterpret_cast<float*>(g.e.ptr);
-    float sq = 0.f;
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {
       const int row = wave * 32 + it * 2 + (lane >> 5);
       const int col = (lane & 31) * 4;
       const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 128 + (col ^ (((row >> 2) & 1) << 5)));
-      if (g.mode == 0) {
-        f32x4* dst = reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col);
-        __builtin_nontemporal_store(v, dst);
-      }
-      if (g.e.sqsum) sq = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], sq))));
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (m0 + row) * g.e.ldc + n0 + col));
     }
     if (g.e.sqsum) tile_sqsum_store(g.e.sqsum + (int64_t)bm * g.nbn + bn, (double)sq, reinterpret_cast<double*>(smem));
     return;
@@ -1784,10 +1803,10 @@ bool dgemm_ok(const MiaOperand& A, const MiaOperand& B, int64_t M, int64_t N, in
   return true;
 }
 
-template <int LA, int LB>
+template <int LA, int LB, bool ADAM = false>
 hipError_t dgemm_launch2(const DArgs& d, hipStream_t s) {
   dim3 grid((unsigned)(d.nbm * d.nbn), (unsigned)d.split);
-  dgemm_kernel<LA, LB><<<grid, NT, 0, s>>>(d);
+  dgemm_kernel<LA, LB, ADAM><<<grid, NT, 0, s>>>(d);
   return hipGetLastError();
 }
 
@@ -2107,14 +2126,19 @@ static int dgemm_mode(const MiaOperand* A, const MiaOperand* B, int64_t M, int64
   d.lda = A->ld; d.ldb = B->ld; d.M = M; d.N = N; d.K = K;
   d.split = 1; d.kper = K;
   d.nbm = (int)(M / 128); d.nbn = (int)(N / 128);
-  d.nfast = 0; d.gm = 1;
+  // sums only: row-block-major tile order (an XCD's concurrent tiles share their dY rows; 0.271 -> 0.259 ms
+  // for FC1); the Adam form keeps column-block-major (row-major measured 2.14 -> 2.18 ms)
+  d.nfast = mode == 1; d.gm = 1;
   d.e.dtype = MIA_F32; d.e.alpha = 1.f; d.e.sqsum = sqsum;
   d.mode = mode;
   if (adam) d.adam = *adam;
   hipStream_t s = as_stream(stream);
   hipError_t err;
   const int la = A->layout, lb = B->layout;
-  if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
+  if (mode == 2) {  // the weight-gradient layouts only (dY and X both K-major: RC x RC)
+    MIA_CHECK_ARG(la == MIA_LAYOUT_RC && lb == MIA_LAYOUT_RC, "gemm_adam: needs RC operands");
+    err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC, true>(d, s);
+  } else if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_KC>(d, s);
   else if (la == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_KC, MIA_LAYOUT_RC>(d, s);
   else if (lb == MIA_LAYOUT_KC) err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_KC>(d, s);
   else err = dgemm_launch2<MIA_LAYOUT_RC, MIA_LAYOUT_RC>(d, s);

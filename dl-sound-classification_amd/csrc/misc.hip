@@ -302,6 +302,49 @@ __global__ void tokens_fwd_kernel(const float* __restrict__ patches, const float
   }
 }
 
+// bf16 mode: the patch GEMM wrote token rows (x[b][t] = bias + patch t-1 of clip b . W for t >= 1, the
+// cls rows hold the bias of a zero patch); add the positional rows, cls token at t = 0, in place
+__global__ void tokens_fwd_inplace_kernel(float4* __restrict__ x, const float4* __restrict__ cls,
+                                          const float4* __restrict__ pos, int B, int N, int D4) {
+  const int64_t total = (int64_t)B * N * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D4);
+    const int tkn = (int)((i / D4) % N);
+    const float4 p = pos[(int64_t)tkn * D4 + d];
+    float4 v = tkn == 0 ? cls[d] : x[i];
+    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    x[i] = v;
+  }
+}
+
+// The patch matrix of the AST patch embedding (Conv2d(1, D, ps, stride st) over the (B, Fm, Tf)
+// spectrogram, reference src/models/ast.py:38 PatchEmbed) in token order: row b*N + t holds patch t-1
+// of clip b as bf16 (k = ky*ps + kx, the order of the flattened OIHW weight), row b*N (the cls slot) is
+// zero.  8 consecutive k per thread, one 16-B store.
+__global__ void ast_patches_kernel(const float* __restrict__ spec, int B, int Fm, int Tf, int ps, int st, int gw,
+                                   int N, uint4* __restrict__ out) {
+  const int k8 = ps * ps / 8;
+  const int64_t total = (int64_t)B * N * k8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % k8);
+    const int64_t row = i / k8;
+    const int tkn = (int)(row % N);
+    const int b = (int)(row / N);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (tkn > 0) {
+      const int p = tkn - 1, gy = p / gw, gx = p - gy * gw;
+      const int k0 = 8 * c, ky = k0 / ps, kx = k0 - ky * ps;
+      const float* src = spec + ((int64_t)b * Fm + gy * st + ky) * Tf + gx * st + kx;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16 lo = (bf16)src[2 * j], hi = (bf16)src[2 * j + 1];
+        w[j] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      }
+    }
+    out[i] = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 // dpos[t][d] = sum_b dout[b][t][d]; dcls = dpos[0]; dpatches[b][p] = dout[b][1+p]
 __global__ void tokens_bwd_kernel(const float* __restrict__ dout, float* __restrict__ dpatches, float* __restrict__ dcls,
                                   float* __restrict__ dpos, int B, int Np, int D) {
@@ -590,6 +633,30 @@ extern "C" int mia_tokens_fwd(const float* patches, const float* cls, const floa
   MIA_CHECK_ARG(patches && cls && pos && out && B > 0 && Np > 0 && D > 0, "tokens_fwd: args");
   tokens_fwd_kernel<<<blocks_for((int64_t)B * (Np + 1) * D), 256, 0, as_stream(stream)>>>(patches, cls, pos, out, B, Np, D);
   MIA_LAUNCH_CHECK("tokens_fwd");
+  return 0;
+}
+
+extern "C" int mia_tokens_fwd_inplace(float* x, const float* cls, const float* pos, int32_t B, int32_t N, int32_t D,
+                                      mia_stream_t stream) {
+  MIA_CHECK_ARG(x && cls && pos && B > 0 && N > 1 && D > 0 && D % 4 == 0, "tokens_fwd_inplace: args");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(cls) | reinterpret_cast<uintptr_t>(pos)) & 15) == 0,
+                "tokens_fwd_inplace: x / cls / pos must be 16-byte aligned");
+  tokens_fwd_inplace_kernel<<<blocks_for((int64_t)B * N * (D / 4)), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<float4*>(x), reinterpret_cast<const float4*>(cls), reinterpret_cast<const float4*>(pos), B, N,
+      D / 4);
+  MIA_LAUNCH_CHECK("tokens_fwd_inplace");
+  return 0;
+}
+
+extern "C" int mia_ast_patches(const float* spec, int32_t B, int32_t Fm, int32_t Tf, int32_t ps, int32_t st, void* out,
+                               mia_stream_t stream) {
+  MIA_CHECK_ARG(spec && out && B > 0 && ps > 0 && st > 0 && Fm >= ps && Tf >= ps && (ps * ps) % 8 == 0,
+                "ast_patches: args");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "ast_patches: out must be 16-byte aligned");
+  const int gh = (Fm - ps) / st + 1, gw = (Tf - ps) / st + 1, N = gh * gw + 1;
+  ast_patches_kernel<<<blocks_for((int64_t)B * N * (ps * ps / 8)), 256, 0, as_stream(stream)>>>(
+      spec, B, Fm, Tf, ps, st, gw, N, reinterpret_cast<uint4*>(out));
+  MIA_LAUNCH_CHECK("ast_patches");
   return 0;
 }
 

@@ -118,6 +118,8 @@ SIGNATURES = {
     "mia_attn_bwd_workspace_bytes": (C.c_int64, [i32, i32, i32, i32]),
     "mia_tokens_fwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_tokens_bwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "mia_ast_patches": (C.c_int, [vp, i32, i32, i32, i32, i32, vp, vp]),
+    "mia_tokens_fwd_inplace": (C.c_int, [vp, vp, vp, i32, i32, i32, vp]),
     "mia_cast": (C.c_int, [vp, i32, vp, i32, i64, vp]),
     "mia_add_inplace": (C.c_int, [vp, vp, i32, i64, vp]),
     "mia_bc_mix": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]),

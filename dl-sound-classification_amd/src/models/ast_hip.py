@@ -110,14 +110,26 @@ class ASTFunction(torch.autograd.Function):
             raise ValueError(f"{N} tokens exceed the positional table ({model.pos_embed.shape[1]})")
         Tt = B * N
         pw, pb, cls, pos = params[0], params[1], params[2], params[3]
-        # patch embedding: Conv2d(1, D, 16, stride 10) as an implicit GEMM over the 1-channel spectrogram
-        patches = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
-        K.gemm(K.conv(spec, L.KC, B, Fm, Tf, 1, gh, gw, ps, ps, sh=st, sw=st, row_kind=True),
-               K.dense(pw.reshape(D, -1), L.KC, D, ps * ps), K.epilogue(patches, D, bias=pb), B * Np, D, ps * ps, cd,
-               tag="patch.fwd")
+        # patch embedding: Conv2d(1, D, 16, stride 10).  bf16: the patch matrix in token order (zero cls
+        # rows, mia_ast_patches) through the dense 256x256 GEMM straight into the token rows of x, then the
+        # cls / positional rows in place; f32: an implicit GEMM over the spectrogram (exact-f32 MFMA)
         x = torch.empty(Tt, D, dtype=torch.float32, device=dev)
-        L.check(L.load().mia_tokens_fwd(patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), x.data_ptr(), B, Np, D,
-                                        L.stream_ptr()), "mia_tokens_fwd")
+        pmat = None
+        if cd == L.BF16:
+            pmat = torch.empty(Tt, ps * ps, dtype=torch.bfloat16, device=dev)
+            L.check(L.load().mia_ast_patches(spec.data_ptr(), B, Fm, Tf, ps, st, pmat.data_ptr(), L.stream_ptr()),
+                    "mia_ast_patches")
+            K.gemm(K.dense(pmat, L.KC, Tt, ps * ps), K.dense(K.bf16_shadow(pw).reshape(D, -1), L.KC, D, ps * ps),
+                   K.epilogue(x, D, bias=pb), Tt, D, ps * ps, cd, tag="patch.fwd")
+            L.check(L.load().mia_tokens_fwd_inplace(x.data_ptr(), cls.data_ptr(), pos.data_ptr(), B, N, D,
+                                                    L.stream_ptr()), "mia_tokens_fwd_inplace")
+        else:
+            patches = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
+            K.gemm(K.conv(spec, L.KC, B, Fm, Tf, 1, gh, gw, ps, ps, sh=st, sw=st, row_kind=True),
+                   K.dense(pw.reshape(D, -1), L.KC, D, ps * ps), K.epilogue(patches, D, bias=pb), B * Np, D, ps * ps,
+                   cd, tag="patch.fwd")
+            L.check(L.load().mia_tokens_fwd(patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), x.data_ptr(), B, Np,
+                                            D, L.stream_ptr()), "mia_tokens_fwd")
         saved_blocks = []
         nb = len(model.transformer)
         scale = (D // Hh) ** -0.5
@@ -172,7 +184,7 @@ class ASTFunction(torch.autograd.Function):
         z = torch.empty(B, wh.shape[0], dtype=torch.float32, device=dev)
         _linear(hc, wh, bh, z, B, cd, tag="head.fwd")
         probs = torch.sigmoid(z)
-        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec, gh=gh, gw=gw, blocks=saved_blocks, xc=xc, wcast=wcast,
+        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec if pmat is None else None, pmat=pmat, gh=gh, gw=gw, blocks=saved_blocks, xc=xc, wcast=wcast,
                      mc=mc, rc=rc, hc=hc, probs=probs, scale=scale)
         ctx.model = model
         ctx.params = params
@@ -250,19 +262,28 @@ class ASTFunction(torch.autograd.Function):
         pos = p[3]
         dpos = torch.zeros_like(pos)
         dcls = torch.empty(1, 1, D, dtype=torch.float32, device=dev)
-        dpatch = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
-        L.check(L.load().mia_tokens_bwd(dx.data_ptr(), dpatch.data_ptr(), dcls.data_ptr(), dpos.data_ptr(), B, Np, D,
-                                        L.stream_ptr()), "mia_tokens_bwd")
         pw = p[0]
         ps, st = model.patch_size, model.patch_stride
-        spec = s["spec"]
-        Fm, Tf = spec.shape[1], spec.shape[2]
         dWpe = torch.empty(D, ps * ps, dtype=torch.float32, device=dev)
-        K.gemm(K.dense(dpatch, L.RC, B * Np, D),
-               K.conv(spec, L.RC, B, Fm, Tf, 1, s["gh"], s["gw"], ps, ps, sh=st, sw=st, row_kind=True),
-               K.epilogue(dWpe, ps * ps), D, ps * ps, B * Np, cd, tag="patch.wgrad")
+        if s["pmat"] is not None:
+            # bf16: dW = dx^T P over all token rows (the zero cls rows of P add nothing), on the bf16 copy of
+            # dx the last LayerNorm backward wrote; the bias gradient = the patch rows of dpos summed
+            L.check(L.load().mia_tokens_bwd(dx.data_ptr(), None, dcls.data_ptr(), dpos.data_ptr(), B, Np, D,
+                                            L.stream_ptr()), "mia_tokens_bwd")
+            K.gemm(K.dense(dxb, L.RC, Tt, D), K.dense(s["pmat"], L.RC, Tt, ps * ps), K.epilogue(dWpe, ps * ps), D,
+                   ps * ps, Tt, cd, tag="patch.wgrad")
+            grads[1] = K.colsum(dpos.view(-1, D)[1:N], Np, D)
+        else:
+            dpatch = torch.empty(B * Np, D, dtype=torch.float32, device=dev)
+            L.check(L.load().mia_tokens_bwd(dx.data_ptr(), dpatch.data_ptr(), dcls.data_ptr(), dpos.data_ptr(), B,
+                                            Np, D, L.stream_ptr()), "mia_tokens_bwd")
+            spec = s["spec"]
+            Fm, Tf = spec.shape[1], spec.shape[2]
+            K.gemm(K.dense(dpatch, L.RC, B * Np, D),
+                   K.conv(spec, L.RC, B, Fm, Tf, 1, s["gh"], s["gw"], ps, ps, sh=st, sw=st, row_kind=True),
+                   K.epilogue(dWpe, ps * ps), D, ps * ps, B * Np, cd, tag="patch.wgrad")
+            grads[1] = K.colsum(dpatch, B * Np, D)
         grads[0] = dWpe.view_as(pw)
-        grads[1] = K.colsum(dpatch, B * Np, D)
         grads[2] = dcls
         grads[3] = dpos
         emit(0, 4)

@@ -471,6 +471,17 @@ int mia_tokens_fwd(const float* patches, const float* cls, const float* pos, flo
 int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, float* dpos, int32_t B,
                    int32_t Np, int32_t D, mia_stream_t stream);
 
+/* bf16 patch embedding (ast.py:38 PatchEmbed = Conv2d(1, D, ps, stride st); replaces the implicit-GEMM
+ * gather): mia_ast_patches writes the (B*N, ps*ps) bf16 patch matrix in TOKEN order (N = gh*gw + 1,
+ * row b*N is a zero row in the cls slot), so one dense GEMM with the bias epilogue writes the token rows
+ * of x directly and the weight gradient is one dense GEMM of the bf16 token gradient against it;
+ * mia_tokens_fwd_inplace then sets x[b][0] = cls + pos[0] and adds pos[t] to every other row.
+ * spec: (B, Fm, Tf) f32; out 16-B aligned; ps*ps % 8 == 0; x, cls, pos 16-B aligned, D % 4 == 0. */
+int mia_ast_patches(const float* spec, int32_t B, int32_t Fm, int32_t Tf, int32_t ps, int32_t st, void* out,
+                    mia_stream_t stream);
+int mia_tokens_fwd_inplace(float* x, const float* cls, const float* pos, int32_t B, int32_t N, int32_t D,
+                           mia_stream_t stream);
+
 /* Elementwise helpers. */
 int mia_cast(const void* src, int32_t sdtype, void* dst, int32_t ddtype, int64_t numel,
              mia_stream_t stream);
