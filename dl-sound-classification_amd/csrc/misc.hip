@@ -579,7 +579,8 @@ extern "C" int64_t mia_adam_workspace_bytes(int32_t ntensors) {
 extern "C" int64_t mia_adam_coef_offset(int32_t ntensors) { return (int64_t)ntensors * ADAM_PARTS * 8; }
 
 extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg, void* const* exp_avg_sq,
-                             void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel, float lr, float beta1,
+                             void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors, int64_t max_numel,
+                             int64_t max_norm_numel, float lr, float beta1,
                              float beta2, float eps, float weight_decay, int32_t step, float clip,
                              float* total_norm_out, void* sqnorm_ws, const void* const* pre_sq,
                              const int64_t* pre_n, const int32_t* steps, mia_stream_t stream) {
@@ -589,7 +590,7 @@ extern "C" int mia_clip_adam(void* const* params, void* const* grads, void* cons
   hipStream_t s = as_stream(stream);
   double* ws = reinterpret_cast<double*>(sqnorm_ws);
   float* coef = reinterpret_cast<float*>(ws + (int64_t)ntensors * ADAM_PARTS);
-  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_numel, 256 * 256)));
+  const int parts = (int)std::min<int64_t>(ADAM_PARTS, std::max<int64_t>(1, cdiv(max_norm_numel, 256 * 256)));
   sqnorm_kernel<<<dim3(parts, ntensors), NT, 0, s>>>(grads, sizes, pre_sq, pre_n, reinterpret_cast<float*>(ws));
   MIA_LAUNCH_CHECK("sqnorm");
   norm_final_kernel<<<1, NF_NT, 0, s>>>(ws, ntensors, parts, clip, total_norm_out, coef);

@@ -106,7 +106,7 @@ SIGNATURES = {
     "mia_soft_ce": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "mia_adam_workspace_bytes": (i64, [i32]),
     "mia_adam_coef_offset": (i64, [i32]),
-    "mia_clip_adam": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp, vp,
+    "mia_clip_adam": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp, vp,
                                 vp, vp]),
     "mia_layernorm_fwd": (C.c_int, [vp, i32, vp, vp, vp, i32, vp, vp, i64, i32, f32, vp]),
     "mia_layernorm_bwd": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp, vp, i64, i32, vp]),

@@ -123,7 +123,8 @@ class FusedAdam(torch.optim.Optimizer):
         with K.probe("optim.step", 0.0, nbytes):
             L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
                                       table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
-                                      max(p.numel() for p in ps),
+                                      max((p.numel() for p, d in zip(ps, deferred) if d is None), default=1),
+                                      max((p.numel() for p, q in zip(ps, pre) if q is None), default=1),
                                       float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
                                       float(grp["weight_decay"]), step, self.clip, tot.data_ptr(), ws.data_ptr(),
                                       table[6].data_ptr() if have_pre else None,

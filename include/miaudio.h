@@ -413,14 +413,17 @@ int mia_soft_ce(const float* logits, const float* y, int32_t B, int32_t C, int32
  * gradient it wrote) instead of re-reading grads[i]; the partials are added in a fixed order.
  * clip <= 0 disables clipping. step is 1-based; steps (optional device int32[n], may be NULL) gives
  * each tensor its own 1-based step for the bias corrections (torch.optim.Adam keeps a step count per
- * parameter; a parameter that had no gradient in some step is behind the others). */
+ * parameter; a parameter that had no gradient in some step is behind the others).
+ * max_numel sizes the update grid (the largest tensor the update pass walks: NULL-gradient tensors
+ * excluded), max_norm_numel the norm grid (the largest tensor whose gradient it reads: pre_sq tensors
+ * excluded); the norm's summation order is a fixed function of max_norm_numel. */
 int64_t mia_adam_workspace_bytes(int32_t ntensors);
 /* byte offset of the device clip coefficient (f32) inside that workspace; a tensor whose grads[] entry is
  * NULL is counted in the norm through pre_sq only and not updated (its update is mia_gemm_adam's) */
 int64_t mia_adam_coef_offset(int32_t ntensors);
 int mia_clip_adam(void* const* params, void* const* grads, void* const* exp_avg,
                   void* const* exp_avg_sq, void* const* shadow_bf16, const int64_t* sizes, int32_t ntensors,
-                  int64_t max_numel, float lr, float beta1, float beta2, float eps,
+                  int64_t max_numel, int64_t max_norm_numel, float lr, float beta1, float beta2, float eps,
                   float weight_decay, int32_t step, float clip, float* total_norm_out,
                   void* sqnorm_ws, const void* const* pre_sq, const int64_t* pre_n, const int32_t* steps,
                   mia_stream_t stream);
