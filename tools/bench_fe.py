@@ -24,11 +24,15 @@ sh = torch.randn(32, generator=g, device=dev)
 bias = torch.randn(64, generator=g, device=dev)
 y2 = torch.empty(B * W2, 64, dtype=torch.bfloat16, device=dev)
 da1 = torch.empty(B * W1, 32, dtype=torch.bfloat16, device=dev)
+dw = torch.empty(64, 512, device=dev)
 runs = {
     "fe_conv2_fwd": lambda: K.fe_conv2_fwd(y1, sc, sh, w0, bias, y2, B, W1, W2),
     "fe_conv2_dgrad": lambda: K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2),
+    "fe_conv2_wgrad": lambda: K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2),
+    "dgrad+wgrad": lambda: (K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2), K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2)),
 }
-byts = {"fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2}
+byts = {"fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2,
+        "fe_conv2_wgrad": (dy2.numel() + y1.numel()) * 2, "dgrad+wgrad": (2 * dy2.numel() + y1.numel() + da1.numel()) * 2}
 flop = 2.0 * B * W2 * 64 * 512
 for name, fn in runs.items():
     for _ in range(3):
@@ -41,4 +45,4 @@ for name, fn in runs.items():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e9:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s", flush=True)
+    print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s", flush=True)
