@@ -220,7 +220,11 @@ class ASTFunction(torch.autograd.Function):
         dx = torch.zeros(Tt, D, dtype=torch.float32, device=dev)
         dx.view(B, N, D)[:, 0] = dxc
         # bf16 mode: a bf16 copy of the residual gradient feeds the next linear backward's GEMMs
-        dxb = K.cast(dx, torch.bfloat16) if cd == L.BF16 else dx
+        if cd == L.BF16:  # only the cls rows are non-zero: a fill, not a cast pass over the whole f32 tensor
+            dxb = torch.zeros(Tt, D, dtype=torch.bfloat16, device=dev)
+            dxb.view(B, N, D)[:, 0] = dxc.to(torch.bfloat16)
+        else:
+            dxb = dx
         dxb2 = torch.empty_like(dxb) if cd == L.BF16 else None
         db_next = None  # column sums of dxb from the LayerNorm backward that wrote it (bf16 mode)
         for i in reversed(range(nb)):
