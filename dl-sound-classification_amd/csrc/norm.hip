@@ -429,32 +429,33 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy,
 // summed per lane in registers, then across the 4 waves through LDS (fixed order, no atomics).
 constexpr int LN_VEC_ROWS = 64;
 
+// lane l holds the PER / 4 groups of 4 consecutive elements d = 4l + 256i (D = 64 * PER, a multiple of
+// 256): every load / store instruction of the wave covers one contiguous 1 KB (f32) / 512 B (bf16) run
 template <int PER>
-__device__ __forceinline__ void ldv(const void* p, int dt, int64_t off, float* f) {
+__device__ __forceinline__ void ldv4(const void* p, int dt, int64_t rowoff, int lane, float* f) {
 #pragma unroll
   for (int q = 0; q < PER / 4; ++q) {
+    const int64_t off = rowoff + 4 * lane + 256 * q;
     if (dt == MIA_BF16) {
-      const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(p) + off + 4 * q);
-      f[4 * q] = __uint_as_float(u.x << 16); f[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
-      f[4 * q + 2] = __uint_as_float(u.y << 16); f[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(p) + off);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f[4 * q + k] = (float)v[k];
     } else {
-      const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + off + 4 * q);
+      const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + off);
       f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
     }
   }
 }
 template <int PER>
-__device__ __forceinline__ void stv(void* p, int dt, int64_t off, const float* f) {
+__device__ __forceinline__ void stv4(void* p, int dt, int64_t rowoff, int lane, const float* f) {
 #pragma unroll
   for (int q = 0; q < PER / 4; ++q) {
+    const int64_t off = rowoff + 4 * lane + 256 * q;
     if (dt == MIA_BF16) {
-      const bf16 a = (bf16)f[4 * q], b = (bf16)f[4 * q + 1], c = (bf16)f[4 * q + 2], d = (bf16)f[4 * q + 3];
-      uint2 u;
-      u.x = (uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16);
-      u.y = (uint32_t)__builtin_bit_cast(unsigned short, c) | ((uint32_t)__builtin_bit_cast(unsigned short, d) << 16);
-      *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(p) + off + 4 * q) = u;
+      const bf16x4 v = {(bf16)f[4 * q], (bf16)f[4 * q + 1], (bf16)f[4 * q + 2], (bf16)f[4 * q + 3]};
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p) + off) = v;
     } else {
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + off + 4 * q) =
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + off) =
           make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
     }
   }
@@ -469,13 +470,12 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
   // CS: also the column sums of the stored dx2 values (the next linear's bias gradient); partial
   // rows are then [blk][3][D] instead of [blk][2][D] (and the LDS plane for them exists only then)
   constexpr int D = 64 * PER;
+  static_assert(D % 256 == 0, "ln_bwd_vec: D must be a multiple of 256");
   constexpr int nq = CS ? 3 : 2;
   __shared__ float red[4][nq][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int d0 = lane * PER;
   float gg[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) gg[i] = g[d0 + i];
+  ldv4<PER>(g, MIA_F32, 0, lane, gg);
   float ag[PER], ab[PER], ac[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; ac[i] = 0.f; }
@@ -483,8 +483,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
   for (int64_t row = r0 + wave; row < r0 + LN_VEC_ROWS && row < rows; row += 4) {
     const float mu = mean[row], rs = rstd[row];
     float dv[PER], xh[PER];
-    ldv<PER>(dy, dydt, row * D + d0, dv);
-    ldv<PER>(x, xdt, row * D + d0, xh);
+    ldv4<PER>(dy, dydt, row * D, lane, dv);
+    ldv4<PER>(x, xdt, row * D, lane, xh);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -502,12 +502,12 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
     for (int i = 0; i < PER; ++i) o[i] = rs * (dv[i] - s1 - xh[i] * s2);
     if (accumulate) {
       float old[PER];
-      ldv<PER>(dx, dxdt, row * D + d0, old);
+      ldv4<PER>(dx, dxdt, row * D, lane, old);
 #pragma unroll
       for (int i = 0; i < PER; ++i) o[i] += old[i];
     }
-    stv<PER>(dx, dxdt, row * D + d0, o);
-    if (dx2) stv<PER>(dx2, dx2dt, row * D + d0, o);
+    stv4<PER>(dx, dxdt, row * D, lane, o);
+    if (dx2) stv4<PER>(dx2, dx2dt, row * D, lane, o);
     if constexpr (CS) {
 #pragma unroll
       for (int i = 0; i < PER; ++i) ac[i] += dx2dt == MIA_BF16 ? (float)(bf16)o[i] : o[i];
@@ -515,9 +515,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    red[wave][0][d0 + i] = ag[i];
-    red[wave][1][d0 + i] = ab[i];
-    if constexpr (CS) red[wave][nq - 1][d0 + i] = ac[i];
+    const int d = 4 * lane + 256 * (i >> 2) + (i & 3);
+    red[wave][0][d] = ag[i];
+    red[wave][1][d] = ab[i];
+    if constexpr (CS) red[wave][nq - 1][d] = ac[i];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nq * D; i += NT) {
@@ -714,7 +715,8 @@ static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, in
   MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_bwd: D must be <= 1024");
   hipStream_t s = as_stream(stream);
   unsigned nb;
-  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0;
+  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx) |
+                    reinterpret_cast<uintptr_t>(dx2) | reinterpret_cast<uintptr_t>(gamma)) & 15) == 0;
   if (D == 768 && al) {
     nb = (unsigned)cdiv(rows, LN_VEC_ROWS);
     if (dx2_colsum)

@@ -28,7 +28,7 @@ rstd = torch.empty(R, device=dev)
 libs = {"product": L.load()}
 for path in filter(None, os.environ.get("LN_LIBS", "").split(",")):
     lib = C.CDLL(str(REPO / path))
-    for n in ("mia_layernorm_fwd", "mia_layernorm_fwd_mx"):
+    for n in ("mia_layernorm_fwd", "mia_layernorm_fwd_mx", "mia_layernorm_bwd_colsum"):
         getattr(lib, n).argtypes = L.SIGNATURES[n][1]
     libs[Path(path).stem] = lib
 s = L.stream_ptr()
@@ -44,23 +44,40 @@ def fwd_mx(lib):
                                      q.data_ptr(), qs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R, D, 1e-6, s), "ln_mx")
 
 
+dyb = (torch.randn(R, D, generator=g, device=dev) * 0.1).to(torch.bfloat16)
+dx = torch.zeros(R, D, device=dev)
+dx2 = torch.empty(R, D, dtype=torch.bfloat16, device=dev)
+dgam, dbet, dcs = (torch.empty(D, device=dev) for _ in range(3))
+part = torch.empty(int(libs["product"].mia_layernorm_partial_bytes(R, D)), dtype=torch.uint8, device=dev)
+
+
+def bwd(lib):
+    L.check(lib.mia_layernorm_bwd_colsum(dyb.data_ptr(), L.BF16, x.data_ptr(), L.F32, gamma.data_ptr(), mean.data_ptr(),
+                                         rstd.data_ptr(), dx.data_ptr(), L.F32, 1, dx2.data_ptr(), L.BF16,
+                                         dgam.data_ptr(), dbet.data_ptr(), dcs.data_ptr(), part.data_ptr(), R, D, s),
+            "ln_bwd")
+
+
 ref = None
 for name, lib in libs.items():
     fwd_mx(lib)
+    dx.zero_()
+    bwd(lib)
     torch.cuda.synchronize()
-    got = (y.clone(), q.clone(), qs.clone(), mean.clone(), rstd.clone())
+    got = (y.clone(), q.clone(), qs.clone(), mean.clone(), rstd.clone(), dx.clone(), dgam.clone(), dcs.clone())
     if ref is None:
         ref = got
     else:
         dy = (got[0].float() - ref[0].float()).abs().max().item()
         print(f"{name}: bf16 out max |diff| {dy:.3g}, fp8 bytes differing {int((got[1] != ref[1]).sum())}, "
               f"scales differing {int((got[2] != ref[2]).sum())}, mean max |diff| "
-              f"{(got[3] - ref[3]).abs().max().item():.3g}", flush=True)
+              f"{(got[3] - ref[3]).abs().max().item():.3g}; bwd dx / dgamma / colsum equal: "
+              f"{[torch.equal(a, b) for a, b in zip(got[5:], ref[5:])]}", flush=True)
 byts = R * D * (4 + 2)
-times = {(n, k): [] for n in libs for k in ("ln", "ln_mx")}
+times = {(n, k): [] for n in libs for k in ("ln", "ln_mx", "ln_bwd")}
 for _ in range(3):
     for name, lib in libs.items():
-        for kind, fn in (("ln", fwd), ("ln_mx", fwd_mx)):
+        for kind, fn in (("ln", fwd), ("ln_mx", fwd_mx), ("ln_bwd", bwd)):
             fn(lib)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -73,4 +90,6 @@ for _ in range(3):
 for (name, kind), ts in times.items():
     ms = min(ts)
     b = byts + (R * D + R * D // 32 if kind == "ln_mx" else 0)
+    if kind == "ln_bwd":
+        b = R * D * (2 + 4 + 4 + 4 + 2)  # dy bf16, x, dx read + write, dx2 bf16
     print(f"{name:14s} {kind:6s} {ms:7.3f} ms {b / ms / 1e6:7.1f} GB/s", flush=True)
