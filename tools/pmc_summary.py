@@ -41,6 +41,7 @@ def main():
     dst = Path(sys.argv[2])
     marker = sys.argv[3] if len(sys.argv) > 3 else "adam_kernel"
     trace = list(csv.DictReader(open(d / "trace" / "run_kernel_trace.csv")))
+    trace.sort(key=lambda r: int(r["Dispatch_Id"]))  # the file is in completion order, not dispatch order
     dur = defaultdict(list)
     grid = {}
     for r in last_step(trace, marker):

@@ -4,6 +4,7 @@ import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Dispatch_Id"]))  # the file is in completion order, not dispatch order
 marker = sys.argv[2] if len(sys.argv) > 2 else "adam_kernel"
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 s, e = idx[-2] + 1, idx[-1] + 1
