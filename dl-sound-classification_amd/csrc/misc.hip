@@ -305,16 +305,13 @@ __global__ void tokens_fwd_kernel(const float* __restrict__ patches, const float
 // bf16 mode: the patch GEMM wrote token rows (x[b][t] = bias + patch t-1 of clip b . W for t >= 1, the
 // cls rows hold the bias of a zero patch); add the positional rows, cls token at t = 0, in place
 __global__ void tokens_fwd_inplace_kernel(float4* __restrict__ x, const float4* __restrict__ cls,
-                                          const float4* __restrict__ pos, int B, int N, int D4) {
-  const int64_t total = (int64_t)B * N * D4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int d = (int)(i % D4);
-    const int tkn = (int)((i / D4) % N);
-    const float4 p = pos[(int64_t)tkn * D4 + d];
-    float4 v = tkn == 0 ? cls[d] : x[i];
-    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-    x[i] = v;
-  }
+                                          const float4* __restrict__ pos, int N, int D4) {
+  const int64_t row = blockIdx.x;  // one token row per block, D4 threads
+  const int tkn = (int)(row % N), d = threadIdx.x;
+  const float4 p = pos[(int64_t)tkn * D4 + d];
+  float4 v = tkn == 0 ? cls[d] : x[row * D4 + d];
+  v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+  x[row * D4 + d] = v;
 }
 
 // The patch matrix of the AST patch embedding (Conv2d(1, D, ps, stride st) over the (B, Fm, Tf)
@@ -357,6 +354,25 @@ __global__ void tokens_bwd_kernel(const float* __restrict__ dout, float* __restr
       const float v = dout[((int64_t)b * (Np + 1) + tkn) * D + d];
       s += v;
       if (tkn > 0 && dpatches) dpatches[((int64_t)b * Np + tkn - 1) * D + d] = v;
+    }
+    if (dpos) dpos[i] = s;
+    if (tkn == 0 && dcls) dcls[d] = s;
+  }
+}
+
+// the same with 16-B accesses (4 consecutive d per thread; the per-element sums keep their order over b)
+__global__ void tokens_bwd_vec_kernel(const float4* __restrict__ dout, float4* __restrict__ dpatches,
+                                      float4* __restrict__ dcls, float4* __restrict__ dpos, int B, int Np, int D4) {
+  const int64_t total = (int64_t)(Np + 1) * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D4);
+    const int tkn = (int)(i / D4);
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int b = 0; b < B; ++b) {
+      const float4 v = dout[((int64_t)b * (Np + 1) + tkn) * D4 + d];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      if (tkn > 0 && dpatches) dpatches[((int64_t)b * Np + tkn - 1) * D4 + d] = v;
     }
     if (dpos) dpos[i] = s;
     if (tkn == 0 && dcls) dcls[d] = s;
@@ -642,9 +658,9 @@ extern "C" int mia_tokens_fwd_inplace(float* x, const float* cls, const float* p
   MIA_CHECK_ARG(x && cls && pos && B > 0 && N > 1 && D > 0 && D % 4 == 0, "tokens_fwd_inplace: args");
   MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(cls) | reinterpret_cast<uintptr_t>(pos)) & 15) == 0,
                 "tokens_fwd_inplace: x / cls / pos must be 16-byte aligned");
-  tokens_fwd_inplace_kernel<<<blocks_for((int64_t)B * N * (D / 4)), 256, 0, as_stream(stream)>>>(
-      reinterpret_cast<float4*>(x), reinterpret_cast<const float4*>(cls), reinterpret_cast<const float4*>(pos), B, N,
-      D / 4);
+  MIA_CHECK_ARG(D / 4 <= 1024 && (int64_t)B * N < (1ll << 31), "tokens_fwd_inplace: D <= 4096, B*N < 2^31");
+  tokens_fwd_inplace_kernel<<<(unsigned)((int64_t)B * N), D / 4, 0, as_stream(stream)>>>(
+      reinterpret_cast<float4*>(x), reinterpret_cast<const float4*>(cls), reinterpret_cast<const float4*>(pos), N, D / 4);
   MIA_LAUNCH_CHECK("tokens_fwd_inplace");
   return 0;
 }
@@ -664,7 +680,14 @@ extern "C" int mia_ast_patches(const float* spec, int32_t B, int32_t Fm, int32_t
 extern "C" int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, float* dpos, int32_t B, int32_t Np,
                               int32_t D, mia_stream_t stream) {
   MIA_CHECK_ARG(dout && B > 0 && Np > 0 && D > 0, "tokens_bwd: args");
-  tokens_bwd_kernel<<<blocks_for((int64_t)(Np + 1) * D), 256, 0, as_stream(stream)>>>(dout, dpatches, dcls, dpos, B, Np, D);
+  const bool vec = D % 4 == 0 && ((reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dpatches) |
+                                   reinterpret_cast<uintptr_t>(dpos) | reinterpret_cast<uintptr_t>(dcls)) & 15) == 0;
+  if (vec)
+    tokens_bwd_vec_kernel<<<blocks_for((int64_t)(Np + 1) * (D / 4)), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(dout), reinterpret_cast<float4*>(dpatches), reinterpret_cast<float4*>(dcls),
+        reinterpret_cast<float4*>(dpos), B, Np, D / 4);
+  else
+    tokens_bwd_kernel<<<blocks_for((int64_t)(Np + 1) * D), 256, 0, as_stream(stream)>>>(dout, dpatches, dcls, dpos, B, Np, D);
   MIA_LAUNCH_CHECK("tokens_bwd");
   return 0;
 }

@@ -83,8 +83,12 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const void* __restrict__ x
     for (int i = 0; i < 4; ++i) { a0 |= (uint32_t)arg[i] << (8 * i); a1 |= (uint32_t)arg[i + 4] << (8 * i); }
     *reinterpret_cast<uint2*>(argmax + aoff) = make_uint2(a0, a1);
     if (win) store8(win, dtype, aoff, raw);  // the winner's raw x (exact: x's own dtype) for the backward
+    if (layout == 0) {
+      store8(out, dtype, aoff, best);  // NHWC: the 8 channels are one 16-B (bf16) / 32-B (f32) run
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) st_elem(out, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C), best[i]);
+      for (int i = 0; i < 8; ++i) st_elem(out, dtype, out_index(layout, b, oy, ox, cg * 8 + i, OH, OW, C), best[i]);
+    }
   }
 }
 
@@ -548,6 +552,8 @@ extern "C" int mia_pool_fwd(const void* x, int32_t dtype, int32_t n, int32_t h, 
                             uint8_t* argmax, void* win, mia_stream_t stream) {
   MIA_CHECK_ARG(x && out && argmax, "pool_fwd: null pointer");
   MIA_CHECK_ARG(!win || (reinterpret_cast<uintptr_t>(win) & 15) == 0, "pool_fwd: win alignment");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(x) | (out_layout == 0 ? reinterpret_cast<uintptr_t>(out) : 0)) & 15) == 0,
+                "pool_fwd: x (and an NHWC out) must be 16-byte aligned");
   MIA_CHECK_ARG(c % 8 == 0 && kh > 0 && kw > 0 && kh * kw <= 256 && h >= kh && w >= kw, "pool_fwd: bad geometry");
   MIA_CHECK_ARG(out_layout >= 0 && out_layout <= 2 && (out_layout != 1 || h / kh == 1), "pool_fwd: bad layout");
   MIA_CHECK_ARG((int64_t)n * h * w * (c / 8) < (1ll << 31), "pool_fwd: too many elements for 32-bit indexing");
