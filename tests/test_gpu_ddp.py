@@ -6,7 +6,9 @@ a warm-up step, a plain step whose gradients are the
 reference, then the same step under GradAllReducer (src/training/ddp.py), whose buckets leave from
 inside EnvNetFunction.backward through ``_grad_ready`` on the side stream (the FC gradients; FC1's
 weight gradient as 16 row chunks through ``_grad_chunk_ready``, one all-reduce per chunk GEMM) and
-from ``finish()`` (the rest).  The kernels are deterministic, so every averaged gradient must equal
+from ``finish()`` (the rest).  The parameters are marked for FusedAdam and the batch is one the
+single-process path defers FC1's weight gradient at: under the reducer it must still be materialised
+and exchanged (its all-reduce needs it).  The kernels are deterministic, so every averaged gradient must equal
 (g_0 + g_1) * 0.5 of the two ranks' plain gradients bit for bit (Lightning DDP's mean over ranks,
 reference base_training.yaml:45-51)."""
 import os
@@ -32,7 +34,7 @@ def _worker(rank, world, port, q):
         from tests._util import envnet_with_hash_params
         dev = torch.device("cuda", 0)
         m = envnet_with_hash_params(dev, compute_dtype="bf16").train()
-        B = 2
+        B = 64  # a batch the single-process path would defer FC1's weight gradient at (B % 64 == 0)
         x = torch.from_numpy(synth_waveform(31 + rank, B, 220_500)[:, None, :]).to(dev)
         y = torch.zeros(B, 50, device=dev)
         y[0, 3 + rank] = 1.0
@@ -47,6 +49,8 @@ def _worker(rank, world, port, q):
         step()
         step()
         plain = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        from src.training.optim import FusedAdam
+        FusedAdam(m.parameters(), lr=1e-3)  # marks the parameters: alone, FC1's gradient would be deferred
         red = GradAllReducer(m, world)
         step()
         red.finish()
