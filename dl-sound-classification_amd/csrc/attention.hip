@@ -387,7 +387,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
       vdma.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
     }
     fwd_qk(s, Ks[P], qf, one, a.mrow, lane);
+    __builtin_amdgcn_s_setprio(1);  // the softmax's VALU issues ahead of the co-resident waves' MFMA streams
     fwd_softmax<decltype(first)::value, decltype(tail)::value>(s, a, pf, j * 64, N, lane);
+    __builtin_amdgcn_s_setprio(0);
     fwd_pv(a, Vs[P], pf, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j + 1's pieces have landed
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -1,7 +1,9 @@
 """Time the flash-attention kernels on the AST shape (1645 tokens, 12 heads, d 64), optionally A/B against
 an experiment build of the same C ABI (ATTN_LIBS=path1,path2: each a shared library exporting mia_attn_fwd /
 mia_attn_bwd, e.g. tools/probe/libattn_ref.so built from a previous attention.hip), interleaved rounds in
-one process, outputs checked equal to the product library's.
+one process, outputs checked equal to the product library's.  Build a reference with attention.hip's
+own flags from the package Makefile (-mllvm -amdgpu-mfma-vgpr-form=1 -fno-slp-vectorize): without them the
+same source runs ~5 % slower and the A/B measures the flags.
     BATCH=256 python tools/bench_attn.py"""
 import ctypes as C
 import os
