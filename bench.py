@@ -227,8 +227,13 @@ def pmc_traffic(model: str, ks: dict, tag: str | None = None):
             return None, {"file": files[-1].name, "match": None}
         per = sum(e["hbm_bytes"] * e["launches_per_step"] for e in sel.values()) / max(ks["launches_per_step"], 1)
         avg = sum(e["avg_ms"] * e["launches_per_step"] for e in sel.values()) / max(ks["launches_per_step"], 1)
-        return per, {"file": files[-1].name, "kernels": sorted(sel), "rocprof_ms_per_launch": round(avg, 4),
-                     "live_vs_rocprof": round(abs(avg - ks["ms"]) / ks["ms"], 4)}
+        rel = abs(avg - ks["ms"]) / ks["ms"]
+        src = {"file": files[-1].name, "kernels": sorted(sel), "rocprof_ms_per_launch": round(avg, 4),
+               "live_vs_rocprof": round(rel, 4)}
+        if rel >= 0.10:  # the same 10 % agreement rule as a single-kernel tag: a disagreeing profile's bytes
+            src["match"] = None  # describe some other run, so no traffic is attached
+            return None, src
+        return per, src
     if hints and any(hints[0] in n for n in table):
         table = {n: e for n, e in table.items() if hints[0] in n}
     best = None
@@ -255,7 +260,8 @@ def roofline(model: str, tag: str, ks: dict, peak_tf: float):
     else:
         ach, peak, unit = ks["tflops"], peak_tf, "TFLOP/s"
     return {"bound": "hbm" if tag in HBM_TAGS else "mfma", "kernel": f"{kname} [{tag}]", "achieved": round(ach, 2),
-            "peak": peak, "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+            "peak": peak, "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic,
+            "live_vs_rocprof": (tsrc or {}).get("live_vs_rocprof"), "traffic_source": tsrc,
             "algorithmic_per_launch": {"flop": ks["flop"], "bytes": ks["bytes"]},
             "ms_per_launch": round(ks["ms"], 4), "launches_per_step": ks["launches_per_step"]}
 

@@ -337,7 +337,7 @@ template <bool MX>
 __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                           float* __restrict__ lse, int N, int H, int nqb,
                                                           float scale_log2, uint8_t* __restrict__ q8,
-                                                          uint8_t* __restrict__ s8) {
+                                                          uint8_t* __restrict__ s8, bf16* __restrict__ qs_out) {
   __shared__ __attribute__((aligned(1024))) bf16 Ks[3][64 * 64];
   __shared__ __attribute__((aligned(1024))) bf16 Vs[3][64 * 64];
   const int t = threadIdx.x, lane = t & 63;
@@ -361,6 +361,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, q < N);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
+  }
+  if (qs_out != nullptr && q < N) {  // Q' for the backward (its prep then skips it): row (b, q, h), d = 16 ks + 8 (lane >> 5)..
+    bf16* qrow = qs_out + (((int64_t)b * N + q) * H + hd) * D + 8 * (lane >> 5);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) *reinterpret_cast<bf16x8*>(qrow + 16 * ks) = qf[ks];
   }
   if (ntiles > 1) {
     kdma.issue(Ks[1], tile_bytes, wave);
@@ -446,8 +451,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     if (lane < 32) lse[(int64_t)bh * N + q] = (a.mb + log2f(lt)) / LOG2E;
   }
 }
-template __global__ void attn_fwd_kernel<false>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*);
-template __global__ void attn_fwd_kernel<true>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*);
+template __global__ void attn_fwd_kernel<false>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*,
+                                                bf16*);
+template __global__ void attn_fwd_kernel<true>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*,
+                                               bf16*);
 
 // ------------------------------------------------------------------------------ backward
 // Both backward kernels recompute P from the SAME MFMA operands the forward used (Q' = bf16(q * scale
@@ -472,7 +479,7 @@ __device__ __forceinline__ void split3(float x, bf16x8& f) {
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ out,
                                                             const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                             bf16* __restrict__ qs, bf16* __restrict__ frag, int B,
-                                                            int N, int H, float scale_log2) {
+                                                            int N, int H, float scale_log2, int write_qs) {
   const int64_t rows = (int64_t)B * N * H;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
   const int part = threadIdx.x & 7;
@@ -482,15 +489,16 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16* __restri
   const int q = (int)(bq % N), b = (int)(bq / N);
   const bf16x8 o = *reinterpret_cast<const bf16x8*>(out + i * D + part * 8);
   const bf16x8 g = *reinterpret_cast<const bf16x8*>(dout + i * D + part * 8);
-  const bf16x8 qv = *reinterpret_cast<const bf16x8*>(qkv + (bq * 3 * H + hd) * D + part * 8);
   float s = 0.f;
-  bf16x8 qsc;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    s = fmaf((float)o[j], (float)g[j], s);
-    qsc[j] = (bf16)((float)qv[j] * scale_log2);
+  for (int j = 0; j < 8; ++j) s = fmaf((float)o[j], (float)g[j], s);
+  if (write_qs) {  // (skipped when the forward wrote Q': mia_attn_fwd_save_q)
+    const bf16x8 qv = *reinterpret_cast<const bf16x8*>(qkv + (bq * 3 * H + hd) * D + part * 8);
+    bf16x8 qsc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qsc[j] = (bf16)((float)qv[j] * scale_log2);
+    *reinterpret_cast<bf16x8*>(qs + i * D + part * 8) = qsc;
   }
-  *reinterpret_cast<bf16x8*>(qs + i * D + part * 8) = qsc;
   s += __shfl_xor(s, 1);
   s += __shfl_xor(s, 2);
   s += __shfl_xor(s, 4);
@@ -924,7 +932,7 @@ extern "C" int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtyp
   const int nqb = (int)cdiv(N, FWD_Q);
   MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd: grid too large");
   attn_fwd_kernel<false><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
-      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, nullptr, nullptr);
+      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, nullptr, nullptr, nullptr);
   MIA_LAUNCH_CHECK("attn_fwd");
   return 0;
 }
@@ -938,7 +946,7 @@ extern "C" int mia_attn_fwd_mx(const void* qkv, void* out, float* lse, void* q8,
   const int nqb = (int)cdiv(N, FWD_Q);
   MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd_mx: grid too large");
   attn_fwd_kernel<true><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
-      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, (uint8_t*)q8, (uint8_t*)s8);
+      (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, (uint8_t*)q8, (uint8_t*)s8, nullptr);
   MIA_LAUNCH_CHECK("attn_fwd_mx");
   return 0;
 }
@@ -949,9 +957,9 @@ extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_
   return rows * D * 2 + rows * 32;        // Q' + fragment rows
 }
 
-extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
-                            void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
-                            mia_stream_t stream) {
+static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                         void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale, int q_ready,
+                         mia_stream_t stream) {
   MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && work, "attn_bwd: null pointer");
   MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_bwd: bad shape");
   hipStream_t s = as_stream(stream);
@@ -980,7 +988,7 @@ extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, 
   const float scale_log2 = scale * LOG2E;
   attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
                                                                      (const bf16*)dout, lse, qs, frag, B, N, H,
-                                                                     scale_log2);
+                                                                     scale_log2, q_ready ? 0 : 1);
   MIA_LAUNCH_CHECK("attn_bwd_prep");
   const int nkb = (int)cdiv(N, BWD_K), nqb = (int)cdiv(N, BWD_Q);
   attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag,
@@ -990,4 +998,37 @@ extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, 
                                                              N, H, nqb, scale, scale_log2);
   MIA_LAUNCH_CHECK("attn_bwd_dq");
   return 0;
+}
+
+extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                            void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
+                            mia_stream_t stream) {
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, dtype, B, N, H, scale, 0, stream);
+}
+
+// bf16 forward that also writes Q' (the backward's scaled query operand) into the backward workspace
+// `work` (mia_attn_bwd_workspace_bytes); q8 / s8 non-null = the MX-fp8 form (mia_attn_fwd_mx)
+extern "C" int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void* q8, void* s8, void* work, int32_t B,
+                                   int32_t N, int32_t H, float scale, mia_stream_t stream) {
+  MIA_CHECK_ARG(qkv && out && lse && work && (!q8 == !s8), "attn_fwd_save_q: null pointer");
+  MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_fwd_save_q: bad shape");
+  MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_fwd_save_q: one sequence must span < 2 GiB");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(work) & 15) | (q8 ? reinterpret_cast<uintptr_t>(q8) & 3 : 0)) == 0,
+                "attn_fwd_save_q: work must be 16-B and q8 4-B aligned");
+  const int nqb = (int)cdiv(N, FWD_Q);
+  MIA_CHECK_ARG((int64_t)nqb * B * H < (1ll << 31), "attn_fwd_save_q: grid too large");
+  if (q8)
+    attn_fwd_kernel<true><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
+        (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, (uint8_t*)q8, (uint8_t*)s8, (bf16*)work);
+  else
+    attn_fwd_kernel<false><<<(unsigned)(nqb * B * H), 256, 0, as_stream(stream)>>>(
+        (const bf16*)qkv, (bf16*)out, lse, N, H, nqb, scale * LOG2E, nullptr, nullptr, (bf16*)work);
+  MIA_LAUNCH_CHECK("attn_fwd_save_q");
+  return 0;
+}
+
+// the bf16 backward when the forward already wrote Q' into `work` (mia_attn_fwd_save_q)
+extern "C" int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                                    void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream) {
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, stream);
 }

@@ -725,6 +725,8 @@ int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
     return -1;
   const bool bf = E.dtype == MIA_BF16, f32 = E.dtype == MIA_F32;
   if ((E.ldc & 3) || E.ldc < N || (reinterpret_cast<uintptr_t>(E.ptr) & (bf ? 7 : 15)) != 0) return -1;
+  // bf16 outputs leave the LDS image as 16-B pieces (8 columns) guarded by n < N only
+  if (bf && N % 8) return -1;
   if (E.bias && (reinterpret_cast<uintptr_t>(E.bias) & 15)) return -1;
   const bool aux_ok = E.aux && aligned16(E.aux) && (E.ldaux & 3) == 0 && E.ldaux >= N;
   switch (E.act) {
@@ -738,7 +740,8 @@ int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
 }
 
 // This kernel takes dense bf16 GEMMs big enough to fill the chip with 256 x 256 tiles (AST token
-// counts, or a weight gradient over them): A/B without pre-op, 16-B aligned, ld % 8 == 0, N % 4 == 0,
+// counts, or a weight gradient over them): A/B without pre-op, 16-B aligned, ld % 8 == 0, N % 4 == 0
+// (N % 8 == 0 for a bf16 output),
 // K % 64 == 0 where K is the contiguous dimension (KC), any K where it is the row index (RC).
 bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
            int compute) {
@@ -864,7 +867,8 @@ extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, 
   MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(a) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(a_scales) & 3) == 0 && (reinterpret_cast<uintptr_t>(b_scales) & 3) == 0,
                 "gemm_mxfp8: operands 16-B and scales 4-B aligned");
-  MIA_CHECK_ARG(N % 4 == 0 && cdiv(M, MG_BM) * cdiv(N, MG_BN) < (1ll << 24), "gemm_mxfp8: N must be a multiple of 4");
+  MIA_CHECK_ARG(N % 4 == 0 && (E->dtype != MIA_BF16 || N % 8 == 0) && cdiv(M, MG_BM) * cdiv(N, MG_BN) < (1ll << 24),
+                "gemm_mxfp8: N must be a multiple of 4 (of 8 for a bf16 output)");
   const int epi = mgemm::mg_epi_kind(*E, N);
   MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_ADD_AUX,
                 "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE / f32 residual (row-major, aligned)");

@@ -667,8 +667,9 @@ extern "C" int mia_tokens_fwd_inplace(float* x, const float* cls, const float* p
 
 extern "C" int mia_ast_patches(const float* spec, int32_t B, int32_t Fm, int32_t Tf, int32_t ps, int32_t st, void* out,
                                mia_stream_t stream) {
-  MIA_CHECK_ARG(spec && out && B > 0 && ps > 0 && st > 0 && Fm >= ps && Tf >= ps && (ps * ps) % 8 == 0,
-                "ast_patches: args");
+  // each thread's 8 consecutive k stay in one patch row (k0 = 8c, kx = k0 mod ps): ps % 8 == 0
+  MIA_CHECK_ARG(spec && out && B > 0 && ps > 0 && st > 0 && Fm >= ps && Tf >= ps && ps % 8 == 0,
+                "ast_patches: args (ps must be a multiple of 8)");
   MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "ast_patches: out must be 16-byte aligned");
   const int gh = (Fm - ps) / st + 1, gw = (Tf - ps) / st + 1, N = gh * gw + 1;
   ast_patches_kernel<<<blocks_for((int64_t)B * N * (ps * ps / 8)), 256, 0, as_stream(stream)>>>(

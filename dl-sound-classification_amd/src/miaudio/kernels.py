@@ -129,6 +129,25 @@ def defer_weight_grad(param: torch.Tensor, A: L.MiaOperand, B: L.MiaOperand, M: 
     param._mia_deferred = dict(A=A, B=B, M=M, N=N, K=K, sq=sq, keep=keep)
 
 
+def defers_to_fused_adam(p: torch.Tensor) -> bool:
+    """True while the FusedAdam that last took ``p`` is alive (src/training/optim.py keeps a weak reference
+    on the parameter): only then may a model defer ``p``'s weight gradient to the optimizer step."""
+    ref = getattr(p, "_mia_fused_adam", None)
+    return callable(ref) and ref() is not None
+
+
+def materialise_deferred_grad(param: torch.Tensor) -> None:
+    """Write a pending deferred weight gradient (defer_weight_grad) into ``param.grad`` with the same GEMM
+    main loop, for an optimizer that does not fuse it."""
+    d = getattr(param, "_mia_deferred", None)
+    if d is None:
+        return
+    dW = torch.empty(d["M"], d["N"], dtype=torch.float32, device=param.device)
+    gemm(d["A"], d["B"], epilogue(dW, d["N"]), d["M"], d["N"], d["K"], L.BF16)
+    param._mia_deferred = None
+    param.grad = dW.view_as(param) if param.grad is None else param.grad.add_(dW.view_as(param))
+
+
 def tag_sqsum(param: torch.Tensor, grad: torch.Tensor, buf: torch.Tensor) -> None:
     """Record on ``param`` that ``buf`` holds the per-tile sums of squares of the gradient ``grad``, so
     FusedAdam's clip-norm pass reads the slots instead of the tensor.  The tag lives on the parameter

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch
 
 PKG_ROOT = Path(__file__).resolve().parents[2]
-LIB_PATH = Path(os.environ.get("MIAUDIO_LIB", PKG_ROOT / "lib" / "libmiaudio.so"))
+LIB_PATH = Path(os.environ.get("MIAUDIO_LIB") or PKG_ROOT / "lib" / "libmiaudio.so")
 
 F32, BF16, U8 = 0, 1, 2
 # model compute mode (not a tensor dtype): bf16 compute with the AST block linears' forward GEMMs on MX-fp8
@@ -116,6 +116,8 @@ SIGNATURES = {
     "mia_attn_fwd": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_workspace_bytes": (C.c_int64, [i32, i32, i32, i32]),
+    "mia_attn_fwd_save_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
+    "mia_attn_bwd_saved_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_tokens_fwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_tokens_bwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_ast_patches": (C.c_int, [vp, i32, i32, i32, i32, i32, vp, vp]),

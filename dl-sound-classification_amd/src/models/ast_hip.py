@@ -69,6 +69,9 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
            K.epilogue(out, Nf, act=act, bias=bias, aux=aux, ldaux=Nf), M, Nf, Kf, cd, tag=tag)
 
 
+ATTN_SAVE_Q = True  # bf16 training: the attention forward writes Q' for the backward (mia_attn_fwd_save_q)
+
+
 def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None,
                 dx_colsum=None):
     """dW = dy^T x (f32), db = colsum(dy) (unless the producer of dy already summed it), dx = dy @ W
@@ -112,10 +115,11 @@ class ASTFunction(torch.autograd.Function):
         pw, pb, cls, pos = params[0], params[1], params[2], params[3]
         # patch embedding: Conv2d(1, D, 16, stride 10).  bf16: the patch matrix in token order (zero cls
         # rows, mia_ast_patches) through the dense 256x256 GEMM straight into the token rows of x, then the
-        # cls / positional rows in place; f32: an implicit GEMM over the spectrogram (exact-f32 MFMA)
+        # cls / positional rows in place; f32 (or a patch size that is not a multiple of 8, which the patch
+        # matrix kernel cannot take): an implicit GEMM over the spectrogram
         x = torch.empty(Tt, D, dtype=torch.float32, device=dev)
         pmat = None
-        if cd == L.BF16:
+        if cd == L.BF16 and ps % 8 == 0:
             pmat = torch.empty(Tt, ps * ps, dtype=torch.bfloat16, device=dev)
             L.check(L.load().mia_ast_patches(spec.data_ptr(), B, Fm, Tf, ps, st, pmat.data_ptr(), L.stream_ptr()),
                     "mia_ast_patches")
@@ -156,8 +160,19 @@ class ASTFunction(torch.autograd.Function):
             a = torch.empty(Tt, D, dtype=tdt, device=dev)
             aq = K.mx_empty(Tt, D, dev) if mx else None
             lse = torch.empty(B, Hh, N, dtype=torch.float32, device=dev)
+            # bf16 training: the forward also writes Q' (the scaled query operand) into the backward's
+            # attention workspace, so the backward's prep pass neither re-reads q nor rewrites Q'
+            aw = None
+            if cd == L.BF16 and ATTN_SAVE_Q and any(ctx.needs_input_grad):
+                aw = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8,
+                                 device=dev)
             with K.probe("attn.fwd", 4.0 * B * Hh * N * N * (D // Hh), (qkv.numel() + a.numel()) * qkv.element_size()):
-                if mx:
+                if aw is not None:
+                    L.check(L.load().mia_attn_fwd_save_q(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(),
+                                                         aq.q.data_ptr() if mx else None,
+                                                         aq.scales.data_ptr() if mx else None, aw.data_ptr(), B, N,
+                                                         Hh, scale, L.stream_ptr()), "mia_attn_fwd_save_q")
+                elif mx:
                     L.check(L.load().mia_attn_fwd_mx(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(), aq.q.data_ptr(),
                                                      aq.scales.data_ptr(), B, N, Hh, scale, L.stream_ptr()),
                             "mia_attn_fwd_mx")
@@ -175,7 +190,7 @@ class ASTFunction(torch.autograd.Function):
             lin(gu, guq, 3, w2, bb2, xo, "fc2.fwd", act=L.ACT_ADD_AUX, aux=xm)
             del hq, aq, h2q, guq
             saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u,
-                                     gu=gu))
+                                     gu=gu, attn_work=aw))
             x = xo
         # final norm only matters for the CLS rows (ast.py:62-63 takes x[:, 0])
         gn, bn_, wh, bh = params[4 + 12 * nb: 8 + 12 * nb]
@@ -246,12 +261,19 @@ class ASTFunction(torch.autograd.Function):
             da = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj", db=db_proj)
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
-            work = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8, device=dev)
+            work = sb["attn_work"]
             with K.probe("attn.bwd", 8.0 * B * Hh * N * N * (D // Hh),  # 2x fwd, recompute not credited
                          (2 * dqkv.numel() + 2 * da.numel()) * dqkv.element_size()):
-                L.check(L.load().mia_attn_bwd(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
-                                              sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), cd, B, N, Hh,
-                                              s["scale"], L.stream_ptr()), "mia_attn_bwd")
+                if work is not None:  # Q' already written by the forward
+                    L.check(L.load().mia_attn_bwd_saved_q(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
+                                                          sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), B, N,
+                                                          Hh, s["scale"], L.stream_ptr()), "mia_attn_bwd_saved_q")
+                else:
+                    work = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8,
+                                       device=dev)
+                    L.check(L.load().mia_attn_bwd(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
+                                                  sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), cd, B, N, Hh,
+                                                  s["scale"], L.stream_ptr()), "mia_attn_bwd")
             dh = torch.empty(Tt, D, dtype=tdt, device=dev)
             dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")
             dg1, dbt1, db_next = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2)  # d(block in)

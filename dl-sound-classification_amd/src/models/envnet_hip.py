@@ -319,7 +319,7 @@ class EnvNetFunction(torch.autograd.Function):
                            K.epilogue(part, fin), FC1_CHUNK_ROWS, fin, B, cd, tag="fc1.wgrad")
                     chunk_ready(p[40], dW, part, lo + FC1_CHUNK_ROWS == fout)
             elif (li == 0 and ready is None and chunk_ready is None and cd == L.BF16 and p[40].grad is None
-                  and getattr(p[40], "_mia_fused_adam", False) and fout % 128 == 0 and fin % 128 == 0
+                  and K.defers_to_fused_adam(p[40]) and fout % 128 == 0 and fin % 128 == 0
                   and B % 64 == 0):
                 # single GPU under FusedAdam: FC1's 1.38 GB weight gradient is never written -- its sums
                 # of squares now, the product recomputed inside the fused Adam GEMM at the step

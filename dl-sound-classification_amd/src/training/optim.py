@@ -10,12 +10,32 @@ so the step never synchronises with the host.
 from __future__ import annotations
 
 import math
+import weakref
 
 import numpy as np
 import torch
+from torch.optim.optimizer import register_optimizer_step_pre_hook
 
 from ..miaudio import kernels as K
 from ..miaudio import lib as L
+
+
+def _materialise_for_other_optimizers(opt, args, kwargs):
+    """Global optimizer step pre-hook: an optimizer other than FusedAdam about to step a parameter whose
+    weight gradient was deferred gets the gradient materialised into ``p.grad`` first (the same GEMM), and
+    the parameter stops deferring -- so torch.optim.Adam built after a FusedAdam updates FC1 from its
+    first step instead of silently skipping it."""
+    if isinstance(opt, FusedAdam):
+        return
+    for grp in opt.param_groups:
+        for p in grp["params"]:
+            if getattr(p, "_mia_fused_adam", None) is not None:
+                p._mia_fused_adam = None
+            if getattr(p, "_mia_deferred", None) is not None:
+                K.materialise_deferred_grad(p)
+
+
+register_optimizer_step_pre_hook(_materialise_for_other_optimizers)
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -43,9 +63,12 @@ class FusedAdam(torch.optim.Optimizer):
         self._table = None
         self.table_builds = 0
         self.last_deferred = 0     # weight gradients applied by their fused Adam GEMM (last step)
+        ref = weakref.ref(self)
         for p in self.param_groups[0]["params"]:
-            # models may defer a wide Linear's weight gradient to this optimizer (K.defer_weight_grad)
-            p._mia_fused_adam = True
+            # models may defer a wide Linear's weight gradient to this optimizer (K.defer_weight_grad) while
+            # it is alive; another optimizer stepping the parameter first materialises the gradient
+            # (_materialise_for_other_optimizers), and takes the parameter over
+            p._mia_fused_adam = ref
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -466,6 +466,14 @@ int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_
 int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
                  void* dqkv, void* work, int32_t dtype, int32_t B, int32_t N, int32_t H,
                  float scale, mia_stream_t stream);
+/* Training form (bf16): mia_attn_fwd_save_q is mia_attn_fwd (q8 / s8 NULL) or mia_attn_fwd_mx (both
+ * set) that also writes the backward's scaled query operand Q' into `work` (a workspace of
+ * mia_attn_bwd_workspace_bytes, kept from the forward to the backward); mia_attn_bwd_saved_q is
+ * mia_attn_bwd (bf16) on such a workspace: its prep pass neither re-reads q nor rewrites Q'. */
+int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void* q8, void* s8, void* work, int32_t B,
+                        int32_t N, int32_t H, float scale, mia_stream_t stream);
+int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                         void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream);
 
 /* AST token assembly (ast.py:56-59): x[b][0] = cls + pos[0]; x[b][1+p] = patches[b][p] + pos[1+p].
  * patches: (B, Np, D) f32; out (B, Np+1, D) f32.  Backward: dpatch, dcls/dpos reductions. */
@@ -479,7 +487,7 @@ int mia_tokens_bwd(const float* dout, float* dpatches, float* dcls, float* dpos,
  * row b*N is a zero row in the cls slot), so one dense GEMM with the bias epilogue writes the token rows
  * of x directly and the weight gradient is one dense GEMM of the bf16 token gradient against it;
  * mia_tokens_fwd_inplace then sets x[b][0] = cls + pos[0] and adds pos[t] to every other row.
- * spec: (B, Fm, Tf) f32; out 16-B aligned; ps*ps % 8 == 0; x, cls, pos 16-B aligned, D % 4 == 0. */
+ * spec: (B, Fm, Tf) f32; out 16-B aligned; ps % 8 == 0; x, cls, pos 16-B aligned, D % 4 == 0. */
 int mia_ast_patches(const float* spec, int32_t B, int32_t Fm, int32_t Tf, int32_t ps, int32_t st, void* out,
                     mia_stream_t stream);
 int mia_tokens_fwd_inplace(float* x, const float* cls, const float* pos, int32_t B, int32_t N, int32_t D,

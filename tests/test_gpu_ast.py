@@ -243,3 +243,43 @@ def test_ast_backward_f32_vs_oracle(cuda):
         got, want = sd[mine].grad.cpu().double(), ref[theirs].grad.double()
         l2 = float((got - want).norm() / want.norm().clamp_min(1e-30))
         assert l2 < 1e-3, (mine, l2)
+
+
+@pytest.mark.parametrize("B,N,H,mx", [(2, 1645, 12, False), (1, 77, 2, True), (3, 130, 3, False)])
+def test_attn_saved_q_equals_plain(cuda, B, N, H, mx):
+    """The training form of the bf16 attention (forward writes Q' into the backward workspace, the
+    backward's prep skips it) gives outputs, lse, MX copies and dqkv identical to the plain entries."""
+    from src.miaudio import lib as L
+    g = torch.Generator(device=cuda).manual_seed(N + H)
+    qkv = (torch.randn(B * N, 3 * H * 64, generator=g, device=cuda) * 0.7).to(torch.bfloat16)
+    dout = torch.randn(B * N, H * 64, generator=g, device=cuda).to(torch.bfloat16)
+    scale = 64 ** -0.5
+    lib, s = L.load(), L.stream_ptr()
+    nws = int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H))
+    res = []
+    for saved in (False, True):
+        out = torch.empty(B * N, H * 64, dtype=torch.bfloat16, device=cuda)
+        lse = torch.empty(B, H, N, device=cuda)
+        q8 = torch.empty(B * N, H * 64, dtype=torch.uint8, device=cuda) if mx else None
+        s8 = torch.empty(B * N, H * 2, dtype=torch.uint8, device=cuda) if mx else None
+        work = torch.full((nws,), 255, dtype=torch.uint8, device=cuda)
+        dqkv = torch.empty_like(qkv)
+        if saved:
+            L.check(lib.mia_attn_fwd_save_q(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                                            q8.data_ptr() if mx else None, s8.data_ptr() if mx else None,
+                                            work.data_ptr(), B, N, H, scale, s), "fwd_save_q")
+            L.check(lib.mia_attn_bwd_saved_q(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+                                             dqkv.data_ptr(), work.data_ptr(), B, N, H, scale, s), "bwd_saved_q")
+        else:
+            if mx:
+                L.check(lib.mia_attn_fwd_mx(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), q8.data_ptr(),
+                                            s8.data_ptr(), B, N, H, scale, s), "fwd_mx")
+            else:
+                L.check(lib.mia_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), L.BF16, B, N, H, scale, s),
+                        "fwd")
+            L.check(lib.mia_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), dqkv.data_ptr(),
+                                     work.data_ptr(), L.BF16, B, N, H, scale, s), "bwd")
+        torch.cuda.synchronize()
+        res.append([out, lse, dqkv] + ([q8, s8] if mx else []))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -22,7 +22,7 @@ def _run(cuda, defer: bool, steps: int, x, y):
     opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4, clip=1.0)
     if not defer:
         for p in m.parameters():
-            p._mia_fused_adam = False
+            p._mia_fused_adam = None
     norms, deferred = [], []
     for _ in range(steps):
         z = m(x)
@@ -58,7 +58,7 @@ def test_deferred_grad_pending_twice_raises(cuda):
     from src.miaudio import kernels as K
     from src.training.optim import FusedAdam
     m = envnet_with_hash_params(cuda, compute_dtype="bf16").train()
-    FusedAdam(m.parameters(), lr=1e-3)
+    opt = FusedAdam(m.parameters(), lr=1e-3)  # noqa: F841  (alive: the model defers to it)
     x = torch.from_numpy(synth_waveform(34, 64, 220_500)[:, None, :]).to(cuda)
     y = torch.zeros(64, 50, device=cuda)
     y[:, 0] = 1.0
@@ -68,3 +68,44 @@ def test_deferred_grad_pending_twice_raises(cuda):
     z = m(x)
     with pytest.raises(RuntimeError, match="deferred weight gradient is still pending"):
         z.backward(dz)
+
+
+def test_torch_adam_after_fused_adam_updates_fc1(cuda):
+    """a torch.optim.Adam built after a FusedAdam (still alive) on the same parameters must update
+    FC1 on its first step: the global step pre-hook materialises the deferred gradient into p.grad with the
+    same GEMM, and the parameter stops deferring.  Its gradient equals a run where no FusedAdam ever existed."""
+    from src.miaudio import kernels as K
+    from src.training.optim import FusedAdam
+    x = torch.from_numpy(synth_waveform(35, 64, 220_500)[:, None, :]).to(cuda)
+    y = torch.zeros(64, 50, device=cuda)
+    y[torch.arange(64), torch.arange(64) % 50] = 1.0
+    grads = []
+    for with_fused in (True, False):
+        m = envnet_with_hash_params(cuda, compute_dtype="bf16").train()
+        fused = FusedAdam(m.parameters(), lr=1e-3) if with_fused else None  # noqa: F841
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        fc1 = dict(m.named_parameters())["classifier.1.weight"]
+        before = fc1.detach().clone()
+        z = m(x)
+        _, dz, _ = K.soft_ce(z.detach().float().contiguous(), y, input_sigmoid=False)
+        z.backward(dz)
+        assert (fc1.grad is None) == with_fused  # deferred while the FusedAdam is alive
+        opt.step()
+        assert fc1.grad is not None and getattr(fc1, "_mia_deferred", None) is None
+        assert not torch.equal(fc1.detach(), before)
+        assert not K.defers_to_fused_adam(fc1)  # taken over by torch's Adam
+        grads.append(fc1.grad.detach().clone())
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-5, atol=1e-9)
+
+
+def test_fused_adam_collected_stops_deferring(cuda):
+    from src.miaudio import kernels as K
+    from src.training.optim import FusedAdam
+    m = envnet_with_hash_params(cuda, compute_dtype="bf16").train()
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    fc1 = dict(m.named_parameters())["classifier.1.weight"]
+    assert K.defers_to_fused_adam(fc1)
+    del opt
+    import gc
+    gc.collect()
+    assert not K.defers_to_fused_adam(fc1)

@@ -1,0 +1,193 @@
+"""GPU: parity at the BENCHED sizes (verdict r3, What's missing 2).
+
+The oracle-sized tests elsewhere run B <= 64.  Several paths are only taken at full size: the deferred FC1
+weight gradient at B = 256, the persistent kernels' item splits over 256 clips, the 256x256 GEMM at
+M = 421 120 token rows, the attention grid at B*H = 3 072, the shape-dependent split-K choices.  Here:
+
+* one EnvNetV2 bf16 train step at B = 256 (FusedAdam alive, so FC1's gradient is deferred into the Adam
+  GEMM) against the oracle step on the same GPU under bf16 autocast and in f32, with the self-calibrated
+  bounds of tests/test_gpu_e2e_bf16.py (reference: src/models/envnet_v2.py:76-85);
+* one ASTModel depth-12 bf16 train step at B = 32 the same way (reference: src/models/ast.py:50-63);
+* the attention kernels at B = 256, H = 12, N = 1645 (the benched grid) against float64 on sampled
+  (clip, head) pairs, forward and backward (timm Attention, ast.py:38,60-61);
+* batch independence at full size: eval-mode EnvNet, AST bf16 and AST fp8-mixed outputs of clips 0-3 at
+  B = 256 against a B = 4 run of the same clips (eval BatchNorm uses running statistics and nothing else
+  crosses clips, so only kernel choices that depend on the batch -- tile / split shapes of the FC GEMMs --
+  may change a summation order; tolerances below).
+"""
+import math
+import os
+
+import pytest
+import torch
+
+from oracle import ast as oast
+from oracle import envnet as oenv
+from oracle.synth import hash_uniform, synth_waveform
+from tests._util import envnet_with_hash_params, hash_params
+from tests.test_gpu_e2e_bf16 import _check, _oracle_step, _rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _labels(cuda, B, seed):
+    g = torch.Generator().manual_seed(seed)
+    y = torch.zeros(B, 50)
+    y[torch.arange(B), torch.randint(0, 50, (B,), generator=g)] = 1.0
+    return y.to(cuda)
+
+
+def test_envnet_bf16_step_b256_deferred_fc1_vs_autocast_oracle(cuda):
+    from src.miaudio import kernels as K
+    from src.training.optim import FusedAdam
+    B = 256
+    x = torch.from_numpy(synth_waveform(41, B, 220_500)[:, None, :]).to(cuda)
+    y = _labels(cuda, B, 41)
+    m = envnet_with_hash_params(cuda, compute_dtype="bf16").train()
+    names = [n for n, _ in m.named_parameters()]
+    opt = FusedAdam(m.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)  # built first: FC1 is deferred
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    z = m(x)
+    loss, dz, _ = K.soft_ce(z.detach().float().contiguous(), y, input_sigmoid=False)
+    z.backward(dz)
+    assert dict(m.named_parameters())["classifier.1.weight"].grad is None  # the deferred path at B = 256
+    opt.step()
+    assert opt.last_deferred == 1
+    total = float(opt.last_total_norm)
+    deltas = {n: p.detach() - before[n] for n, p in m.named_parameters()}
+    zz, loss = z.detach().float(), float(loss)
+    del z, dz, m, opt, before
+    torch.cuda.empty_cache()
+
+    def ref(autocast):
+        p = {k: torch.from_numpy(v.copy()).to(cuda) for k, v in hash_params(100).items()}
+        for n in names:
+            p[n].requires_grad_(True)
+        r = _oracle_step(p, names, lambda q: oenv.forward(q, x, training=True, dropout_p=0.0), y, autocast)
+        torch.cuda.empty_cache()
+        return r
+
+    r16, r32 = ref(True), ref(False)
+    _check("envnet-b256", zz, loss, total, deltas, {}, r16, r32,
+           tol={"logits": 0.2, "loss": 0.03, "gradnorm": 0.03, "sign": 0.95})
+
+
+def _ast(cuda, cd, depth, st, hw, hb):
+    from src.models.ast import ASTModel
+    m = ASTModel(num_classes=50, compute_dtype=cd, depth=depth)
+    m.load_vit_state(st)
+    with torch.no_grad():
+        m.head.weight.copy_(torch.from_numpy(hw))
+        m.head.bias.copy_(torch.from_numpy(hb))
+    return m.to(cuda)
+
+
+def test_ast_depth12_bf16_step_b32_vs_autocast_oracle(cuda):
+    os.environ["MIA_QUIET"] = "1"
+    from src.miaudio import kernels as K
+    from src.training.optim import FusedAdam
+    B = 32
+    st = oast.deit_hash_state(300)
+    hw, hb = oast.head_hash(901, 50)
+    m = _ast(cuda, "bf16", 12, st, hw, hb).train()
+    x = torch.from_numpy(hash_uniform(33, (B, 128, 1379))).to(cuda)
+    y = _labels(cuda, B, 33)
+    pmap = dict(m.named_parameters())
+    before = {n: p.detach().clone() for n, p in pmap.items()}
+    probs = m(x)
+    loss, dp, _ = K.soft_ce(probs.detach().float().contiguous(), y, input_sigmoid=False)
+    probs.backward(dp)
+    opt = FusedAdam(m.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
+    opt.step()
+    total = float(opt.last_total_norm)
+    deltas = {n: p.detach() - before[n] for n, p in pmap.items()}
+    pp, loss = probs.detach().float(), float(loss)
+    del probs, dp, m, opt, before, pmap
+    torch.cuda.empty_cache()
+    ref_names = list(oast.model_params(st, hw, hb))
+    assert set(ref_names) == set(deltas), set(ref_names) ^ set(deltas)
+
+    def ref(autocast):
+        p = {k: v.to(cuda).requires_grad_(True) for k, v in oast.model_params(st, hw, hb).items()}
+        r = _oracle_step(p, ref_names, lambda q: oast.forward(q, x), y, autocast)
+        torch.cuda.empty_cache()
+        return r
+
+    r16, r32 = ref(True), ref(False)
+    # depth 12 instead of 2: the fixed bounds are the depth-2 test's widened 3x; the self-calibrated bounds
+    # (HIP no further from f32 than 1.25x autocast's distance) are the same
+    _check("ast-d12-b32", pp, loss, total, deltas, {}, r16, r32,
+           tol={"logits": 0.045, "loss": 0.006, "gradnorm": 0.018, "sign": 0.97})
+
+
+def test_attention_benched_grid_b256_h12(cuda):
+    """mia_attn_fwd_save_q / mia_attn_bwd_saved_q (the training form) over the whole benched grid
+    (B*H = 3 072 blocks of 13 query / key blocks each); sampled (clip, head) pairs against float64, with the
+    bounds of test_gpu_ast.test_attention_fwd_bwd (bf16)."""
+    from src.miaudio import lib as L
+    B, N, H = 256, 1645, 12
+    g = torch.Generator(device=cuda).manual_seed(5)
+    qkv = (torch.randn(B * N, 3 * H * 64, generator=g, device=cuda) * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B * N, H * 64, generator=g, device=cuda).to(torch.bfloat16)
+    lib, s = L.load(), L.stream_ptr()
+    out = torch.empty(B * N, H * 64, dtype=torch.bfloat16, device=cuda)
+    lse = torch.empty(B, H, N, device=cuda)
+    work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H)), dtype=torch.uint8, device=cuda)
+    dq = torch.full_like(qkv, float("nan"))
+    L.check(lib.mia_attn_fwd_save_q(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), None, None, work.data_ptr(), B,
+                                    N, H, 0.125, s), "fwd_save_q")
+    L.check(lib.mia_attn_bwd_saved_q(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), dq.data_ptr(),
+                                     work.data_ptr(), B, N, H, 0.125, s), "bwd_saved_q")
+    torch.cuda.synchronize()
+    assert torch.isfinite(dq.float()).all() and torch.isfinite(out.float()).all()
+    qkv4 = qkv.view(B, N, 3, H, 64)
+    for b, h in [(0, 0), (1, 11), (97, 5), (128, 0), (200, 7), (255, 11)]:
+        q, k, v = (qkv4[b, :, i, h].double().requires_grad_(True) for i in range(3))
+        o = torch.softmax(q @ k.t() / 8.0, -1) @ v
+        o.backward(dout.view(B, N, H, 64)[b, :, h].double())
+        got = out.view(B, N, H, 64)[b, :, h].double()
+        assert float((got - o).abs().max() / o.abs().max()) < 2e-2, (b, h)
+        lref = torch.logsumexp(q.detach() @ k.detach().t() / 8.0, -1)
+        assert float((lse[b, h].double() - lref).abs().max()) < 2e-2, (b, h)
+        d4 = dq.view(B, N, 3, H, 64)
+        for i, ref in enumerate((q.grad, k.grad, v.grad)):
+            e = float((d4[b, :, i, h].double() - ref).abs().max() / ref.abs().max())
+            assert e < 6e-2, (b, h, "qkv"[i], e)
+
+
+def test_envnet_eval_batch_independence_b256(cuda):
+    B = 256
+    m = envnet_with_hash_params(cuda, compute_dtype="bf16").eval()
+    x = torch.from_numpy(synth_waveform(43, B, 220_500)[:, None, :]).to(cuda)
+    with torch.no_grad():
+        z256 = m(x)[:4].float()
+        z4 = m(x[:4].contiguous()).float()
+    e = _rel(z256, z4)
+    print(f"envnet eval B=256 vs B=4: rel-L2 {e:.3g}, max |d| {float((z256 - z4).abs().max()):.3g}")
+    # clips never mix in eval; the FC GEMMs' kernel / split choice depends on B (M = rows), so their sums may
+    # be ordered differently: one bf16 rounding of the logits at most
+    assert e < 8e-3, e
+    assert torch.equal(z256.argmax(1), z4.argmax(1))
+
+
+@pytest.mark.parametrize("cd", ["bf16", "fp8"])
+def test_ast_eval_batch_independence_b256(cuda, cd):
+    os.environ["MIA_QUIET"] = "1"
+    B = 256
+    st = oast.deit_hash_state(300)
+    hw, hb = oast.head_hash(901, 50)
+    m = _ast(cuda, cd, 12, st, hw, hb).eval()
+    x = torch.from_numpy(hash_uniform(34, (B, 128, 1379))).to(cuda)
+    with torch.no_grad():
+        p256 = m(x)[:4].float()
+        torch.cuda.empty_cache()
+        p4 = m(x[:4].contiguous()).float()
+    e = _rel(p256, p4)
+    print(f"ast[{cd}] eval B=256 vs B=4: rel-L2 {e:.3g}, max |d| {float((p256 - p4).abs().max()):.3g}")
+    # every token row is computed independently of the batch (LayerNorm per row, attention per (clip, head),
+    # MX blocks along K within a row): the 256-row GEMM tiles only change which rows share a tile
+    assert e < 2e-3, e
+    assert torch.equal(p256.argmax(1), p4.argmax(1))
+    del m
+    torch.cuda.empty_cache()
+    assert math.isfinite(e)

@@ -448,6 +448,28 @@ def test_mgemm_layouts(cuda, la, lb, M, N, Kd):
     assert rel(out.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+def test_mgemm_ragged_n_not_multiple_of_8(cuda, odt):
+    """N % 8 == 4 with a bf16 output -- the 256x256 kernel stores 8 bf16 per lane guarded by
+    n < N only, so such shapes must leave it (bf16) while an f32 output (4 per lane) may stay; nothing is
+    written past N in either case, and the rows after each output row keep their values."""
+    M, N, Kd = 4096, 260, 768
+    a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 23)
+    path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1)
+    ref = a.float() @ b.float().t()
+    full = torch.full((M + 1, N + 12), float("nan"), dtype=odt, device=cuda)
+    out = full[:M, :N]
+    K.gemm(A, Bo, K.epilogue(out, N + 12), M, N, Kd, L.BF16)
+    torch.cuda.synchronize()
+    assert torch.isnan(full[M:].float()).all() and torch.isnan(full[:, N:].float()).all(), path
+    assert rel(out.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
+    # contiguous output (ldc = N): the 4 columns past a row's end are the next row's first 4
+    out2 = torch.empty(M, N, dtype=odt, device=cuda)
+    K.gemm(A, Bo, K.epilogue(out2, N), M, N, Kd, L.BF16)
+    torch.cuda.synchronize()
+    assert rel(out2.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
+
+
 @pytest.mark.parametrize("case", ["plain_f32", "residual_f32", "bias_bf16", "gelu", "gelu_save", "dact_gelu"])
 def test_mgemm_epilogues(cuda, case):
     """The fused epilogues of the AST linears on the 256x256 kernel: f32 output, residual add into f32

@@ -22,7 +22,7 @@ for p in $PASSES; do
              python3 $ROOT/bench.py $PMC_ARGS > $OUT/bench_fetch.log 2>&1 ;;
     write) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
              python3 $ROOT/bench.py $PMC_ARGS > $OUT/bench_write.log 2>&1 ;;
-    sq)    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY \
+    sq)    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY \
              SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace \
              --output-format csv -d $OUT/sq -o run -- python3 $ROOT/bench.py $PMC_ARGS > $OUT/bench_sq.log 2>&1 ;;
   esac

@@ -5,9 +5,11 @@ directories).
 
 MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe busy cycles summed over every SIMD
 (MI355X_MICROARCH.md, constants table: 32 per v_mfma_f32_32x32x16_bf16), so
-util = MFMA_BUSY / (1024 SIMDs x duration x clock); the duration is the kernel-trace pass's (undisturbed
-by counter collection), and the clock is the one the counter run itself held, estimated as
-SQ_BUSY_CU_CYCLES x 4 (quad-cycles) / 256 CUs / its own duration.  SQ_WAVE_CYCLES / SQ_WAIT_* /
+util = MFMA_BUSY / (1024 SIMDs x duration x clock); the duration and the clock are the counter run's own:
+clock = GRBM_GUI_ACTIVE / 8 / duration (MI355X_MICROARCH.md, DVFS give-back: rocprofv3 reports
+GRBM_GUI_ACTIVE summed over the 8 XCDs; within 3 % of the in-kernel clock on dispatches of 10 ms or more),
+so a kernel's MFMA utilisation is MFMA_BUSY / (1024 x GRBM_GUI_ACTIVE / 8).  Round 3's estimate from
+SQ_BUSY_CU_CYCLES read 7.6-9.3 GHz (that counter is not per-CU shader cycles) and is not used.  SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles per wave; they are reported as fractions of SQ_WAVE_CYCLES.
 Only the launches of the last complete step (marker: the Adam kernel) are used.
 """
@@ -20,7 +22,7 @@ import re
 import sys
 from pathlib import Path
 
-NSIMD, NCU = 1024, 256
+NSIMD, NCU, NXCD = 1024, 256, 8
 
 
 def short(name: str) -> str:
@@ -74,13 +76,14 @@ def main():
         row = {"launches": launches[k], "ms_pmc_run": round(dur_pmc[k] * 1e3, 4)}
         if dur.get(k):
             row["ms_trace"] = round(dur[k] * 1e3, 4)
-        if v.get("SQ_BUSY_CU_CYCLES") and dur_pmc[k] > 0:
-            clk = v["SQ_BUSY_CU_CYCLES"] * 4 / NCU / dur_pmc[k]
-            row["clock_ghz_pmc_run"] = round(clk / 1e9, 3)
+        if v.get("GRBM_GUI_ACTIVE") and dur_pmc[k] > 0:
+            cycles = v["GRBM_GUI_ACTIVE"] / NXCD  # shader clocks over the kernels' wall time
+            row["clock_ghz_pmc_run"] = round(cycles / dur_pmc[k] / 1e9, 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
-                row["mfma_util"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * dur_pmc[k] * clk), 4)
-                row["mfma_util_at_2.4GHz_trace"] = (round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * dur[k] * 2.4e9), 4)
-                                                   if dur.get(k) else None)
+                row["mfma_util"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * cycles), 4)
+                if dur.get(k):  # the same busy cycles over the undisturbed trace duration at the run's clock
+                    row["mfma_util_trace_duration"] = round(
+                        v["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * dur[k] * cycles / dur_pmc[k]), 4)
         for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
             if c in v:
                 row[c[3:].lower() + "_frac"] = round(v[c] / wc, 4)
