@@ -4,6 +4,11 @@ from pathlib import Path
 
 import pytest
 
+# The oracle's torch convs on the GPU (EnvNet-v2 at B = 256 in tests/test_gpu_fullsize.py): MIOpen's
+# default find mode benchmarks and compiles solvers for every new shape, minutes of silence on a fresh
+# box; FAST takes its immediate-mode choice.  Set before torch loads MIOpen.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 REPO = Path(__file__).resolve().parents[1]
 PKG = REPO / "dl-sound-classification_amd"
 for p in (str(REPO), str(PKG)):

@@ -44,11 +44,11 @@ def _oracle_step(params, names, fwd, y, autocast: bool):
 
 def _check(tag, z, loss, total, deltas, grads, ref, ref32, tol):
     zr, lr_, gr, tr, dr = ref
-    z32, t32 = ref32[0], ref32[3]
+    z32, l32, t32 = ref32[0], ref32[1], ref32[3]
     ez, ez32, ea32 = _rel(z, zr), _rel(z, z32), _rel(zr, z32)
     gh32, ga32 = abs(total - t32) / t32, abs(tr - t32) / t32
     print(f"[{tag}] logits rel-L2 vs autocast {ez:.4f} (vs f32 {ez32:.4f}; autocast vs f32 {ea32:.4f})"
-          f" loss {loss:.5f}/{lr_:.5f} gradnorm {total:.5f}/{tr:.5f} (f32 {t32:.5f}: hip {gh32:.5f}, "
+          f" loss {loss:.5f}/{lr_:.5f} (f32 {l32:.5f}) gradnorm {total:.5f}/{tr:.5f} (f32 {t32:.5f}: hip {gh32:.5f}, "
           f"autocast {ga32:.5f})")
     assert ez < tol["logits"], ez
     # the HIP bf16 step is as close to the f32 step as autocast bf16 is (verdict r2)
@@ -66,8 +66,10 @@ def _check(tag, z, loss, total, deltas, grads, ref, ref32, tol):
     print(f"[{tag}] argmax: hip {z.argmax(1).tolist()} autocast {zr.argmax(1).tolist()} f32 {a32.tolist()} "
           f"decided {decided.tolist()}")
     assert torch.equal(z.argmax(1)[decided], a32[decided]), (z.argmax(1), a32, decided)
-    assert abs(loss - lr_) <= tol["loss"] * abs(lr_)
-    assert abs(total - tr) <= tol["gradnorm"] * tr
+    # loss and grad norm against the f32 step: within the fixed tolerance, or no further from it than the
+    # autocast step is (its distance depends on the bf16 conv algorithms MIOpen picks for the oracle)
+    assert abs(loss - l32) <= max(tol["loss"] * abs(l32), 1.25 * abs(lr_ - l32) + 1e-4), (loss, lr_, l32)
+    assert abs(total - t32) <= max(tol["gradnorm"] * t32, 2.0 * abs(tr - t32) + 1e-4), (total, tr, t32)
     agree, n = 0, 0
     for name, d in deltas.items():
         g = gr[name].flatten()

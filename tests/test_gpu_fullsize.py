@@ -17,6 +17,7 @@ M = 421 120 token rows, the attention grid at B*H = 3 072, the shape-dependent s
 """
 import math
 import os
+import time
 
 import pytest
 import torch
@@ -28,6 +29,11 @@ from tests._util import envnet_with_hash_params, hash_params
 from tests.test_gpu_e2e_bf16 import _check, _oracle_step, _rel
 
 pytestmark = pytest.mark.gpu
+_T0 = time.time()
+
+
+def _t(msg):
+    print(f"[fullsize {time.time() - _T0:7.1f}s] {msg}", flush=True)
 
 
 def _labels(cuda, B, seed):
@@ -56,6 +62,7 @@ def test_envnet_bf16_step_b256_deferred_fc1_vs_autocast_oracle(cuda):
     total = float(opt.last_total_norm)
     deltas = {n: p.detach() - before[n] for n, p in m.named_parameters()}
     zz, loss = z.detach().float(), float(loss)
+    _t("envnet b256: HIP step done")
     del z, dz, m, opt, before
     torch.cuda.empty_cache()
 
@@ -65,6 +72,7 @@ def test_envnet_bf16_step_b256_deferred_fc1_vs_autocast_oracle(cuda):
             p[n].requires_grad_(True)
         r = _oracle_step(p, names, lambda q: oenv.forward(q, x, training=True, dropout_p=0.0), y, autocast)
         torch.cuda.empty_cache()
+        _t(f"envnet b256: oracle step done (autocast={autocast})")
         return r
 
     r16, r32 = ref(True), ref(False)
@@ -102,6 +110,7 @@ def test_ast_depth12_bf16_step_b32_vs_autocast_oracle(cuda):
     total = float(opt.last_total_norm)
     deltas = {n: p.detach() - before[n] for n, p in pmap.items()}
     pp, loss = probs.detach().float(), float(loss)
+    _t("ast d12 b32: HIP step done")
     del probs, dp, m, opt, before, pmap
     torch.cuda.empty_cache()
     ref_names = list(oast.model_params(st, hw, hb))
@@ -111,6 +120,7 @@ def test_ast_depth12_bf16_step_b32_vs_autocast_oracle(cuda):
         p = {k: v.to(cuda).requires_grad_(True) for k, v in oast.model_params(st, hw, hb).items()}
         r = _oracle_step(p, ref_names, lambda q: oast.forward(q, x), y, autocast)
         torch.cuda.empty_cache()
+        _t(f"ast d12 b32: oracle step done (autocast={autocast})")
         return r
 
     r16, r32 = ref(True), ref(False)
