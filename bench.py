@@ -204,7 +204,7 @@ KERNEL_HINT = {
     "conv2.wgrad": ["fe_wgrad_kernel"],
     "conv1.fwd": ["fe_conv1_kernel"],
     "attn.fwd": ["attn_fwd_kernel"],
-    "attn.bwd": ["attn_bwd_prep_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"],
+    "attn.bwd": ["attn_bwd_prep_kernel", "attn_bwd_fused_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"],
     "optim.step": ["sqnorm_kernel", "norm_final_kernel", "adam_kernel", "dgemm_kernel<1, 1, true>"],
     "logmel.fwd": ["fft_mel_db_kernel", "clip_stats_kernel", "clip_norm_kernel", "logmel"],
 }

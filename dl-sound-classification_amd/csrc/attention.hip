@@ -788,6 +788,328 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   }
 }
 
+// ------------------------------------------------------------------------------ fused backward
+// One pass per (b, h, 256-key block) computes S, dP and dS ONCE and all three products from them:
+// dV^T += dO^T P and dK^T += Q'^T dS in registers (key on the lane, as the key-parallel kernel above),
+// and the block's share of dQ = dS K (dS^T staged in LDS, K^T read from an LDS image of the block's keys):
+// five MFMA products per tile instead of the seven of the two-kernel form (whose query-parallel kernel
+// recomputes S and dP with the query on the lane).
+//
+// dQ sums over the key blocks of one (b, h).  No float atomics (the sum would depend on arrival order):
+// an ORDERED HAND-OFF.  Key block kb walks the query tiles rotated by FB_LAG * kb (tile T at step
+// (T + FB_LAG kb) mod nt), and the blocks add their partial of tile T in the fixed order of the steps
+// at which they reach it: a running f32 sum in the workspace, the last block of the order writing bf16
+// dQ.  Each hand-off follows MI355X_MICROARCH.md's visibility table, row 1: every byte of the running
+// sum is stored and loaded `sc1` (16 B per lane, to registers), every storing wave waits vmcnt(0) before
+// a workgroup barrier behind which ONE lane stores the `sc1` flag; the consumer's wave 0 polls that flag
+// with `sc1` loads and the other waves load behind a barrier it joins.  The lag gives the predecessor
+// one whole step of slack.  A block waits only for contributions made at strictly earlier steps of
+// blocks dispatched before it or resident with it, so a chain cannot wait on itself; the spin is bounded
+// anyway (FB_SPIN_TICKS of the 100 MHz real-time counter) and a timeout is recorded in the workspace's
+// error word (mia_attn_bwd_error_offset) instead of hanging the GPU.  Bit-reproducible: the order is a
+// fixed function of (kb, T, N).
+constexpr int FB_K = 256;        // keys per workgroup: 8 waves x 32
+constexpr int FB_LAG = 3;        // rotation lag between consecutive key blocks of one (b, h)
+constexpr int FB_SUB = 4096;     // bytes of one 32 x 32 f32 dQ^T sub-tile in register order
+constexpr int FB_TILE = 4 * FB_SUB;
+constexpr unsigned long long FB_SPIN_TICKS = 20000000ull;  // 200 ms at 100 MHz
+
+// LDS map of the fused kernel (one __shared__ array)
+constexpr int FBL_Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
+constexpr int FBL_G = FBL_Q + 2 * 8192;         // [2][64][64] bf16 dO tiles (sw_off)
+constexpr int FBL_F = FBL_G + 2 * 8192;         // [2][2][64][8] bf16 fifth-k-step rows
+constexpr int FBL_K = FBL_F + 2 * 2048;         // [256][64] bf16 the block's keys (sw_off)
+constexpr int FBL_S = FBL_K + 32768;            // [256][64] bf16 dS^T of the current tile (sw_off)
+constexpr int FBL_R = FBL_S + 32768;            // [4][4096 B] f32 key-half partials (register order)
+constexpr int FBL_O = FBL_R + 4 * FB_SUB;       // [64][72] bf16 final dQ rows
+constexpr int FBL_BYTES = FBL_O + 64 * LROW * 2;
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned fb_ld_flag(const unsigned* p) {
+  unsigned v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void fb_st_flag(unsigned* p, unsigned v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// wave-uniform: poll `flag` until it reads `want` (bounded; a timeout sets the error word, and once it is
+// set every later wait of the launch gives up at once, so a broken chain still drains the grid quickly)
+__device__ __forceinline__ void fb_wait(const unsigned* flag, unsigned want, unsigned* err) {
+  if (fb_ld_flag(flag) == want) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    __builtin_amdgcn_s_sleep(4);
+    if (fb_ld_flag(flag) == want) return;
+    if (fb_ld_flag(err) != 0u) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > FB_SPIN_TICKS) {
+      fb_st_flag(err, 1u);
+      return;
+    }
+  }
+}
+
+// the tile key block kb processes at step j, and its position in tile T's chain of contributions
+__device__ __forceinline__ int fb_tile(int j, int kb, int nt) {
+  const int t = j - FB_LAG * kb;
+  return t < 0 ? t + nt : t;
+}
+__device__ __forceinline__ int fb_pos(int kb, int T, int nkb, int nt) {
+  auto step = [&](int k) { const int s = T + FB_LAG * k; return s >= nt ? s - nt : s; };
+  const int mine = step(kb);
+  int p = 0;
+  for (int k = 0; k < nkb; ++k) p += step(k) < mine;
+  return p;
+}
+
+// one 64-row tile by LDS-DMA with 8 waves: wave w loads rows 8w .. 8w + 7 (one 1-KB piece)
+struct TileDMA8 {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned voff;
+  __device__ __forceinline__ void init(const bf16* g, int64_t ld, int N, int wave, int lane) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(((int64_t)(N - 1) * ld + 64) * 2), 0x00020000);
+    const int r = 8 * wave + (lane >> 3);
+    voff = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
+  }
+  __device__ __forceinline__ void issue(char* tile, unsigned row0_bytes, int wave) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 1024), 16, voff, row0_bytes, 0, 0);
+  }
+};
+
+// S', dP' of 32 queries x this wave's 32 keys -> dS; dV^T, dK^T MFMAs; dS^T (bf16) into the LDS image
+// (K row fragments from the block's LDS image Kt, V fragments in registers; `mid` runs between the halves)
+template <bool TAIL, class Mid>
+__device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
+                                             const bf16* F_, const bf16* Kt, bf16* dsT, const bf16x8 (&vf)[4],
+                                             bf16x8 one, bool key_ok, int q0, int N, int wave, int lane, Mid&& mid) {
+  const int krow = 32 * wave + (lane & 31);
+#pragma unroll
+  for (int sq = 0; sq < 2; ++sq) {
+    if (sq == 1) mid();
+    const int qr = sq * 32 + (lane & 31);
+    f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), frag_row_sw(Kt, krow, 0, lane), zero16());
+    f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
+#pragma unroll
+    for (int ks = 1; ks < 4; ++ks) {
+      sc = mfma(frag_row_sw(Q_, qr, ks, lane), frag_row_sw(Kt, krow, ks, lane), sc);
+      dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
+    }
+    sc = mfma(row_frag(F_ + qr * 8), one, sc);
+    dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(sc[r]);
+      if constexpr (TAIL) {
+        if (q0 + sq * 32 + acc_row(r, lane) >= N) p = 0.f;
+      }
+      p = key_ok ? p : 0.f;  // keys past the sequence end: no contribution to dQ
+      sc[r] = p;
+      dp[r] *= p;
+    }
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
+      // dS^T[key][q]: elements 0..3 = queries 16 sk + 4h + 0..3, 4..7 = 16 sk + 8 + 4h + 0..3 (of this sq)
+      const int qa = sq * 32 + 16 * sk + 4 * (lane >> 5);
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa)) = bf16x4{df[0], df[1], df[2], df[3]};
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        dv[dh] = mfma(frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane), pf, dv[dh]);
+        dk[dh] = mfma(frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane), df, dk[dh]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                             const bf16* __restrict__ qs, const bf16* __restrict__ frag,
+                                                             bf16* __restrict__ dqkv, float* chain, unsigned* flags,
+                                                             unsigned* err, int N, int H, int nkb, float scale,
+                                                             float dk_scale) {
+  __shared__ __attribute__((aligned(1024))) char lds[FBL_BYTES];
+  const int t = threadIdx.x, lane0 = t & 63;
+  int lane = lane0;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);  // the key blocks of one (b, h): consecutive, one XCD
+  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
+  const int nt = (N + 63) / 64;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + FBL_K);
+  bf16* const dsT = reinterpret_cast<bf16*>(lds + FBL_S);
+  float* const red = reinterpret_cast<float*>(lds + FBL_R);
+  bf16* const dqo = reinterpret_cast<bf16*>(lds + FBL_O);
+  // the block's 256 keys -> Kt (wave w: its own 32 keys, 4 pieces; keys past N read as zeros)
+  {
+    const __amdgpu_buffer_rsrc_t kr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = 32 * wave + 8 * i + (lane >> 3);  // local key row
+      const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + FBL_K + (4 * wave + i) * 1024), 16, vo,
+                                               (unsigned)((int64_t)(kb * FB_K + 32 * wave + 8 * i) * ldt * 2), 0, 0);
+    }
+  }
+  TileDMA8 qd, gd;
+  FragDMA fd;
+  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  fd.init(frag + (int64_t)bh * 2 * N * 8, N);
+  {
+    const int T0 = fb_tile(0, kb, nt);
+    qd.issue(lds + FBL_Q, (unsigned)T0 * tile_bytes, wave);
+    gd.issue(lds + FBL_G, (unsigned)T0 * tile_bytes, wave);
+    fd.issue(reinterpret_cast<bf16*>(lds + FBL_F), (unsigned)T0 * 64u, wave, lane);
+  }
+  const int key = kb * FB_K + wave * 32 + (lane & 31);
+  const bool key_ok = key < N;
+  bf16x8 vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key_ok);
+  const bf16x8 one = ones3(lane);
+  f32x16 dk[2], dv[2];
+  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+  // the running dQ sums of this (b, h): [nt][4 sub-tiles][16 regs / 4][64 lanes][4] f32, and their flags
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(chain + (int64_t)bh * nt * (FB_TILE / 4)), 0, nt * FB_TILE, 0x00020000);
+  unsigned* const fl = flags + (int64_t)bh * nt;
+  const int last = nkb - 1;
+  const int dh = wave & 1, qh = (wave >> 1) & 1, kh = wave >> 2;  // this wave's dQ^T sub-tile and key half
+  if (wave == 0) {
+    const int T0 = fb_tile(0, kb, nt), p0 = fb_pos(kb, T0, nkb, nt);
+    if (p0 > 0) fb_wait(fl + T0, (unsigned)p0, err);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int prev_T = -1, prev_pos = 0;  // the tile whose running sum this block stored last step (to publish)
+  bool prev_final = false;
+  for (int j = 0; j < nt; ++j) {
+    const int T = fb_tile(j, kb, nt), pos = fb_pos(kb, T, nkb, nt);
+    const int P = j & 1;
+    // the lane index made opaque per step: every lane-derived LDS address (swizzled, ~40 distinct ones) is
+    // recomputed in the step instead of hoisted to kernel entry and spilled around the loop
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    // the previous step's final dQ rows (staged in dqo behind its last barrier): whole 128-B rows
+    if (prev_final) {
+      const int r = t >> 3, c = t & 7, q = prev_T * 64 + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
+      if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+    }
+    if (j + 1 < nt) {
+      const int T1 = fb_tile(j + 1, kb, nt);
+      qd.issue(lds + FBL_Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      gd.issue(lds + FBL_G + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      fd.issue(reinterpret_cast<bf16*>(lds + FBL_F + (P ^ 1) * 2048), (unsigned)T1 * 64u, wave, lane);
+    }
+    const bf16* Q_ = reinterpret_cast<const bf16*>(lds + FBL_Q + P * 8192);
+    const bf16* G_ = reinterpret_cast<const bf16*>(lds + FBL_G + P * 8192);
+    const bf16* F_ = reinterpret_cast<const bf16*>(lds + FBL_F + P * 2048);
+    // the running sum of tile T so far (its predecessor's flag was matched last step), sc1 to registers,
+    // issued half way through the tile body (flies under the second half)
+    u32x4 run[4];
+    auto load_run = [&]() __attribute__((always_inline)) {
+      if (kh == 0 && pos > 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * FB_TILE + wave * FB_SUB + g * 1024, 16);
+      }
+    };
+    if (T == nt - 1 && nt * 64 != N)
+      fb_tile_body<true>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
+    else
+      fb_tile_body<false>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // B1: dS^T of all 256 keys in LDS
+    __builtin_amdgcn_sched_barrier(0);
+    // dQ^T (32 d x 32 q sub-tile (dh, qh)) over this wave's key half: K^T from Kt, dS^T from dsT
+    f32x16 dq = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int k0 = kh * 128 + 16 * ks;
+      dq = mfma(frag_tr_sw(Kt, k0, 32 * dh, lane), frag_tr_sw(dsT, k0, 32 * qh, lane), dq);
+    }
+    if (kh == 1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(red + (wave - 4) * (FB_SUB / 4) + g * 256 + lane * 4) =
+            f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+    }
+    if (wave == 0 && j + 1 < nt) {  // the next tile's predecessor (one step of slack in lockstep)
+      const int T1 = fb_tile(j + 1, kb, nt), p1 = fb_pos(kb, T1, nkb, nt);
+      if (p1 > 0) fb_wait(fl + T1, (unsigned)p1, err);
+    }
+    // every wave: the next tile's DMA, this tile's running-sum loads and the previous sum's stores are done
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // B2
+    __builtin_amdgcn_sched_barrier(0);
+    if (wave == 0 && lane == 0 && prev_T >= 0 && prev_pos < last) fb_st_flag(fl + prev_T, (unsigned)(prev_pos + 1));
+    const bool final = pos == last;
+    if (kh == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(red + wave * (FB_SUB / 4) + g * 256 + lane * 4);
+        v += f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+        if (pos > 0) v += __builtin_bit_cast(f32x4, run[g]);
+        if (!final) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cr, lane * 16,
+                                                 T * FB_TILE + wave * FB_SUB + g * 1024, 16);
+        } else {  // rows d = 32 dh + 8 g + 4 h + 0..3 of query 32 qh + (lane & 31)
+          const int q = 32 * qh + (lane & 31), d0 = 32 * dh + 8 * g + 4 * (lane >> 5);
+          *reinterpret_cast<bf16x4*>(dqo + q * LROW + d0) =
+              bf16x4{(bf16)(v[0] * scale), (bf16)(v[1] * scale), (bf16)(v[2] * scale), (bf16)(v[3] * scale)};
+        }
+      }
+    }
+    if (final) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // B3: dqo complete (stored at the top of the next step)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    prev_T = T; prev_pos = pos; prev_final = final;
+  }
+  // the last step's running sum: drained by every storing wave, then published
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave == 0 && lane == 0 && prev_pos < last) fb_st_flag(fl + prev_T, (unsigned)(prev_pos + 1));
+  if (prev_final) {
+    const int r = t >> 3, c = t & 7, q = prev_T * 64 + r;
+    const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
+    if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+  }
+  // dK, dV: staged through the dS^T image as [key][d] rows, stored as whole 128-B rows
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const f32x16* acc = which == 0 ? dk : dv;
+    const float sc = which == 0 ? dk_scale : 1.f;
+    __syncthreads();
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * h2 + 8 * g + 4 * (lane >> 5);
+        *reinterpret_cast<bf16x4*>(dsT + sw_off(32 * wave + (lane & 31), d0)) =
+            bf16x4{(bf16)(acc[h2][4 * g] * sc), (bf16)(acc[h2][4 * g + 1] * sc), (bf16)(acc[h2][4 * g + 2] * sc),
+                   (bf16)(acc[h2][4 * g + 3] * sc)};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 64 * i + (t >> 3), c = t & 7, k = kb * FB_K + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(dsT + sw_off(r, c * 8));
+      if (k < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + k) * ldt + (1 + which) * H * D + hd * D + c * 8) = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ f32 path
 // Reference-precision kernels (exact f32 arithmetic, no flash tiling) used when the model runs
 // in f32 for parity; one wave per query (forward, dQ) or per key (dK/dV); scores staged in LDS.
@@ -951,15 +1273,37 @@ extern "C" int mia_attn_fwd_mx(const void* qkv, void* out, float* lse, void* q8,
   return 0;
 }
 
+// bf16 workspace: [Q' rows x 64 bf16][fragment rows: rows x 32 B][fused form: flags (B*H*nt u32) + error
+// word, one 256-B-aligned block zeroed per call][running dQ sums: B*H*nt x 16 KB f32]
+static int64_t round256(int64_t x) { return (x + 255) / 256 * 256; }
+static int64_t fb_flags_offset(int32_t B, int32_t N, int32_t H) {
+  const int64_t rows = (int64_t)B * N * H;
+  return round256(rows * D * 2 + rows * 32);
+}
+static int64_t fb_flags_bytes(int32_t B, int32_t N, int32_t H) { return round256(((int64_t)B * H * cdiv(N, 64) + 1) * 4); }
+
+// the fused form needs every chain gap >= FB_LAG steps (so a block only ever waits for a contribution made
+// at an earlier step): nkb == 1, or nt - FB_LAG (nkb - 1) >= FB_LAG; N in (256, 384] falls back
+static bool fb_ok(int32_t N) {
+  const int nt = (int)cdiv(N, 64), nkb = (int)cdiv(N, FB_K);
+  return nkb == 1 || nt - FB_LAG * (nkb - 1) >= FB_LAG;
+}
+
 extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_t H) {
   const int64_t rows = (int64_t)B * N * H;
   if (dtype == MIA_F32) return rows * 4;  // delta
-  return rows * D * 2 + rows * 32;        // Q' + fragment rows
+  return fb_flags_offset(B, N, H) + fb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * FB_TILE;
+}
+
+// byte offset in the bf16 workspace of the fused backward's error word: 0 after a call = every dQ hand-off
+// matched; non-zero = a bounded wait gave up (dQ of that call is not valid)
+extern "C" int64_t mia_attn_bwd_error_offset(int32_t B, int32_t N, int32_t H) {
+  return fb_flags_offset(B, N, H) + (int64_t)B * H * cdiv(N, 64) * 4;
 }
 
 static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                          void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale, int q_ready,
-                         mia_stream_t stream) {
+                         int fused, mia_stream_t stream) {
   MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && work, "attn_bwd: null pointer");
   MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_bwd: bad shape");
   hipStream_t s = as_stream(stream);
@@ -990,6 +1334,22 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
                                                                      (const bf16*)dout, lse, qs, frag, B, N, H,
                                                                      scale_log2, q_ready ? 0 : 1);
   MIA_LAUNCH_CHECK("attn_bwd_prep");
+  if (fused && fb_ok(N)) {
+    const int nkb = (int)cdiv(N, FB_K);
+    MIA_CHECK_ARG((int64_t)nkb * B * H < (1ll << 31) && (int64_t)cdiv(N, 64) * FB_TILE < (1ll << 31),
+                  "attn_bwd: grid too large");
+    char* wb = reinterpret_cast<char*>(work);
+    unsigned* flags = reinterpret_cast<unsigned*>(wb + fb_flags_offset(B, N, H));
+    float* chain = reinterpret_cast<float*>(wb + fb_flags_offset(B, N, H) + fb_flags_bytes(B, N, H));
+    // every flag and the error word start at 0 in each call (stream-ordered, no host sync)
+    hipError_t e = hipMemsetAsync(flags, 0, (size_t)fb_flags_bytes(B, N, H), s);
+    if (e != hipSuccess) return mia::fail(-(int)e, "attn_bwd: memset: %s", hipGetErrorString(e));
+    attn_bwd_fused_kernel<<<(unsigned)(nkb * B * H), 512, 0, s>>>(
+        (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
+        flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb, scale, 1.f / LOG2E);
+    MIA_LAUNCH_CHECK("attn_bwd_fused");
+    return 0;
+  }
   const int nkb = (int)cdiv(N, BWD_K), nqb = (int)cdiv(N, BWD_Q);
   attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag,
                                                                (bf16*)dqkv, N, H, nkb, 1.f / LOG2E);
@@ -1003,7 +1363,15 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
 extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                             void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
                             mia_stream_t stream) {
-  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, dtype, B, N, H, scale, 0, stream);
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, dtype, B, N, H, scale, 0, 1, stream);
+}
+
+// the bf16 backward in its two-kernel form (key-parallel dK/dV + query-parallel dQ, each recomputing S and
+// dP): the fused form's yardstick; q_ready = the forward wrote Q' into `work` (mia_attn_fwd_save_q)
+extern "C" int mia_attn_bwd_two_pass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                                     void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
+                                     mia_stream_t stream) {
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, q_ready, 0, stream);
 }
 
 // bf16 forward that also writes Q' (the backward's scaled query operand) into the backward workspace
@@ -1030,5 +1398,5 @@ extern "C" int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void*
 // the bf16 backward when the forward already wrote Q' into `work` (mia_attn_fwd_save_q)
 extern "C" int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                                     void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream) {
-  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, stream);
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, 1, stream);
 }
