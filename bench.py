@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--probe", default=None, help="comma list of probe tags to time live (default: auto)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N > 1 ranks on one GPU")
+    ap.add_argument("--fc1-exchange", choices=["gather", "allreduce"], default="gather",
+                    help="N > 1, EnvNet FC1 weight gradient: all-gather the bf16 operands and defer the averaged "
+                         "gradient to the fused Adam GEMM (the N = 1 program), or materialise + chunked all-reduce")
     return ap.parse_args()
 
 
@@ -130,7 +133,7 @@ def build_envnet_step(args, dev, rank, world, B):
     model = EnvNetV2(num_classes=50, dropout=0.5, compute_dtype=args.dtype).to(dev).train()
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
     wav, labels, g = make_batch(B, 220_500, dev, rank)
-    ddp = GradAllReducer(model, world) if world > 1 else None
+    ddp = GradAllReducer(model, world, fc1_exchange=args.fc1_exchange) if world > 1 else None
 
     def step():
         x, y, _ = bc_mix(wav, labels, 50, gen=g)
@@ -299,8 +302,10 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
             dist.all_gather(every, mine)
             nbytes = sum(p.numel() * p.element_size() for p in ddp.params)
             comm = {"exposed_ms_per_step": [round(float(v), 3) for v in every],
-                    "allreduce_bytes_per_step": nbytes, "chunks_per_step": ddp.last_chunks,
-                    "backend": dist.get_backend()}
+                    "allreduce_bytes_per_step": nbytes - ddp.last_gathered_param_bytes,
+                    "allgather_bytes_per_rank_per_step": ddp.last_gathered_bytes,
+                    "chunks_per_step": ddp.last_chunks, "fc1_exchange": ddp.fc1_exchange,
+                    "gathered_per_step": ddp.last_gathered, "backend": dist.get_backend()}
             ddp.timing = None
     kstats = {}
     for tag, recs in probes.items():

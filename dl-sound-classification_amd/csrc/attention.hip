@@ -808,21 +808,23 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
 // anyway (FB_SPIN_TICKS of the 100 MHz real-time counter) and a timeout is recorded in the workspace's
 // error word (mia_attn_bwd_error_offset) instead of hanging the GPU.  Bit-reproducible: the order is a
 // fixed function of (kb, T, N).
-constexpr int FB_K = 256;        // keys per workgroup: 8 waves x 32
 constexpr int FB_LAG = 3;        // rotation lag between consecutive key blocks of one (b, h)
 constexpr int FB_SUB = 4096;     // bytes of one 32 x 32 f32 dQ^T sub-tile in register order
 constexpr int FB_TILE = 4 * FB_SUB;
 constexpr unsigned long long FB_SPIN_TICKS = 20000000ull;  // 200 ms at 100 MHz
 
-// LDS map of the fused kernel (one __shared__ array)
-constexpr int FBL_Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
-constexpr int FBL_G = FBL_Q + 2 * 8192;         // [2][64][64] bf16 dO tiles (sw_off)
-constexpr int FBL_F = FBL_G + 2 * 8192;         // [2][2][64][8] bf16 fifth-k-step rows
-constexpr int FBL_K = FBL_F + 2 * 2048;         // [256][64] bf16 the block's keys (sw_off)
-constexpr int FBL_S = FBL_K + 32768;            // [256][64] bf16 dS^T of the current tile (sw_off)
-constexpr int FBL_R = FBL_S + 32768;            // [4][4096 B] f32 key-half partials (register order)
-constexpr int FBL_O = FBL_R + 4 * FB_SUB;       // [64][72] bf16 final dQ rows
-constexpr int FBL_BYTES = FBL_O + 64 * LROW * 2;
+// LDS map of the fused kernel (one __shared__ array); NW waves = 32 NW keys per workgroup
+template <int NW>
+struct FbLds {
+  static constexpr int Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
+  static constexpr int G = Q + 2 * 8192;             // [2][64][64] bf16 dO tiles (sw_off)
+  static constexpr int F = G + 2 * 8192;             // [2][2][64][8] bf16 fifth-k-step rows
+  static constexpr int K = F + 2 * 2048;             // [32 NW][64] bf16 the block's keys (sw_off)
+  static constexpr int S = K + NW * 4096;            // [32 NW][64] bf16 dS^T of the current tile (sw_off)
+  static constexpr int R = S + NW * 4096;            // NW = 8: [4][4096 B] f32 key-half partials
+  static constexpr int O = R + (NW == 8 ? 4 * FB_SUB : 0);  // [64][72] bf16 final dQ rows
+  static constexpr int BYTES = O + 64 * LROW * 2;
+};
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -864,17 +866,25 @@ __device__ __forceinline__ int fb_pos(int kb, int T, int nkb, int nt) {
   return p;
 }
 
-// one 64-row tile by LDS-DMA with 8 waves: wave w loads rows 8w .. 8w + 7 (one 1-KB piece)
-struct TileDMA8 {
+// one 64-row tile by LDS-DMA with NW waves: wave w loads the 8 / NW pieces (8 rows, 1 KB) from 8w / NW
+template <int NW>
+struct TileDMAn {
+  static constexpr int PW = 8 / NW;
   __amdgpu_buffer_rsrc_t rsrc;
-  unsigned voff;
+  unsigned voff[PW];
   __device__ __forceinline__ void init(const bf16* g, int64_t ld, int N, int wave, int lane) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(((int64_t)(N - 1) * ld + 64) * 2), 0x00020000);
-    const int r = 8 * wave + (lane >> 3);
-    voff = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int r = 8 * (PW * wave + i) + (lane >> 3);
+      voff[i] = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
+    }
   }
   __device__ __forceinline__ void issue(char* tile, unsigned row0_bytes, int wave) const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 1024), 16, voff, row0_bytes, 0, 0);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + (PW * wave + i) * 1024), 16, voff[i], row0_bytes,
+                                               0, 0);
   }
 };
 
@@ -924,12 +934,14 @@ __device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], c
   }
 }
 
-__global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                             const bf16* __restrict__ qs, const bf16* __restrict__ frag,
-                                                             bf16* __restrict__ dqkv, float* chain, unsigned* flags,
-                                                             unsigned* err, int N, int H, int nkb, float scale,
-                                                             float dk_scale) {
-  __shared__ __attribute__((aligned(1024))) char lds[FBL_BYTES];
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const bf16* __restrict__ qs,
+    const bf16* __restrict__ frag, bf16* __restrict__ dqkv, float* chain, unsigned* flags, unsigned* err, int N,
+    int H, int nkb, float scale, float dk_scale, int dbg) {
+  using Lm = FbLds<NW>;
+  constexpr int FB_K = 32 * NW, NT = 64 * NW;
+  __shared__ __attribute__((aligned(1024))) char lds[Lm::BYTES];
   const int t = threadIdx.x, lane0 = t & 63;
   int lane = lane0;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -939,11 +951,11 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
   const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
-  bf16* const Kt = reinterpret_cast<bf16*>(lds + FBL_K);
-  bf16* const dsT = reinterpret_cast<bf16*>(lds + FBL_S);
-  float* const red = reinterpret_cast<float*>(lds + FBL_R);
-  bf16* const dqo = reinterpret_cast<bf16*>(lds + FBL_O);
-  // the block's 256 keys -> Kt (wave w: its own 32 keys, 4 pieces; keys past N read as zeros)
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + Lm::K);
+  bf16* const dsT = reinterpret_cast<bf16*>(lds + Lm::S);
+  float* const red = reinterpret_cast<float*>(lds + Lm::R);
+  bf16* const dqo = reinterpret_cast<bf16*>(lds + Lm::O);
+  // the block's keys -> Kt (wave w: its own 32 keys, 4 pieces; keys past N read as zeros)
   {
     const __amdgpu_buffer_rsrc_t kr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
@@ -951,20 +963,20 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     for (int i = 0; i < 4; ++i) {
       const int rl = 32 * wave + 8 * i + (lane >> 3);  // local key row
       const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + FBL_K + (4 * wave + i) * 1024), 16, vo,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + Lm::K + (4 * wave + i) * 1024), 16, vo,
                                                (unsigned)((int64_t)(kb * FB_K + 32 * wave + 8 * i) * ldt * 2), 0, 0);
     }
   }
-  TileDMA8 qd, gd;
+  TileDMAn<NW> qd, gd;
   FragDMA fd;
   qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   fd.init(frag + (int64_t)bh * 2 * N * 8, N);
   {
     const int T0 = fb_tile(0, kb, nt);
-    qd.issue(lds + FBL_Q, (unsigned)T0 * tile_bytes, wave);
-    gd.issue(lds + FBL_G, (unsigned)T0 * tile_bytes, wave);
-    fd.issue(reinterpret_cast<bf16*>(lds + FBL_F), (unsigned)T0 * 64u, wave, lane);
+    qd.issue(lds + Lm::Q, (unsigned)T0 * tile_bytes, wave);
+    gd.issue(lds + Lm::G, (unsigned)T0 * tile_bytes, wave);
+    fd.issue(reinterpret_cast<bf16*>(lds + Lm::F), (unsigned)T0 * 64u, wave, lane);
   }
   const int key = kb * FB_K + wave * 32 + (lane & 31);
   const bool key_ok = key < N;
@@ -979,7 +991,8 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
       (void*)(chain + (int64_t)bh * nt * (FB_TILE / 4)), 0, nt * FB_TILE, 0x00020000);
   unsigned* const fl = flags + (int64_t)bh * nt;
   const int last = nkb - 1;
-  const int dh = wave & 1, qh = (wave >> 1) & 1, kh = wave >> 2;  // this wave's dQ^T sub-tile and key half
+  // this wave's dQ^T sub-tile and key half (NW = 4: every wave a whole sub-tile over all 128 keys)
+  const int dh = wave & 1, qh = (wave >> 1) & 1, kh = NW == 8 ? wave >> 2 : 0;
   if (wave == 0) {
     const int T0 = fb_tile(0, kb, nt), p0 = fb_pos(kb, T0, nkb, nt);
     if (p0 > 0) fb_wait(fl + T0, (unsigned)p0, err);
@@ -997,24 +1010,27 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     asm volatile("" : "+v"(lane));
     // the previous step's final dQ rows (staged in dqo behind its last barrier): whole 128-B rows
     if (prev_final) {
-      const int r = t >> 3, c = t & 7, q = prev_T * 64 + r;
-      const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
-      if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+#pragma unroll
+      for (int i = 0; i < 512 / NT; ++i) {
+        const int r = (t >> 3) + i * (NT / 8), c = t & 7, q = prev_T * 64 + r;
+        const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
+        if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+      }
     }
     if (j + 1 < nt) {
       const int T1 = fb_tile(j + 1, kb, nt);
-      qd.issue(lds + FBL_Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
-      gd.issue(lds + FBL_G + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
-      fd.issue(reinterpret_cast<bf16*>(lds + FBL_F + (P ^ 1) * 2048), (unsigned)T1 * 64u, wave, lane);
+      qd.issue(lds + Lm::Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      gd.issue(lds + Lm::G + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      fd.issue(reinterpret_cast<bf16*>(lds + Lm::F + (P ^ 1) * 2048), (unsigned)T1 * 64u, wave, lane);
     }
-    const bf16* Q_ = reinterpret_cast<const bf16*>(lds + FBL_Q + P * 8192);
-    const bf16* G_ = reinterpret_cast<const bf16*>(lds + FBL_G + P * 8192);
-    const bf16* F_ = reinterpret_cast<const bf16*>(lds + FBL_F + P * 2048);
+    const bf16* Q_ = reinterpret_cast<const bf16*>(lds + Lm::Q + P * 8192);
+    const bf16* G_ = reinterpret_cast<const bf16*>(lds + Lm::G + P * 8192);
+    const bf16* F_ = reinterpret_cast<const bf16*>(lds + Lm::F + P * 2048);
     // the running sum of tile T so far (its predecessor's flag was matched last step), sc1 to registers,
     // issued half way through the tile body (flies under the second half)
     u32x4 run[4];
     auto load_run = [&]() __attribute__((always_inline)) {
-      if (kh == 0 && pos > 0) {
+      if (kh == 0 && pos > 0 && !(dbg & 4)) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * FB_TILE + wave * FB_SUB + g * 1024, 16);
@@ -1030,18 +1046,19 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     __builtin_amdgcn_sched_barrier(0);
     // dQ^T (32 d x 32 q sub-tile (dh, qh)) over this wave's key half: K^T from Kt, dS^T from dsT
     f32x16 dq = zero16();
+    if (!(dbg & 2))
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const int k0 = kh * 128 + 16 * ks;
       dq = mfma(frag_tr_sw(Kt, k0, 32 * dh, lane), frag_tr_sw(dsT, k0, 32 * qh, lane), dq);
     }
-    if (kh == 1) {
+    if (NW == 8 && kh == 1) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(red + (wave - 4) * (FB_SUB / 4) + g * 256 + lane * 4) =
             f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
     }
-    if (wave == 0 && j + 1 < nt) {  // the next tile's predecessor (one step of slack in lockstep)
+    if (wave == 0 && j + 1 < nt && !(dbg & 1)) {  // the next tile's predecessor (one step of slack in lockstep)
       const int T1 = fb_tile(j + 1, kb, nt), p1 = fb_pos(kb, T1, nkb, nt);
       if (p1 > 0) fb_wait(fl + T1, (unsigned)p1, err);
     }
@@ -1055,10 +1072,10 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     if (kh == 0) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(red + wave * (FB_SUB / 4) + g * 256 + lane * 4);
-        v += f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
-        if (pos > 0) v += __builtin_bit_cast(f32x4, run[g]);
-        if (!final) {
+        f32x4 v = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+        if constexpr (NW == 8) v = *reinterpret_cast<const f32x4*>(red + wave * (FB_SUB / 4) + g * 256 + lane * 4) + v;
+        if (pos > 0 && !(dbg & 4)) v += __builtin_bit_cast(f32x4, run[g]);
+        if (!final && !(dbg & 4)) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cr, lane * 16,
                                                  T * FB_TILE + wave * FB_SUB + g * 1024, 16);
         } else {  // rows d = 32 dh + 8 g + 4 h + 0..3 of query 32 qh + (lane & 31)
@@ -1081,9 +1098,12 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
   __syncthreads();
   if (wave == 0 && lane == 0 && prev_pos < last) fb_st_flag(fl + prev_T, (unsigned)(prev_pos + 1));
   if (prev_final) {
-    const int r = t >> 3, c = t & 7, q = prev_T * 64 + r;
-    const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
-    if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+#pragma unroll
+    for (int i = 0; i < 512 / NT; ++i) {
+      const int r = (t >> 3) + i * (NT / 8), c = t & 7, q = prev_T * 64 + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
+      if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
+    }
   }
   // dK, dV: staged through the dS^T image as [key][d] rows, stored as whole 128-B rows
 #pragma unroll
@@ -1103,7 +1123,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = 64 * i + (t >> 3), c = t & 7, k = kb * FB_K + r;
+      const int r = (NT / 8) * i + (t >> 3), c = t & 7, k = kb * FB_K + r;
       const uint4 v = *reinterpret_cast<const uint4*>(dsT + sw_off(r, c * 8));
       if (k < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + k) * ldt + (1 + which) * H * D + hd * D + c * 8) = v;
     }
@@ -1284,6 +1304,9 @@ static int64_t fb_flags_bytes(int32_t B, int32_t N, int32_t H) { return round256
 
 // the fused form needs every chain gap >= FB_LAG steps (so a block only ever waits for a contribution made
 // at an earlier step): nkb == 1, or nt - FB_LAG (nkb - 1) >= FB_LAG; N in (256, 384] falls back
+static int g_attn_dbg = 0;  // EXPERIMENT: 1 no waits, 2 no dQ MFMAs, 4 no running-sum traffic
+extern "C" int mia_attn_debug_mode(int32_t m) { g_attn_dbg = m; return 0; }
+constexpr int FB_K = 256;  // keys per workgroup of the production (8-wave) form
 static bool fb_ok(int32_t N) {
   const int nt = (int)cdiv(N, 64), nkb = (int)cdiv(N, FB_K);
   return nkb == 1 || nt - FB_LAG * (nkb - 1) >= FB_LAG;
@@ -1344,9 +1367,16 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
     // every flag and the error word start at 0 in each call (stream-ordered, no host sync)
     hipError_t e = hipMemsetAsync(flags, 0, (size_t)fb_flags_bytes(B, N, H), s);
     if (e != hipSuccess) return mia::fail(-(int)e, "attn_bwd: memset: %s", hipGetErrorString(e));
-    attn_bwd_fused_kernel<<<(unsigned)(nkb * B * H), 512, 0, s>>>(
-        (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
-        flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb, scale, 1.f / LOG2E);
+    if (g_attn_dbg & 16) {  // EXPERIMENT: 4-wave form (128 keys; chain positions are NOT valid: waits off)
+      const int nkb4 = (int)cdiv(N, 128);
+      attn_bwd_fused_kernel<4><<<(unsigned)(nkb4 * B * H), 256, 0, s>>>(
+          (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
+          flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb4, scale, 1.f / LOG2E, g_attn_dbg | 1);
+    } else {
+      attn_bwd_fused_kernel<8><<<(unsigned)(nkb * B * H), 512, 0, s>>>(
+          (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
+          flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb, scale, 1.f / LOG2E, g_attn_dbg);
+    }
     MIA_LAUNCH_CHECK("attn_bwd_fused");
     return 0;
   }

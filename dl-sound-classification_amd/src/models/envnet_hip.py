@@ -291,6 +291,7 @@ class EnvNetFunction(torch.autograd.Function):
         keep_scale = 1.0 / (1.0 - s["drop_p"]) if s["drop_p"] > 0 else 1.0
         ready = getattr(ctx.model, "_grad_ready", None)
         chunk_ready = getattr(ctx.model, "_grad_chunk_ready", None)
+        gather = getattr(ctx.model, "_grad_gather", None)
 
         def emit(lo, hi):
             # hand finished gradients to the data-parallel reducer now (overlaps the rest of the
@@ -308,8 +309,14 @@ class EnvNetFunction(torch.autograd.Function):
             Wt = s["wfc"][li]
             fout, fin = Wt.shape
             hin = acts[li]
-            dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
-            if li == 0 and chunk_ready is not None and fout % FC1_CHUNK_ROWS == 0 and fout > FC1_CHUNK_ROWS:
+            dW = torch.empty(fout, fin, dtype=torch.float32, device=dev) if li > 0 else None
+            if (li == 0 and gather is not None and cd == L.BF16 and fout % 128 == 0 and fin % 128 == 0
+                    and B % 64 == 0 and gather(p[40], dcur, hin)):
+                # data-parallel, gather form (ddp.py): the operands went to the reducer, which defers the
+                # averaged gradient over every rank's rows to FusedAdam; nothing to write here
+                pass
+            elif li == 0 and chunk_ready is not None and fout % FC1_CHUNK_ROWS == 0 and fout > FC1_CHUNK_ROWS:
+                dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
                 # data-parallel: FC1's 1.38 GB weight gradient as row chunks of 86.5 MB, each all-reduced
                 # as soon as its GEMM is enqueued (the reducer averages it in place; the per-tile sums of
                 # squares would describe the un-averaged gradient, so none are written)
@@ -325,8 +332,9 @@ class EnvNetFunction(torch.autograd.Function):
                 # of squares now, the product recomputed inside the fused Adam GEMM at the step
                 K.defer_weight_grad(p[40], K.dense(dcur, L.RC, B, fout), K.dense(hin, L.RC, B, fin), fout, fin, B,
                                     keep=(dcur, hin), tag="fc1.wgrad")
-                dW = None
             else:
+                if dW is None:
+                    dW = torch.empty(fout, fin, dtype=torch.float32, device=dev)
                 # FC1/FC2: the GEMM epilogue also writes per-tile sums of squares of dW, so the clip-norm
                 # pass of FusedAdam does not re-read the 1.4 GB (K.sqsum_slots)
                 sq = K.sqsum_slots(dW, fout, fin) if li < 2 else None

@@ -17,6 +17,18 @@ as 16 weight-gradient GEMMs of 256 rows (86.5 MB each) and every chunk's all-red
 soon as its GEMM is enqueued, so the transfer of the largest gradient starts after 1/16 of its
 GEMM instead of after all of it (64-128 MB chunks, FC head first).
 
+``fc1_exchange`` chooses how a gradient that FusedAdam could take deferred (EnvNet's FC1: dW = dY^T X,
+never written on one GPU; src/miaudio/kernels.py::defer_weight_grad) crosses the ranks:
+
+* ``"gather"`` (default): the backward hands the reducer its two bf16 operands instead of the product;
+  the reducer all-gathers dY (B x 4096, pre-scaled by 1/world) and X (B x 84 480) on the comm stream --
+  45 MB per rank instead of a 1.38 GB f32 ring all-reduce -- and ``finish()`` defers the AVERAGED gradient
+  (dY_all / world)^T X_all, K = world * B, to FusedAdam exactly as one GPU does.  Every rank runs the same
+  sums-only and Adam GEMMs on identical operands, so the parameters stay identical bit for bit, and the
+  per-GPU program at N > 1 is the N = 1 program with K = world * B in those two GEMMs;
+* ``"allreduce"``: FC1's gradient is materialised as 16 row chunks, each all-reduced as its GEMM is enqueued
+  (above).
+
 The per-step BatchNorm buffer broadcast (DDP ``broadcast_buffers``) is one coalesced collective per
 dtype, issued after the gradient exchange.  torch DDP broadcasts rank 0's buffers at the start of
 each forward; the values it sends there (rank 0's statistics after the previous step's forward) are
@@ -36,7 +48,10 @@ BUCKET_BYTES = 64 << 20
 
 class GradAllReducer:
     def __init__(self, model: torch.nn.Module, world: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 broadcast_buffers: bool = True):
+                 broadcast_buffers: bool = True, fc1_exchange: str = "gather"):
+        if fc1_exchange not in ("gather", "allreduce"):
+            raise ValueError(f"fc1_exchange must be 'gather' or 'allreduce', not {fc1_exchange!r}")
+        self.fc1_exchange = fc1_exchange
         self.model = model
         self.world = world or dist.get_world_size()
         self.params = [p for p in model.parameters() if p.requires_grad]
@@ -56,6 +71,11 @@ class GradAllReducer:
         for m in model.modules():
             m._grad_ready = self.grad_ready
             m._grad_chunk_ready = self.grad_chunk_ready
+            m._grad_gather = self.grad_gather if fc1_exchange == "gather" else None
+        self.gathers = []  # (param, dY_all, X_all, M, N, K) launched this step, deferred in finish()
+        self.gathered = self.last_gathered = 0
+        self.gathered_bytes = self.last_gathered_bytes = 0            # operand bytes each rank sends
+        self.gathered_param_bytes = self.last_gathered_param_bytes = 0  # f32 gradient bytes not all-reduced
         self.fired = self.last_fired = 0  # gradients received through _grad_ready per step (tests)
         self.chunks = self.last_chunks = 0  # row chunks launched through _grad_chunk_ready per step
         self.timing = None
@@ -114,6 +134,52 @@ class GradAllReducer:
             self.done.add(id(param))
             self.fired += 1
 
+    def _all_gather(self, out, inp):
+        """out (world * rows, cols) <- the ranks' inp (rows, cols) in rank order."""
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(out, inp)
+        else:  # gloo (rehearsal / CPU tests): list form, then the rank-ordered copy
+            parts = list(out.chunk(self.world, 0))
+            tmp = [torch.empty_like(inp) for _ in range(self.world)]
+            dist.all_gather(tmp, inp)
+            for d, t in zip(parts, tmp):
+                d.copy_(t)
+
+    def grad_gather(self, param, dy, x) -> bool:
+        """Called from inside the backward for a weight gradient dW = dy^T x (dy: (B, M), x: (B, N), bf16)
+        that FusedAdam may take deferred.  Returns False (the caller materialises dW as usual) unless the
+        parameter defers; otherwise the operands leave now on the comm stream and ``finish()`` defers the
+        averaged gradient over all ranks' rows."""
+        from ..miaudio import kernels as K
+        if id(param) not in self.index or id(param) in self.done or not K.defers_to_fused_adam(param):
+            return False
+        B, M = dy.shape
+        N = x.shape[1]
+        dy_all = torch.empty(self.world * B, M, dtype=dy.dtype, device=dy.device)
+        x_all = torch.empty(self.world * B, N, dtype=x.dtype, device=x.device)
+
+        def run():
+            dys = dy * (1.0 / self.world)  # exact in bf16 for a power-of-two world
+            self._all_gather(dy_all, dys)
+            self._all_gather(x_all, x)
+            return dys
+
+        if self.cuda:
+            ev = torch.cuda.current_stream().record_event()
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                keep = run()
+            for t in (dy, x, dy_all, x_all, keep):
+                t.record_stream(self.stream)
+        else:
+            run()
+        self.gathers.append((param, dy_all, x_all, M, N, self.world * B))
+        self.done.add(id(param))
+        self.gathered += 1
+        self.gathered_bytes += (dy.numel() + x.numel()) * dy.element_size()
+        self.gathered_param_bytes += param.numel() * 4
+        return True
+
     def exposed_ms(self):
         """Mean over the recorded steps of the time the exchange ran past the end of the backward."""
         if not self.timing:
@@ -145,6 +211,13 @@ class GradAllReducer:
             self.timing.append((t0, t1))
         if self.cuda:
             torch.cuda.current_stream().wait_stream(self.stream)
+        if self.gathers:
+            from ..miaudio import kernels as K
+            from ..miaudio import lib as L
+            for param, dy_all, x_all, M, N, Kk in self.gathers:
+                K.defer_weight_grad(param, K.dense(dy_all, L.RC, Kk, M), K.dense(x_all, L.RC, Kk, N), M, N, Kk,
+                                    keep=(dy_all, x_all), tag="fc1.wgrad")
+            self.gathers.clear()
         for flat, tensors, copied in self.pending:
             if copied:
                 off = 0
@@ -156,6 +229,9 @@ class GradAllReducer:
         self.done.clear()
         self.last_fired, self.fired = self.fired, 0
         self.last_chunks, self.chunks = self.chunks, 0
+        self.last_gathered, self.gathered = self.gathered, 0
+        self.last_gathered_bytes, self.gathered_bytes = self.gathered_bytes, 0
+        self.last_gathered_param_bytes, self.gathered_param_bytes = self.gathered_param_bytes, 0
         if self.broadcast_buffers:
             self._broadcast_buffers()
 

@@ -155,7 +155,9 @@ def _to(batch, dev):
 class Trainer:
     def __init__(self, max_epochs=1, accelerator="auto", precision=32, devices=1, log_every_n_steps=50,
                  gradient_clip_val=0.0, logger=None, callbacks=None, limit_train_batches=None,
-                 limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, **unused):
+                 limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, fc1_exchange="gather",
+                 **unused):
+        self.fc1_exchange = str(fc1_exchange)  # DDP: how FC1's deferred weight gradient crosses ranks (ddp.py)
         self.max_epochs = int(max_epochs)
         self.gradient_clip_val = float(gradient_clip_val or 0.0)
         self.precision = str(precision)
@@ -292,7 +294,7 @@ class Trainer:
             start_epoch = ck.get("epoch", -1) + 1
         if self.world > 1:
             from .ddp import GradAllReducer
-            self.ddp = GradAllReducer(module, self.world)
+            self.ddp = GradAllReducer(module, self.world, fc1_exchange=self.fc1_exchange)
         if self.logger is not None and self.is_global_zero:
             self.logger.log_hyperparams(module.hparams)
         fused_clip = getattr(self.optimizer, "handles_clipping", False)

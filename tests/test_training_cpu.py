@@ -496,3 +496,60 @@ def test_trainer_runs_modelcheckpoint_last(tmp_path):
         for cb in tr.callbacks:
             cb.on_epoch_end(tr, _M, {"val/acc": v, "epoch": ep})
     assert saved["es"] == {"best": 0.7, "wait": 0}
+
+
+class _Owner:  # stands in for a live FusedAdam (the parameter defers while its owner is alive)
+    pass
+
+
+def _gather_worker(rank, world, port, q):
+    """GradAllReducer(fc1_exchange="gather") plumbing on CPU/gloo: the backward hands (param, dY, X) to
+    ``_grad_gather``; ``finish()`` must defer ONE gradient over the rank-ordered concatenation of every
+    rank's rows, with dY pre-scaled by 1/world (so (dY_all)^T X_all is the averaged gradient).  The HIP
+    sums-only GEMM is replaced by a recorder (no GPU here); the GPU test runs the real one."""
+    import weakref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src.miaudio import kernels as K
+    from src.training.ddp import GradAllReducer
+    rec = []
+    K.defer_weight_grad = lambda p, A, B, M, N, Kk, keep, tag=None: rec.append((keep, M, N, Kk))
+    lin = torch.nn.Linear(6, 4)
+    owner = _Owner()
+    lin.weight._mia_fused_adam = weakref.ref(owner)
+    red = GradAllReducer(lin, world)
+    assert lin._grad_gather == red.grad_gather
+    g = torch.Generator().manual_seed(50 + rank)
+    dy, x = torch.randn(8, 4, generator=g), torch.randn(8, 6, generator=g)
+    assert red.grad_gather(lin.weight, dy, x)
+    assert not red.grad_gather(lin.bias, dy[:, :1].contiguous(), x)  # not deferrable: caller materialises
+    red.finish()
+    (dy_all, x_all), M, N, Kk = rec[0][0], rec[0][1], rec[0][2], rec[0][3]
+    q.put((rank, len(rec), (M, N, Kk), red.last_gathered, dy.numpy(), x.numpy(), dy_all.numpy(), x_all.numpy()))
+    dist.destroy_process_group()
+
+
+def test_grad_allreducer_fc1_gather_gloo():
+    import numpy as np
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, *rest = q.get(timeout=60)
+        res[r] = rest
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        n, shape, gathered, _, _, dy_all, x_all = res[r]
+        assert n == 1 and gathered == 1 and shape == (4, 6, 8 * world)
+        # identical operands on every rank: the ranks' rows in rank order, dY / world
+        np.testing.assert_array_equal(dy_all, np.concatenate([res[k][3] for k in range(world)]) / world)
+        np.testing.assert_array_equal(x_all, np.concatenate([res[k][4] for k in range(world)]))
+        avg = dy_all.T.astype(np.float64) @ x_all
+        want = sum(res[k][3].T.astype(np.float64) @ res[k][4] for k in range(world)) / world
+        np.testing.assert_allclose(avg, want, rtol=1e-6, atol=1e-7)

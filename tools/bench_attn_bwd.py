@@ -46,6 +46,22 @@ print("fused error word", int(work[off:off + 4].view(torch.int32).item()), flush
 d = (dq["fused"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
 print(f"fused vs two-pass: max |d| / max {float(d):.3g}", flush=True)
 flop = 8.0 * B * H * N * N * D  # 2x the forward, recompute not credited
+MODES = [int(v) for v in os.environ.get("MODES", "").split(",") if v]
+if MODES:
+    import ctypes
+    lib.mia_attn_debug_mode.argtypes = [ctypes.c_int32]
+    for r in range(2):
+        for m in MODES:
+            lib.mia_attn_debug_mode(m)
+            run("fused")
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(ITERS):
+                run("fused")
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"mode {m}: {e0.elapsed_time(e1) / ITERS:7.3f} ms", flush=True)
+    lib.mia_attn_debug_mode(0)
 for r in range(ROUNDS):
     for name in ("two", "fused"):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
