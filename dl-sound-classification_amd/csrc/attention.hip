@@ -797,34 +797,35 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
 //
 // dQ sums over the key blocks of one (b, h).  No float atomics (the sum would depend on arrival order):
 // an ORDERED HAND-OFF.  Key block kb walks the query tiles rotated by FB_LAG * kb (tile T at step
-// (T + FB_LAG kb) mod nt), and the blocks add their partial of tile T in the fixed order of the steps
-// at which they reach it: a running f32 sum in the workspace, the last block of the order writing bf16
-// dQ.  Each hand-off follows MI355X_MICROARCH.md's visibility table, row 1: every byte of the running
-// sum is stored and loaded `sc1` (16 B per lane, to registers), every storing wave waits vmcnt(0) before
-// a workgroup barrier behind which ONE lane stores the `sc1` flag; the consumer's wave 0 polls that flag
-// with `sc1` loads and the other waves load behind a barrier it joins.  The lag gives the predecessor
-// one whole step of slack.  A block waits only for contributions made at strictly earlier steps of
-// blocks dispatched before it or resident with it, so a chain cannot wait on itself; the spin is bounded
-// anyway (FB_SPIN_TICKS of the 100 MHz real-time counter) and a timeout is recorded in the workspace's
-// error word (mia_attn_bwd_error_offset) instead of hanging the GPU.  Bit-reproducible: the order is a
-// fixed function of (kb, T, N).
+// (T + FB_LAG kb) mod nt), and the blocks add their partial of tile T in the fixed order of the steps at
+// which they reach it: a running f32 sum in the workspace, the last block of the order writing bf16 dQ.
+// The tile's dQ^T is four 32 x 32 sub-tiles; waves 0-3 each own one (the partial of waves 4-7 -- the other
+// key half -- reaches them through LDS behind a per-wave LDS flag) and hand it off on their own: every
+// byte of the running sum is stored and loaded `sc1` (16 B per lane, to registers), the storing wave waits
+// vmcnt(0) before its `sc1` flag store, the consuming wave polls that flag with `sc1` loads before it loads
+// (MI355X_MICROARCH.md, visibility table row 1 with one storing wave per flag; Guideline 16 R1).  So a step
+// has ONE workgroup barrier (dS^T complete; dS^T is double-buffered).  Within a step a wave publishes its
+// previous sum before the barrier and polls for its next tile after it, so with a lag of >= 2 steps between
+// consecutive contributions a block only ever waits for an event earlier in (step, phase) order: a chain
+// cannot wait on itself.  The spin is bounded anyway (FB_SPIN_TICKS of the 100 MHz real-time counter) and a
+// timeout is recorded in the workspace's error word (mia_attn_bwd_error_offset) instead of hanging the GPU.
+// Bit-reproducible: the order is a fixed function of (kb, T, N).
+constexpr int FB_K = 256;        // keys per workgroup: 8 waves x 32
 constexpr int FB_LAG = 3;        // rotation lag between consecutive key blocks of one (b, h)
 constexpr int FB_SUB = 4096;     // bytes of one 32 x 32 f32 dQ^T sub-tile in register order
 constexpr int FB_TILE = 4 * FB_SUB;
+constexpr int FB_OP = 80;        // bytes per query row of a wave's staged bf16 dQ sub-tile (32 d + pad)
 constexpr unsigned long long FB_SPIN_TICKS = 20000000ull;  // 200 ms at 100 MHz
 
-// LDS map of the fused kernel (one __shared__ array); NW waves = 32 NW keys per workgroup
-template <int NW>
-struct FbLds {
-  static constexpr int Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
-  static constexpr int G = Q + 2 * 8192;             // [2][64][64] bf16 dO tiles (sw_off)
-  static constexpr int F = G + 2 * 8192;             // [2][2][64][8] bf16 fifth-k-step rows
-  static constexpr int K = F + 2 * 2048;             // [32 NW][64] bf16 the block's keys (sw_off)
-  static constexpr int S = K + NW * 4096;            // [32 NW][64] bf16 dS^T of the current tile (sw_off)
-  static constexpr int R = S + NW * 4096;            // NW = 8: [4][4096 B] f32 key-half partials
-  static constexpr int O = R + (NW == 8 ? 4 * FB_SUB : 0);  // [64][72] bf16 final dQ rows
-  static constexpr int BYTES = O + 64 * LROW * 2;
-};
+// LDS map (one __shared__ array)
+constexpr int FBL_Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
+constexpr int FBL_G = FBL_Q + 2 * 8192;         // [2][64][64] bf16 dO tiles (sw_off)
+constexpr int FBL_F = FBL_G + 2 * 8192;         // [2][2][64][8] bf16 fifth-k-step rows
+constexpr int FBL_K = FBL_F + 2 * 2048;         // [256][64] bf16 the block's keys (sw_off)
+constexpr int FBL_S = FBL_K + 32768;            // [2][256][64] bf16 dS^T (sw_off), double-buffered
+constexpr int FBL_R = FBL_S + 2 * 32768;        // [4][4096 B] key-half partials; reused as staged bf16 dQ
+constexpr int FBL_FL = FBL_R + 4 * FB_SUB;      // [4] int LDS flags: partial of step j ready (j + 1)
+constexpr int FBL_BYTES = FBL_FL + 64;
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -866,30 +867,22 @@ __device__ __forceinline__ int fb_pos(int kb, int T, int nkb, int nt) {
   return p;
 }
 
-// one 64-row tile by LDS-DMA with NW waves: wave w loads the 8 / NW pieces (8 rows, 1 KB) from 8w / NW
-template <int NW>
-struct TileDMAn {
-  static constexpr int PW = 8 / NW;
+// one 64-row tile by LDS-DMA with 8 waves: wave w loads rows 8w .. 8w + 7 (one 1-KB piece)
+struct TileDMA8 {
   __amdgpu_buffer_rsrc_t rsrc;
-  unsigned voff[PW];
+  unsigned voff;
   __device__ __forceinline__ void init(const bf16* g, int64_t ld, int N, int wave, int lane) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(((int64_t)(N - 1) * ld + 64) * 2), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int r = 8 * (PW * wave + i) + (lane >> 3);
-      voff[i] = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
-    }
+    const int r = 8 * wave + (lane >> 3);
+    voff = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
   }
   __device__ __forceinline__ void issue(char* tile, unsigned row0_bytes, int wave) const {
-#pragma unroll
-    for (int i = 0; i < PW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + (PW * wave + i) * 1024), 16, voff[i], row0_bytes,
-                                               0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 1024), 16, voff, row0_bytes, 0, 0);
   }
 };
 
-// S', dP' of 32 queries x this wave's 32 keys -> dS; dV^T, dK^T MFMAs; dS^T (bf16) into the LDS image
-// (K row fragments from the block's LDS image Kt, V fragments in registers; `mid` runs between the halves)
+// S', dP' of 32 queries x this wave's 32 keys -> dS; dV^T, dK^T MFMAs; dS^T (bf16) into the LDS image.
+// K row fragments from the block's LDS image Kt, V fragments in registers; `mid` runs between the halves.
 template <bool TAIL, class Mid>
 __device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
                                              const bf16* F_, const bf16* Kt, bf16* dsT, const bf16x8 (&vf)[4],
@@ -934,14 +927,12 @@ __device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], c
   }
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const bf16* __restrict__ qs,
-    const bf16* __restrict__ frag, bf16* __restrict__ dqkv, float* chain, unsigned* flags, unsigned* err, int N,
-    int H, int nkb, float scale, float dk_scale, int dbg) {
-  using Lm = FbLds<NW>;
-  constexpr int FB_K = 32 * NW, NT = 64 * NW;
-  __shared__ __attribute__((aligned(1024))) char lds[Lm::BYTES];
+__global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                             const bf16* __restrict__ qs, const bf16* __restrict__ frag,
+                                                             bf16* __restrict__ dqkv, float* chain, unsigned* flags,
+                                                             unsigned* err, int N, int H, int nkb, float scale,
+                                                             float dk_scale) {
+  __shared__ __attribute__((aligned(1024))) char lds[FBL_BYTES];
   const int t = threadIdx.x, lane0 = t & 63;
   int lane = lane0;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -951,11 +942,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
   const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
-  bf16* const Kt = reinterpret_cast<bf16*>(lds + Lm::K);
-  bf16* const dsT = reinterpret_cast<bf16*>(lds + Lm::S);
-  float* const red = reinterpret_cast<float*>(lds + Lm::R);
-  bf16* const dqo = reinterpret_cast<bf16*>(lds + Lm::O);
-  // the block's keys -> Kt (wave w: its own 32 keys, 4 pieces; keys past N read as zeros)
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + FBL_K);
+  volatile int* const lflag = reinterpret_cast<volatile int*>(lds + FBL_FL);
+  // the block's 256 keys -> Kt (wave w: its own 32 keys, 4 pieces; keys past N read as zeros)
   {
     const __amdgpu_buffer_rsrc_t kr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
@@ -963,20 +952,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
     for (int i = 0; i < 4; ++i) {
       const int rl = 32 * wave + 8 * i + (lane >> 3);  // local key row
       const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + Lm::K + (4 * wave + i) * 1024), 16, vo,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + FBL_K + (4 * wave + i) * 1024), 16, vo,
                                                (unsigned)((int64_t)(kb * FB_K + 32 * wave + 8 * i) * ldt * 2), 0, 0);
     }
   }
-  TileDMAn<NW> qd, gd;
+  if (t < 4) lflag[t] = 0;
+  TileDMA8 qd, gd;
   FragDMA fd;
   qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   fd.init(frag + (int64_t)bh * 2 * N * 8, N);
   {
     const int T0 = fb_tile(0, kb, nt);
-    qd.issue(lds + Lm::Q, (unsigned)T0 * tile_bytes, wave);
-    gd.issue(lds + Lm::G, (unsigned)T0 * tile_bytes, wave);
-    fd.issue(reinterpret_cast<bf16*>(lds + Lm::F), (unsigned)T0 * 64u, wave, lane);
+    qd.issue(lds + FBL_Q, (unsigned)T0 * tile_bytes, wave);
+    gd.issue(lds + FBL_G, (unsigned)T0 * tile_bytes, wave);
+    fd.issue(reinterpret_cast<bf16*>(lds + FBL_F), (unsigned)T0 * 64u, wave, lane);
   }
   const int key = kb * FB_K + wave * 32 + (lane & 31);
   const bool key_ok = key < N;
@@ -987,20 +977,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
   f32x16 dk[2], dv[2];
   dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
   // the running dQ sums of this (b, h): [nt][4 sub-tiles][16 regs / 4][64 lanes][4] f32, and their flags
+  // [nt][4]: flag (T, s) = number of key blocks whose partial of sub-tile s of tile T is in the sum
   const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(chain + (int64_t)bh * nt * (FB_TILE / 4)), 0, nt * FB_TILE, 0x00020000);
-  unsigned* const fl = flags + (int64_t)bh * nt;
+  unsigned* const fl = flags + (int64_t)bh * nt * 4;
   const int last = nkb - 1;
-  // this wave's dQ^T sub-tile and key half (NW = 4: every wave a whole sub-tile over all 128 keys)
-  const int dh = wave & 1, qh = (wave >> 1) & 1, kh = NW == 8 ? wave >> 2 : 0;
-  if (wave == 0) {
-    const int T0 = fb_tile(0, kb, nt), p0 = fb_pos(kb, T0, nkb, nt);
-    if (p0 > 0) fb_wait(fl + T0, (unsigned)p0, err);
-  }
+  const int dh = wave & 1, qh = (wave >> 1) & 1, kh = wave >> 2;  // this wave's dQ^T sub-tile and key half
+  const int sub = wave & 3;
+  // (pos 0 at step 0 for every block: its first tile never waits)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int prev_T = -1, prev_pos = 0;  // the tile whose running sum this block stored last step (to publish)
-  bool prev_final = false;
+  int prev_T = -1;
+  bool prev_pub = false;  // this wave stored tile prev_T's running sum last step (kh == 0): publish it
+  unsigned prev_val = 0;
   for (int j = 0; j < nt; ++j) {
     const int T = fb_tile(j, kb, nt), pos = fb_pos(kb, T, nkb, nt);
     const int P = j & 1;
@@ -1008,104 +997,100 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
     // recomputed in the step instead of hoisted to kernel entry and spilled around the loop
     int lane = lane0;
     asm volatile("" : "+v"(lane));
-    // the previous step's final dQ rows (staged in dqo behind its last barrier): whole 128-B rows
-    if (prev_final) {
-#pragma unroll
-      for (int i = 0; i < 512 / NT; ++i) {
-        const int r = (t >> 3) + i * (NT / 8), c = t & 7, q = prev_T * 64 + r;
-        const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
-        if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
-      }
-    }
     if (j + 1 < nt) {
       const int T1 = fb_tile(j + 1, kb, nt);
-      qd.issue(lds + Lm::Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
-      gd.issue(lds + Lm::G + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
-      fd.issue(reinterpret_cast<bf16*>(lds + Lm::F + (P ^ 1) * 2048), (unsigned)T1 * 64u, wave, lane);
+      qd.issue(lds + FBL_Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      gd.issue(lds + FBL_G + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
+      fd.issue(reinterpret_cast<bf16*>(lds + FBL_F + (P ^ 1) * 2048), (unsigned)T1 * 64u, wave, lane);
     }
-    const bf16* Q_ = reinterpret_cast<const bf16*>(lds + Lm::Q + P * 8192);
-    const bf16* G_ = reinterpret_cast<const bf16*>(lds + Lm::G + P * 8192);
-    const bf16* F_ = reinterpret_cast<const bf16*>(lds + Lm::F + P * 2048);
-    // the running sum of tile T so far (its predecessor's flag was matched last step), sc1 to registers,
-    // issued half way through the tile body (flies under the second half)
+    const bf16* Q_ = reinterpret_cast<const bf16*>(lds + FBL_Q + P * 8192);
+    const bf16* G_ = reinterpret_cast<const bf16*>(lds + FBL_G + P * 8192);
+    const bf16* F_ = reinterpret_cast<const bf16*>(lds + FBL_F + P * 2048);
+    bf16* const dsT = reinterpret_cast<bf16*>(lds + FBL_S + P * 32768);
+    // the running sum of this wave's sub-tile of T so far (its own poll matched at the end of the last
+    // step), sc1 to registers, issued half way through the tile body (flies under the second half)
     u32x4 run[4];
     auto load_run = [&]() __attribute__((always_inline)) {
-      if (kh == 0 && pos > 0 && !(dbg & 4)) {
+      if (kh == 0 && pos > 0) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * FB_TILE + wave * FB_SUB + g * 1024, 16);
+          run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * FB_TILE + sub * FB_SUB + g * 1024, 16);
       }
     };
     if (T == nt - 1 && nt * 64 != N)
       fb_tile_body<true>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
     else
       fb_tile_body<false>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // this wave's loads (next tile's DMA, the running sum) and last step's running-sum stores are done:
+    // publish last step's sum (the storing wave itself, behind its own vmcnt(0))
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (prev_pub && lane == 0) fb_st_flag(fl + prev_T * 4 + sub, prev_val);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();  // B1: dS^T of all 256 keys in LDS
+    __builtin_amdgcn_s_barrier();  // the one barrier of the step: dS^T of all 256 keys, next tile's operands
     __builtin_amdgcn_sched_barrier(0);
     // dQ^T (32 d x 32 q sub-tile (dh, qh)) over this wave's key half: K^T from Kt, dS^T from dsT
     f32x16 dq = zero16();
-    if (!(dbg & 2))
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const int k0 = kh * 128 + 16 * ks;
       dq = mfma(frag_tr_sw(Kt, k0, 32 * dh, lane), frag_tr_sw(dsT, k0, 32 * qh, lane), dq);
     }
-    if (NW == 8 && kh == 1) {
+    float* const red = reinterpret_cast<float*>(lds + FBL_R + sub * FB_SUB);
+    prev_pub = false;
+    if (kh == 1) {  // the other key half's partial -> LDS, then its LDS flag
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4*>(red + (wave - 4) * (FB_SUB / 4) + g * 256 + lane * 4) =
-            f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
-    }
-    if (wave == 0 && j + 1 < nt && !(dbg & 1)) {  // the next tile's predecessor (one step of slack in lockstep)
-      const int T1 = fb_tile(j + 1, kb, nt), p1 = fb_pos(kb, T1, nkb, nt);
-      if (p1 > 0) fb_wait(fl + T1, (unsigned)p1, err);
-    }
-    // every wave: the next tile's DMA, this tile's running-sum loads and the previous sum's stores are done
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();  // B2
-    __builtin_amdgcn_sched_barrier(0);
-    if (wave == 0 && lane == 0 && prev_T >= 0 && prev_pos < last) fb_st_flag(fl + prev_T, (unsigned)(prev_pos + 1));
-    const bool final = pos == last;
-    if (kh == 0) {
+        *reinterpret_cast<f32x4*>(red + g * 256 + lane * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) lflag[sub] = j + 1;
+    } else {
+      while (lflag[sub] != j + 1) __builtin_amdgcn_s_sleep(1);
+      const bool final = pos == last;
+      f32x4 v[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        f32x4 v = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
-        if constexpr (NW == 8) v = *reinterpret_cast<const f32x4*>(red + wave * (FB_SUB / 4) + g * 256 + lane * 4) + v;
-        if (pos > 0 && !(dbg & 4)) v += __builtin_bit_cast(f32x4, run[g]);
-        if (!final && !(dbg & 4)) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cr, lane * 16,
-                                                 T * FB_TILE + wave * FB_SUB + g * 1024, 16);
-        } else {  // rows d = 32 dh + 8 g + 4 h + 0..3 of query 32 qh + (lane & 31)
-          const int q = 32 * qh + (lane & 31), d0 = 32 * dh + 8 * g + 4 * (lane >> 5);
-          *reinterpret_cast<bf16x4*>(dqo + q * LROW + d0) =
-              bf16x4{(bf16)(v[0] * scale), (bf16)(v[1] * scale), (bf16)(v[2] * scale), (bf16)(v[3] * scale)};
+        v[g] = *reinterpret_cast<const f32x4*>(red + g * 256 + lane * 4) +
+               f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+        if (pos > 0) v[g] += __builtin_bit_cast(f32x4, run[g]);
+      }
+      if (!final) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[g]), cr, lane * 16,
+                                                 T * FB_TILE + sub * FB_SUB + g * 1024, 16);
+        prev_pub = true;
+        prev_val = (unsigned)(pos + 1);
+      } else {
+        // bf16 dQ of the sub-tile staged in this wave's (consumed) partial slot as [32 q][32 d] rows, then
+        // stored as 64-B row pieces: query 32 qh + (lane & 31), d = 32 dh + 8 g + 4 h + 0..3
+        char* const st = reinterpret_cast<char*>(red);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partial is in registers
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(st + (lane & 31) * FB_OP + (8 * g + 4 * (lane >> 5)) * 2) =
+              bf16x4{(bf16)(v[g][0] * scale), (bf16)(v[g][1] * scale), (bf16)(v[g][2] * scale),
+                     (bf16)(v[g][3] * scale)};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int pc = lane + 64 * i, r = pc >> 2, c = pc & 3, q = T * 64 + 32 * qh + r;
+          const uint4 x = *reinterpret_cast<const uint4*>(st + r * FB_OP + c * 16);
+          if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + 32 * dh + c * 8) = x;
         }
       }
+      // the next tile's predecessor for this sub-tile (published before its barrier of this step or earlier)
+      if (j + 1 < nt) {
+        const int T1 = fb_tile(j + 1, kb, nt), p1 = fb_pos(kb, T1, nkb, nt);
+        if (p1 > 0) fb_wait(fl + T1 * 4 + sub, (unsigned)p1, err);
+      }
     }
-    if (final) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // B3: dqo complete (stored at the top of the next step)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    prev_T = T; prev_pos = pos; prev_final = final;
+    prev_T = T;
   }
-  // the last step's running sum: drained by every storing wave, then published
+  // the last step's running sum: drained by its storing wave, then published
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave == 0 && lane == 0 && prev_pos < last) fb_st_flag(fl + prev_T, (unsigned)(prev_pos + 1));
-  if (prev_final) {
-#pragma unroll
-    for (int i = 0; i < 512 / NT; ++i) {
-      const int r = (t >> 3) + i * (NT / 8), c = t & 7, q = prev_T * 64 + r;
-      const uint4 v = *reinterpret_cast<const uint4*>(dqo + r * LROW + c * 8);
-      if (q < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + q) * ldt + hd * D + c * 8) = v;
-    }
-  }
-  // dK, dV: staged through the dS^T image as [key][d] rows, stored as whole 128-B rows
+  if (prev_pub && lane == 0) fb_st_flag(fl + prev_T * 4 + sub, prev_val);
+  // dK, dV: staged through a dS^T image as [key][d] rows, stored as whole 128-B rows
+  bf16* const stg = reinterpret_cast<bf16*>(lds + FBL_S);
 #pragma unroll
   for (int which = 0; which < 2; ++which) {
     const f32x16* acc = which == 0 ? dk : dv;
@@ -1116,15 +1101,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_fused_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d0 = 32 * h2 + 8 * g + 4 * (lane >> 5);
-        *reinterpret_cast<bf16x4*>(dsT + sw_off(32 * wave + (lane & 31), d0)) =
+        *reinterpret_cast<bf16x4*>(stg + sw_off(32 * wave + (lane & 31), d0)) =
             bf16x4{(bf16)(acc[h2][4 * g] * sc), (bf16)(acc[h2][4 * g + 1] * sc), (bf16)(acc[h2][4 * g + 2] * sc),
                    (bf16)(acc[h2][4 * g + 3] * sc)};
       }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = (NT / 8) * i + (t >> 3), c = t & 7, k = kb * FB_K + r;
-      const uint4 v = *reinterpret_cast<const uint4*>(dsT + sw_off(r, c * 8));
+      const int r = 64 * i + (t >> 3), c = t & 7, k = kb * FB_K + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + sw_off(r, c * 8));
       if (k < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + k) * ldt + (1 + which) * H * D + hd * D + c * 8) = v;
     }
   }
@@ -1300,16 +1285,15 @@ static int64_t fb_flags_offset(int32_t B, int32_t N, int32_t H) {
   const int64_t rows = (int64_t)B * N * H;
   return round256(rows * D * 2 + rows * 32);
 }
-static int64_t fb_flags_bytes(int32_t B, int32_t N, int32_t H) { return round256(((int64_t)B * H * cdiv(N, 64) + 1) * 4); }
+static int64_t fb_flags_bytes(int32_t B, int32_t N, int32_t H) {
+  return round256(((int64_t)B * H * cdiv(N, 64) * 4 + 1) * 4);  // [B*H][nt][4 sub-tiles] + error word
+}
 
-// the fused form needs every chain gap >= FB_LAG steps (so a block only ever waits for a contribution made
-// at an earlier step): nkb == 1, or nt - FB_LAG (nkb - 1) >= FB_LAG; N in (256, 384] falls back
-static int g_attn_dbg = 0;  // EXPERIMENT: 1 no waits, 2 no dQ MFMAs, 4 no running-sum traffic
-extern "C" int mia_attn_debug_mode(int32_t m) { g_attn_dbg = m; return 0; }
-constexpr int FB_K = 256;  // keys per workgroup of the production (8-wave) form
+// the fused form needs every gap between consecutive contributions to a tile to be >= 2 steps
+// (nt - FB_LAG (nkb - 1) >= 2 at the wrap; FB_LAG >= 2 elsewhere): true for every N (nt >= 4 nkb - 3)
 static bool fb_ok(int32_t N) {
   const int nt = (int)cdiv(N, 64), nkb = (int)cdiv(N, FB_K);
-  return nkb == 1 || nt - FB_LAG * (nkb - 1) >= FB_LAG;
+  return nkb == 1 || nt - FB_LAG * (nkb - 1) >= 2;
 }
 
 extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_t H) {
@@ -1321,7 +1305,7 @@ extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_
 // byte offset in the bf16 workspace of the fused backward's error word: 0 after a call = every dQ hand-off
 // matched; non-zero = a bounded wait gave up (dQ of that call is not valid)
 extern "C" int64_t mia_attn_bwd_error_offset(int32_t B, int32_t N, int32_t H) {
-  return fb_flags_offset(B, N, H) + (int64_t)B * H * cdiv(N, 64) * 4;
+  return fb_flags_offset(B, N, H) + (int64_t)B * H * cdiv(N, 64) * 16;
 }
 
 static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
@@ -1367,16 +1351,9 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
     // every flag and the error word start at 0 in each call (stream-ordered, no host sync)
     hipError_t e = hipMemsetAsync(flags, 0, (size_t)fb_flags_bytes(B, N, H), s);
     if (e != hipSuccess) return mia::fail(-(int)e, "attn_bwd: memset: %s", hipGetErrorString(e));
-    if (g_attn_dbg & 16) {  // EXPERIMENT: 4-wave form (128 keys; chain positions are NOT valid: waits off)
-      const int nkb4 = (int)cdiv(N, 128);
-      attn_bwd_fused_kernel<4><<<(unsigned)(nkb4 * B * H), 256, 0, s>>>(
-          (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
-          flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb4, scale, 1.f / LOG2E, g_attn_dbg | 1);
-    } else {
-      attn_bwd_fused_kernel<8><<<(unsigned)(nkb * B * H), 512, 0, s>>>(
-          (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
-          flags + (int64_t)B * H * cdiv(N, 64), N, H, nkb, scale, 1.f / LOG2E, g_attn_dbg);
-    }
+    attn_bwd_fused_kernel<<<(unsigned)(nkb * B * H), 512, 0, s>>>(
+        (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, chain, flags,
+        flags + (int64_t)B * H * cdiv(N, 64) * 4, N, H, nkb, scale, 1.f / LOG2E);
     MIA_LAUNCH_CHECK("attn_bwd_fused");
     return 0;
   }
