@@ -883,10 +883,12 @@ struct TileDMA8 {
 
 // S', dP' of 32 queries x this wave's 32 keys -> dS; dV^T, dK^T MFMAs; dS^T (bf16) into the LDS image.
 // K row fragments from the block's LDS image Kt, V fragments in registers; `mid` runs between the halves.
-template <bool TAIL, class Mid>
+// qn = valid queries in the tile (>= 64: all); masking p by (query valid and key valid) is one select per
+// element with a per-lane bound, cheaper than a second copy of the body
+template <class Mid>
 __device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
                                              const bf16* F_, const bf16* Kt, bf16* dsT, const bf16x8 (&vf)[4],
-                                             bf16x8 one, bool key_ok, int q0, int N, int wave, int lane, Mid&& mid) {
+                                             bf16x8 one, bool key_ok, int qn, int wave, int lane, Mid&& mid) {
   const int krow = 32 * wave + (lane & 31);
 #pragma unroll
   for (int sq = 0; sq < 2; ++sq) {
@@ -901,13 +903,13 @@ __device__ __forceinline__ void fb_tile_body(f32x16 (&dk)[2], f32x16 (&dv)[2], c
     }
     sc = mfma(row_frag(F_ + qr * 8), one, sc);
     dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
+    // rows of this lane: sq * 32 + acc_row(r) = sq * 32 + 4h + (r & 3) + 8 (r >> 2); valid iff < qn, and
+    // only if this lane's key is valid: one per-lane bound, lim = key_ok ? qn - sq * 32 - 4h : 0
+    const int lim = key_ok ? qn - sq * 32 - 4 * (lane >> 5) : 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       float p = __builtin_amdgcn_exp2f(sc[r]);
-      if constexpr (TAIL) {
-        if (q0 + sq * 32 + acc_row(r, lane) >= N) p = 0.f;
-      }
-      p = key_ok ? p : 0.f;  // keys past the sequence end: no contribution to dQ
+      p = ((r & 3) + 8 * (r >> 2)) < lim ? p : 0.f;
       sc[r] = p;
       dp[r] *= p;
     }
@@ -990,13 +992,11 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
   int prev_T = -1;
   bool prev_pub = false;  // this wave stored tile prev_T's running sum last step (kh == 0): publish it
   unsigned prev_val = 0;
-  for (int j = 0; j < nt; ++j) {
+  // one step; the buffer parity P is a compile-time constant (the loop is unrolled by 2), so every LDS
+  // operand address is a per-lane offset + an immediate
+  auto step = [&](int j, auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
     const int T = fb_tile(j, kb, nt), pos = fb_pos(kb, T, nkb, nt);
-    const int P = j & 1;
-    // the lane index made opaque per step: every lane-derived LDS address (swizzled, ~40 distinct ones) is
-    // recomputed in the step instead of hoisted to kernel entry and spilled around the loop
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
     if (j + 1 < nt) {
       const int T1 = fb_tile(j + 1, kb, nt);
       qd.issue(lds + FBL_Q + (P ^ 1) * 8192, (unsigned)T1 * tile_bytes, wave);
@@ -1017,10 +1017,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
           run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * FB_TILE + sub * FB_SUB + g * 1024, 16);
       }
     };
-    if (T == nt - 1 && nt * 64 != N)
-      fb_tile_body<true>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
-    else
-      fb_tile_body<false>(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, T * 64, N, wave, lane, load_run);
+    fb_tile_body(dk, dv, Q_, G_, F_, Kt, dsT, vf, one, key_ok, N - T * 64, wave, lane, load_run);
     // this wave's loads (next tile's DMA, the running sum) and last step's running-sum stores are done:
     // publish last step's sum (the storing wave itself, behind its own vmcnt(0))
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1085,6 +1082,16 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
       }
     }
     prev_T = T;
+  };
+  {
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    int j = 0;
+    for (; j + 1 < nt; j += 2) {
+      step(j, P0{});
+      step(j + 1, P1{});
+    }
+    if (j < nt) step(j, P0{});
   }
   // the last step's running sum: drained by its storing wave, then published
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
