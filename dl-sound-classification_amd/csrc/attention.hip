@@ -1377,15 +1377,25 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
 extern "C" int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                             void* work, int32_t dtype, int32_t B, int32_t N, int32_t H, float scale,
                             mia_stream_t stream) {
-  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, dtype, B, N, H, scale, 0, 1, stream);
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, dtype, B, N, H, scale, 0, 0, stream);
 }
 
 // the bf16 backward in its two-kernel form (key-parallel dK/dV + query-parallel dQ, each recomputing S and
-// dP): the fused form's yardstick; q_ready = the forward wrote Q' into `work` (mia_attn_fwd_save_q)
+// dP; what mia_attn_bwd / mia_attn_bwd_saved_q run); q_ready = the forward wrote Q' into `work`
+// (mia_attn_fwd_save_q)
 extern "C" int mia_attn_bwd_two_pass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                                      void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
                                      mia_stream_t stream) {
   return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, q_ready, 0, stream);
+}
+
+// the bf16 backward in its fused one-pass form (S, dP, dS once per tile; dQ by the ordered hand-off):
+// five MFMA products per tile instead of seven, but at B = 256, N = 1645 it measured 8.5-8.6 ms per layer
+// against 8.2 ms for the two-kernel form, so it is not the default
+extern "C" int mia_attn_bwd_fused(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                                  void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
+                                  mia_stream_t stream) {
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, q_ready, 1, stream);
 }
 
 // bf16 forward that also writes Q' (the backward's scaled query operand) into the backward workspace
@@ -1412,5 +1422,5 @@ extern "C" int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void*
 // the bf16 backward when the forward already wrote Q' into `work` (mia_attn_fwd_save_q)
 extern "C" int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                                     void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream) {
-  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, 1, stream);
+  return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, 0, stream);
 }

@@ -119,6 +119,7 @@ SIGNATURES = {
     "mia_attn_fwd_save_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_saved_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_two_pass": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),
+    "mia_attn_bwd_fused": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),
     "mia_attn_bwd_error_offset": (C.c_int64, [i32, i32, i32]),
     "mia_tokens_fwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_tokens_bwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),

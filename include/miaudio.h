@@ -458,10 +458,9 @@ int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
  * lse: f32 (B, H, N) saved for backward. */
 int mia_attn_fwd(const void* qkv, void* out, float* lse, int32_t dtype, int32_t B, int32_t N,
                  int32_t H, float scale, mia_stream_t stream);
-/* Deterministic backward, no float atomics.  bf16: ONE fused pass per (b, h, 256-key block) computing
- * S, dP, dS once and dV, dK in registers and dQ as an ordered hand-off of running f32 sums between the
- * key blocks of one (b, h) (fixed order: bit-reproducible); sequence lengths in (256, 384] use the
- * two-kernel form (key-parallel dK/dV + query-parallel dQ).  f32: exact reference-precision kernels.
+/* Deterministic backward, no float atomics.  bf16: a key-parallel dK/dV kernel + a query-parallel dQ
+ * kernel (each recomputes S and dP; mia_attn_bwd_fused below is the one-pass alternative).
+ * f32: exact reference-precision kernels.
  * dout: (B, N, H, 64) bf16; dqkv: (B, N, 3, H, 64) bf16 (fully written);
  * work: 16-B aligned workspace of mia_attn_bwd_workspace_bytes() bytes (bf16: the scaled Q operand,
  * per-query row-constant fragments, hand-off flags and running sums; f32: rowsum(dO * O)). */
@@ -477,11 +476,16 @@ int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void* q8, void* 
                         int32_t N, int32_t H, float scale, mia_stream_t stream);
 int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                          void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream);
-/* The bf16 backward in its two-kernel form (the fused form's yardstick); q_ready: `work` already holds
- * Q' (mia_attn_fwd_save_q). */
+/* The bf16 backward in its two-kernel form (what mia_attn_bwd / mia_attn_bwd_saved_q run), and in a
+ * fused one-pass form: per (b, h, 256-key block) S, dP, dS are computed once, dV / dK accumulate in
+ * registers and dQ is summed over the key blocks by an ordered hand-off of running f32 sums in `work`
+ * (fixed order: bit-reproducible).  q_ready: `work` already holds Q' (mia_attn_fwd_save_q). */
 int mia_attn_bwd_two_pass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                           void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
                           mia_stream_t stream);
+int mia_attn_bwd_fused(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                       void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
+                       mia_stream_t stream);
 /* Byte offset in the bf16 workspace of a u32 error word: 0 after a fused backward = every dQ hand-off
  * matched; non-zero = a bounded wait gave up and that call's dQ is not valid. */
 int64_t mia_attn_bwd_error_offset(int32_t B, int32_t N, int32_t H);

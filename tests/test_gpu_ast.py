@@ -317,8 +317,8 @@ def test_attention_bwd_fused_vs_two_pass(cuda, B, N, H):
             L.check(lib.mia_attn_bwd_two_pass(tq.data_ptr(), out.data_ptr(), td.data_ptr(), lse.data_ptr(),
                                               dq.data_ptr(), work.data_ptr(), B, N, H, 0.125, 1, s), "two")
         else:
-            L.check(lib.mia_attn_bwd_saved_q(tq.data_ptr(), out.data_ptr(), td.data_ptr(), lse.data_ptr(),
-                                             dq.data_ptr(), work.data_ptr(), B, N, H, 0.125, s), "fused")
+            L.check(lib.mia_attn_bwd_fused(tq.data_ptr(), out.data_ptr(), td.data_ptr(), lse.data_ptr(),
+                                           dq.data_ptr(), work.data_ptr(), B, N, H, 0.125, 1, s), "fused")
             torch.cuda.synchronize()
             assert _err_word(lib, work, B, N, H) == 0
         torch.cuda.synchronize()

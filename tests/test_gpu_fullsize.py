@@ -150,6 +150,16 @@ def test_attention_benched_grid_b256_h12(cuda):
                                      work.data_ptr(), B, N, H, 0.125, s), "bwd_saved_q")
     torch.cuda.synchronize()
     assert torch.isfinite(dq.float()).all() and torch.isfinite(out.float()).all()
+    # the fused one-pass form over the same grid (7 key blocks per (b, h) handing dQ on): error word 0 and
+    # the two-kernel result up to summation order
+    dq2 = torch.full_like(qkv, float("nan"))
+    L.check(lib.mia_attn_bwd_fused(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), dq2.data_ptr(),
+                                   work.data_ptr(), B, N, H, 0.125, 1, s), "bwd_fused")
+    torch.cuda.synchronize()
+    off = int(lib.mia_attn_bwd_error_offset(B, N, H))
+    assert int(work[off:off + 4].view(torch.int32).item()) == 0
+    e = float((dq2.float() - dq.float()).abs().max() / dq.float().abs().max())
+    assert e < 5e-3, e
     qkv4 = qkv.view(B, N, 3, H, 64)
     for b, h in [(0, 0), (1, 11), (97, 5), (128, 0), (200, 7), (255, 11)]:
         q, k, v = (qkv4[b, :, i, h].double().requires_grad_(True) for i in range(3))

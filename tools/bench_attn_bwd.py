@@ -1,5 +1,5 @@
 """Time the bf16 attention backward on the AST shape (N 1645, H 12, d 64): the fused one-pass form
-(mia_attn_bwd_saved_q) against the two-kernel form (mia_attn_bwd_two_pass), interleaved rounds in one
+(mia_attn_bwd_fused) against the two-kernel form (mia_attn_bwd_two_pass), interleaved rounds in one
 process, HIP events on the launch stream; the fused form's error word checked, results compared.
     BATCH=256 python tools/bench_attn_bwd.py"""
 import os
@@ -29,8 +29,8 @@ dq = {k: torch.empty_like(qkv) for k in ("fused", "two")}
 
 def run(name):
     if name == "fused":
-        L.check(lib.mia_attn_bwd_saved_q(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
-                                         dq[name].data_ptr(), work.data_ptr(), B, N, H, D ** -0.5, s), name)
+        L.check(lib.mia_attn_bwd_fused(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+                                       dq[name].data_ptr(), work.data_ptr(), B, N, H, D ** -0.5, 1, s), name)
     else:
         L.check(lib.mia_attn_bwd_two_pass(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
                                           dq[name].data_ptr(), work.data_ptr(), B, N, H, D ** -0.5, 1, s), name)
@@ -46,22 +46,6 @@ print("fused error word", int(work[off:off + 4].view(torch.int32).item()), flush
 d = (dq["fused"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
 print(f"fused vs two-pass: max |d| / max {float(d):.3g}", flush=True)
 flop = 8.0 * B * H * N * N * D  # 2x the forward, recompute not credited
-MODES = [int(v) for v in os.environ.get("MODES", "").split(",") if v]
-if MODES:
-    import ctypes
-    lib.mia_attn_debug_mode.argtypes = [ctypes.c_int32]
-    for r in range(2):
-        for m in MODES:
-            lib.mia_attn_debug_mode(m)
-            run("fused")
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(ITERS):
-                run("fused")
-            e1.record()
-            torch.cuda.synchronize()
-            print(f"mode {m}: {e0.elapsed_time(e1) / ITERS:7.3f} ms", flush=True)
-    lib.mia_attn_debug_mode(0)
 for r in range(ROUNDS):
     for name in ("two", "fused"):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
