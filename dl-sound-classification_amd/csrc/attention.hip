@@ -175,6 +175,22 @@ __device__ __forceinline__ int xcd_work_item(int L, int total) {
   return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
 }
 
+// Tiles s0 .. ntiles - 1 of a 3-slot ring with no remainder code: the last round's second and third
+// tiles are guarded inside the loop (wave-uniform branches), so every tile is the loop's own code and
+// register allocation (straight-line remainder copies spilled)
+template <int S0, class Body>
+__device__ __forceinline__ void ring3_guarded(int s0, int ntiles, Body&& body) {
+  using F = std::false_type;
+  using C0 = std::integral_constant<int, S0 % 3>;
+  using C1 = std::integral_constant<int, (S0 + 1) % 3>;
+  using C2 = std::integral_constant<int, (S0 + 2) % 3>;
+  for (int j = s0; j < ntiles; j += 3) {
+    body(F{}, C0{}, j);
+    if (j + 1 < ntiles) body(F{}, C1{}, j + 1);
+    if (j + 2 < ntiles) body(F{}, C2{}, j + 2);
+  }
+}
+
 // Tiles s0 .. ntiles - 1 of a 3-slot LDS ring (K/V or Q/dO tiles arrive by LDS-DMA two tiles ahead of
 // their use), slot = tile % 3 as a compile-time constant (tile s0's slot is S0 % 3, so every LDS address
 // is base + immediate); the last tile is the TAIL form when `tail`.  body(tail_t, slot_t, j).
@@ -290,13 +306,17 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&s)[2], float d, bf16x8 (&
   }
 }
 
-template <bool FIRST, bool TAIL>
-__device__ __forceinline__ void fwd_softmax(f32x16 (&s)[2], FwdAcc& a, bf16x8 (&pf)[4], int k0, int N, int lane) {
-  if constexpr (TAIL) {
+// kvalid = keys of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask, so the ring's
+// last tiles are the loop's own code (per-tile TAIL copies spilled ~260 VGPRs in the remainder code)
+template <bool FIRST>
+__device__ __forceinline__ void fwd_softmax(f32x16 (&s)[2], FwdAcc& a, bf16x8 (&pf)[4], int kvalid, int lane) {
+  if (kvalid < 64) {
+    const int lim = kvalid - 4 * (lane >> 5);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if (k0 + acc_row(r, lane) >= N) s[0][r] = -INFINITY;
-      if (k0 + 32 + acc_row(r, lane) >= N) s[1][r] = -INFINITY;
+      const int row = (r & 3) + 8 * (r >> 2);
+      if (row >= lim) s[0][r] = -INFINITY;
+      if (row + 32 >= lim) s[1][r] = -INFINITY;
     }
   }
   float la, lb;
@@ -383,7 +403,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
   f32x16 s[2];
   bf16x8 pf[4];
   // one tile in slot P of the 3-slot ring: tile j + 2's DMA flies under this tile's work and tile j + 1's
-  auto tile = [&](auto first, auto tail, auto slot, int j) __attribute__((always_inline)) {
+  auto tile = [&](auto first, auto, auto slot, int j) __attribute__((always_inline)) {
     constexpr int P = decltype(slot)::value;
     constexpr int PN = (P + 2) % 3;
     const bool ahead = j + 2 < ntiles;
@@ -393,7 +413,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     }
     fwd_qk(s, Ks[P], qf, one, a.mrow, lane);
     __builtin_amdgcn_s_setprio(1);  // the softmax's VALU issues ahead of the co-resident waves' MFMA streams
-    fwd_softmax<decltype(first)::value, decltype(tail)::value>(s, a, pf, j * 64, N, lane);
+    fwd_softmax<decltype(first)::value>(s, a, pf, N - j * 64, lane);
     __builtin_amdgcn_s_setprio(0);
     fwd_pv(a, Vs[P], pf, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j + 1's pieces have landed
@@ -406,14 +426,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
   if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 and the Q fragments
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const bool tail = (ntiles * 64 != N);
-  if (ntiles == 1) {
-    if (tail) tile(T{}, T{}, P0{}, 0);
-    else tile(T{}, F{}, P0{}, 0);
-  } else {
-    tile(T{}, F{}, P0{}, 0);
-    ring3<1>(1, ntiles, tail, [&](auto tl, auto sl, int j) __attribute__((always_inline)) { tile(F{}, tl, sl, j); });
-  }
+  tile(T{}, F{}, P0{}, 0);
+  ring3_guarded<1>(1, ntiles, [&](auto tl, auto sl, int j) __attribute__((always_inline)) { tile(F{}, tl, sl, j); });
   const float lt = half_exchange_sum(a.l);
   const float inv = 1.f / lt;
   if constexpr (MX) {
@@ -550,10 +564,10 @@ __device__ __forceinline__ bf16x8 row_frag(const bf16* row) { return *reinterpre
 // registers over the whole sequence: no atomics, deterministic.
 constexpr int BWD_K = 128;
 
-template <bool TAIL>
+// qvalid = queries of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask in one body
 __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
                                           const bf16* F_, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one,
-                                          int q0, int N, int lane) {
+                                          int qvalid, int lane) {
 #pragma unroll
   for (int sq = 0; sq < 2; ++sq) {
     const int qr = sq * 32 + (lane & 31);
@@ -567,14 +581,14 @@ __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], cons
     sc = mfma(row_frag(F_ + qr * 8), one, sc);
     dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p = __builtin_amdgcn_exp2f(sc[r]);
-      if constexpr (TAIL) {
-        if (q0 + sq * 32 + acc_row(r, lane) >= N) p = 0.f;
-      }
-      sc[r] = p;
-      dp[r] *= p;
+    for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r]);
+    if (qvalid < 64) {  // the sequence's last, partial query tile: rows past it contribute nothing
+      const int lim = qvalid - sq * 32 - 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = ((r & 3) + 8 * (r >> 2)) < lim ? sc[r] : 0.f;
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] *= sc[r];
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
       const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
@@ -627,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
       gd.issue(Gs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
       fd.issue(Fs[P ^ 1], (unsigned)(j + 1) * 64u, wave, lane);
     }
-    dkdv_tile<decltype(tail)::value>(dk, dv, Qs[P], Gs[P], Fs[P], kf, vf, one, j * 64, N, lane);
+    dkdv_tile(dk, dv, Qs[P], Gs[P], Fs[P], kf, vf, one, N - j * 64, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -637,19 +651,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   using P1 = std::integral_constant<int, 1>;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const bool tail = (ntiles * 64 != N);
-  int j = 0;
-  for (; j + 2 < ntiles; j += 2) {
+  for (int j = 0; j < ntiles; j += 2) {  // no remainder code (see ring3_guarded)
     tile(F{}, P0{}, j);
-    tile(F{}, P1{}, j + 1);
-  }
-  if (j + 1 < ntiles) {  // tiles j (even) and j + 1 = last
-    tile(F{}, P0{}, j);
-    if (tail) tile(T{}, P1{}, j + 1);
-    else tile(F{}, P1{}, j + 1);
-  } else {  // tile j (even) is the last
-    if (tail) tile(T{}, P0{}, j);
-    else tile(F{}, P0{}, j);
+    if (j + 1 < ntiles) tile(F{}, P1{}, j + 1);
   }
   if (key >= N) return;
   bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
@@ -678,9 +682,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 // straight from the accumulators.
 constexpr int BWD_Q = 128;
 
-template <bool TAIL>
+// kvalid = keys of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask in one body, so
+// the ring's remainder tiles are the same code as its loop (per-tile TAIL copies spilled 76 VGPRs there)
 __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const bf16* V_, const bf16x8 (&qf)[4],
-                                        const bf16x8 (&gf)[4], bf16x8 one, bf16x8 lf, bf16x8 df_, int k0, int N,
+                                        const bf16x8 (&gf)[4], bf16x8 one, bf16x8 lf, bf16x8 df_, int kvalid,
                                         int lane) {
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh) {
@@ -695,13 +700,14 @@ __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const 
     sc = mfma(one, lf, sc);
     dp = mfma(one, df_, dp);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p = __builtin_amdgcn_exp2f(sc[r]);
-      if constexpr (TAIL) {
-        if (k0 + 32 * kh + acc_row(r, lane) >= N) p = 0.f;
-      }
-      dp[r] *= p;
+    for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r]);
+    if (kvalid < 64) {
+      const int lim = kvalid - 32 * kh - 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = ((r & 3) + 8 * (r >> 2)) < lim ? sc[r] : 0.f;
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] *= sc[r];
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
       const bf16x8 dsf = acc_frag(dp, sk);
@@ -766,7 +772,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
       kd.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
       vd.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
     }
-    dq_tile<decltype(tail)::value>(acc, Ks[P], Vs[P], qf, gf, one, lf, dlf, j * 64, N, lane);
+    dq_tile(acc, Ks[P], Vs[P], qf, gf, one, lf, dlf, N - j * 64, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -774,7 +780,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 and the Q / dO fragments
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  ring3<0>(0, ntiles, ntiles * 64 != N, tile);
+  ring3_guarded<0>(0, ntiles, tile);
   if (!qv) return;
   bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
 #pragma unroll
