@@ -125,6 +125,16 @@ __device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* lds, int k0, int c0, in
   return __builtin_bit_cast(bf16x8, c);
 }
 
+// Make the compiler wait for global loads of loop-invariant fragments HERE (before the tile loop): otherwise
+// it re-checks them with a vmcnt at the loop head of every iteration, and vmcnt also counts the loop's
+// own in-flight tile DMAs (lds_dma16), so every tile would wait for its successor's load.
+template <int n>
+__device__ __forceinline__ void settle(const bf16x8 (&f)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) asm volatile("" ::"v"(f[i]));
+}
+__device__ __forceinline__ void settle1(const bf16x8& f) { asm volatile("" ::"v"(f)); }
+
 // accumulator registers 8s..8s+7 -> bf16 operand fragment
 __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   bf16x8 f;
@@ -241,6 +251,21 @@ constexpr float FWD_SUM_LIMIT = 65536.f;
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
 
+// 16 B per lane from a buffer into LDS (buffer_load_dwordx4 ... lds, M0 = the wave's LDS destination) as
+// inline asm: issued through the builtin, the compiler treats the in-flight DMA as a possible writer of
+// every LDS location and puts vmcnt(0) in front of the next ds_read -- in these kernels the NEXT tile's
+// DMA, so every tile waited for its successor's load.  Here the kernels' own counted vmcnt + barrier
+// order the DMA against its readers (each issue site says which), and M0 is saved and restored.
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, const void* lds, unsigned voff, unsigned soff) {
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_vp)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(a), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
+}
+
 // x rounded toward +inf to a bf16-representable float (its negation is exact in bf16)
 __device__ __forceinline__ float bf16_ceil(float x) {
   unsigned u = __builtin_bit_cast(unsigned, x);
@@ -267,9 +292,7 @@ struct TileDMA {
   }
   __device__ __forceinline__ void issue(bf16* tile, unsigned row0_bytes, int wave) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + (2 * wave + i) * 512), 16, voff[i], row0_bytes,
-                                               0, 0);
+    for (int i = 0; i < 2; ++i) lds_dma16(rsrc, tile + (2 * wave + i) * 512, voff[i], row0_bytes);
   }
 };
 
@@ -382,6 +405,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
   }
+  settle(qf);
   if (qs_out != nullptr && q < N) {  // Q' for the backward (its prep then skips it): row (b, q, h), d = 16 ks + 8 (lane >> 5)..
     bf16* qrow = qs_out + (((int64_t)b * N + q) * H + hd) * D + 8 * (lane >> 5);
 #pragma unroll
@@ -547,9 +571,7 @@ struct FragDMA {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(2 * part_bytes), 0x00020000);
   }
   __device__ __forceinline__ void issue(bf16* tile, unsigned row0, int wave, int lane) const {
-    if (wave < 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 512), 16,
-                                               (unsigned)wave * part_bytes + lane * 16, row0 * 16, 0, 0);
+    if (wave < 2) lds_dma16(rsrc, tile + wave * 512, (unsigned)wave * part_bytes + lane * 16, row0 * 16);
   }
 };
 
@@ -568,18 +590,33 @@ constexpr int BWD_K = 128;
 __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
                                           const bf16* F_, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one,
                                           int qvalid, int lane) {
+  // the row fragments of query half sq (Q', dO, the two fifth-k-step rows), loaded one half ahead: half 1's
+  // fly under half 0's softmax and dV / dK products instead of one LDS latency in front of every MFMA
+  bf16x8 fr[2][10];
+  auto load = [&](int sq, bf16x8 (&f)[10]) __attribute__((always_inline)) {
+    const int qr = sq * 32 + (lane & 31);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f[ks] = frag_row_sw(Q_, qr, ks, lane);
+      f[4 + ks] = frag_row_sw(G_, qr, ks, lane);
+    }
+    f[8] = row_frag(F_ + qr * 8);
+    f[9] = row_frag(F_ + 512 + qr * 8);
+  };
+  load(0, fr[0]);
 #pragma unroll
   for (int sq = 0; sq < 2; ++sq) {
-    const int qr = sq * 32 + (lane & 31);
-    f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), kf[0], zero16());
-    f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
+    const bf16x8 (&f)[10] = fr[sq];
+    f32x16 sc = mfma(f[0], kf[0], zero16());
+    f32x16 dp = mfma(f[4], vf[0], zero16());
 #pragma unroll
     for (int ks = 1; ks < 4; ++ks) {
-      sc = mfma(frag_row_sw(Q_, qr, ks, lane), kf[ks], sc);
-      dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
+      sc = mfma(f[ks], kf[ks], sc);
+      dp = mfma(f[4 + ks], vf[ks], dp);
     }
-    sc = mfma(row_frag(F_ + qr * 8), one, sc);
-    dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
+    sc = mfma(f[8], one, sc);
+    dp = mfma(f[9], one, dp);
+    if (sq == 0) load(1, fr[1]);
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r]);
     if (qvalid < 64) {  // the sequence's last, partial query tile: rows past it contribute nothing
@@ -631,6 +668,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
     kf[ks] = load_frag_global(base + (int64_t)key * ldt + H * D, ks, lane, key < N);
     vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
   }
+  settle(kf);
+  settle(vf);
   const bf16x8 one = ones3(lane);
   f32x16 dk[2], dv[2];
   dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
@@ -756,6 +795,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
       for (int j = 0; j < 8; ++j) { lf[j] = (bf16)0.f; dlf[j] = (bf16)0.f; }
     }
   }
+  settle(qf);
+  settle(gf);
+  settle1(lf);
+  settle1(dlf);
   if (ntiles > 1) {
     kd.issue(Ks[1], tile_bytes, wave);
     vd.issue(Vs[1], tile_bytes, wave);
@@ -883,7 +926,7 @@ struct TileDMA8 {
     voff = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
   }
   __device__ __forceinline__ void issue(char* tile, unsigned row0_bytes, int wave) const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_vp)(tile + wave * 1024), 16, voff, row0_bytes, 0, 0);
+    lds_dma16(rsrc, tile + wave * 1024, voff, row0_bytes);
   }
 };
 
@@ -960,8 +1003,8 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
     for (int i = 0; i < 4; ++i) {
       const int rl = 32 * wave + 8 * i + (lane >> 3);  // local key row
       const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_vp)(lds + FBL_K + (4 * wave + i) * 1024), 16, vo,
-                                               (unsigned)((int64_t)(kb * FB_K + 32 * wave + 8 * i) * ldt * 2), 0, 0);
+      lds_dma16(kr, lds + FBL_K + (4 * wave + i) * 1024, vo,
+                (unsigned)((int64_t)(kb * FB_K + 32 * wave + 8 * i) * ldt * 2));
     }
   }
   if (t < 4) lflag[t] = 0;
@@ -981,6 +1024,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
   bf16x8 vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key_ok);
+  settle(vf);
   const bf16x8 one = ones3(lane);
   f32x16 dk[2], dv[2];
   dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
