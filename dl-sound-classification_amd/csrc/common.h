@@ -21,6 +21,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 namespace mia {
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);
+int cu_count();  // compute units of the current device (cached; 256 on MI355X)
 }  // namespace mia
 
 #define MIA_CHECK_ARG(cond, ...)                       \

@@ -20,6 +20,17 @@ int fail(int code, const char* fmt, ...) {
   va_end(ap);
   return code < 0 ? code : -1;
 }
+int cu_count() {
+  static int ncu = 0;  // every device of the node is the same part
+  if (!ncu) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      ncu = n;
+    else
+      ncu = 256;
+  }
+  return ncu;
+}
 }  // namespace mia
 
 extern "C" const char* mia_last_error_string(void) { return g_err; }

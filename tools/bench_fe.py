@@ -25,16 +25,32 @@ bias = torch.randn(64, generator=g, device=dev)
 y2 = torch.empty(B * W2, 64, dtype=torch.bfloat16, device=dev)
 da1 = torch.empty(B * W1, 32, dtype=torch.bfloat16, device=dev)
 dw = torch.empty(64, 512, device=dev)
+T = 220500
+x = torch.randn(B, T, generator=g, device=dev) * 0.1
+w1 = (torch.randn(32, 64, generator=g, device=dev) * 0.1).to(torch.bfloat16)
+b1 = torch.randn(32, generator=g, device=dev) * 0.1
+y1c = torch.empty(B * W1, 32, dtype=torch.bfloat16, device=dev)
 runs = {
+    "fe_conv1_fwd": lambda: K.fe_conv1_fwd(x, w1, b1, y1c, B, T, stats=True),
     "fe_conv2_fwd": lambda: K.fe_conv2_fwd(y1, sc, sh, w0, bias, y2, B, W1, W2),
     "fe_conv2_dgrad": lambda: K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2),
     "fe_conv2_wgrad": lambda: K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2),
     "dgrad+wgrad": lambda: (K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2), K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2)),
 }
-byts = {"fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2,
+byts = {"fe_conv1_fwd": x.numel() * 4 + y1c.numel() * 2, "fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2,
         "fe_conv2_wgrad": (dy2.numel() + y1.numel()) * 2, "dgrad+wgrad": (2 * dy2.numel() + y1.numel() + da1.numel()) * 2}
 flop = 2.0 * B * W2 * 64 * 512
+want = set(sys.argv[1:])
+
+
+def digest(t):
+    v = t.reshape(-1).view(torch.int32).to(torch.int64)
+    return int((v * torch.arange(1, v.numel() + 1, device=v.device, dtype=torch.int64).remainder(65521)).sum()) & (2**64 - 1)
+
+
 for name, fn in runs.items():
+    if want and name not in want:
+        continue
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -45,4 +61,6 @@ for name, fn in runs.items():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s", flush=True)
+    out = {"fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name)
+    dg = f"digest {digest(out):x}" if out is not None else ""
+    print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s  {dg}", flush=True)
