@@ -3,62 +3,79 @@
 // Per frame f (hop 160): the 400 windowed samples x[f*160-200+u]*hann[u] (reflect padding at the
 // clip edges, = torch.stft center=True with the 400-tap window centred in n_fft=1024) are packed as
 // 200 complex points z[n] = x[2n] + i x[2n+1], transformed by a 512-point Stockham radix-8 FFT in
-// LDS (one wave per frame, 3 passes in one in-place buffer per wave; window taps and twiddles held in
-// registers), split into the 513 real-FFT bins, squared, reduced into the 128 htk mel bands (sparse
-// band table staged in LDS: start/len/offset/weights), and converted to dB (f32 log10).
-// A block owns 16 consecutive frames of one clip: the 2,800-sample input segment is read from HBM
-// once with coalesced loads into LDS, and the 128 x 16 dB tile is written back as 128 rows of
-// 16 contiguous frames.  Per-clip top_db clamp + mean / unbiased-std normalisation need the clip
-// max first, so two light passes follow (stats over the dB tensor, which stays in the 256 MB
-// Infinity Cache at batch 256, then an in-place normalise).
+// LDS (one wave per frame, 3 passes in one in-place buffer per wave), split into the 513 real-FFT
+// bins, squared, reduced into the 128 htk mel bands (sparse band table staged in LDS:
+// start/len/offset/weights), and converted to dB (10 log10 = 10 log10(2) * v_log_f32).
+// Complex values are float2 vectors: every complex add is one v_pk_add_f32, every twiddle
+// multiply one v_pk_mul_f32 + one v_pk_fma_f32 (op_sel swizzles, no moves); the Stockham buffer is
+// XOR-swizzled (first-pass writes 1-2-way instead of 8-way bank conflicts).
+// Persistent 4-wave workgroups (three per CU: 46 KB LDS, <= 168 VGPRs) walk (clip, 16-frame chunk)
+// items: the 2,800-sample input segment of the NEXT chunk is loaded into registers (coalesced,
+// reflect-padded) while this chunk's 16 frames are computed (4 per wave), then committed to LDS
+// behind the chunk's tile store; the mel table, window taps and the twiddles of the three passes are
+// read once per workgroup (the real-split twiddles derived per frame from one per lane).  Each mel
+// band is widened in LDS to whole 16-B aligned groups of 4 bins with zero weights, so the band loop
+// reads 4 bins and 4 weights with one ds_read_b128 each.  The 128 x 16 dB tile is written back as
+// 128 rows of 16 contiguous frames.  Measured at B = 256 (tools/bench_logmel.py, tools/logmel_pmc.sh):
+// 0.75 -> 0.66 ms for the three passes; ~400 VALU and ~110 LDS instructions per frame, the band loop
+// ~36 % of the kernel and most of its LDS bank conflicts (lanes = bands read data-dependent bins).
+// Per-clip top_db clamp + mean / unbiased-std normalisation need the clip max first, so two light
+// passes follow (stats over the dB tensor, which stays in the 256 MB Infinity Cache at batch 256,
+// then an in-place normalise).
 #include "common.h"
 
 namespace {
 
-constexpr int FB = 16;          // frames per block (3 blocks per CU by LDS)
+constexpr int FB = 16;          // frames per chunk (LW waves x 4)
+constexpr int LW = 4;           // waves per workgroup
+constexpr int LNT = 64 * LW;
 constexpr int NFFT = 1024;
 constexpr int NC = 512;         // complex FFT size
 constexpr int HOP = 160;
 constexpr int WIN = 400;
 constexpr int NMEL_MAX = 128;
-constexpr int SEG = (FB - 1) * HOP + WIN;  // 2800 samples
+constexpr int SEG = (FB - 1) * HOP + WIN;  // 5360 samples
+constexpr int SPT = (SEG + LNT - 1) / LNT;  // segment samples per thread
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct MelTables {
   const float* window;   // [WIN]
-  const float2* tw512;   // [512] exp(-2 pi i q / 512)
-  const float2* tw1024;  // [513] exp(-2 pi i k / 1024)
+  const f2* tw512;       // [512] exp(-2 pi i q / 512)
+  const f2* tw1024;      // [513] exp(-2 pi i k / 1024)
   const int* band_start; // [n_mels]
   const int* band_len;   // [n_mels]
   const int* band_off;   // [n_mels] offset into band_w
   const float* band_w;   // [nnz]
 };
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul_mi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) { return __builtin_elementwise_fma(a.yy, b.yx * f2{-1.f, 1.f}, a.xx * b); }
+__device__ __forceinline__ f2 mul_mi(f2 a) { return a.yx * f2{1.f, -1.f}; }  // a * (-i)
 
 // In-register DFT8 (natural-order output), W8 = exp(-2 pi i / 8).
-__device__ __forceinline__ void dft8(float2 (&v)[8]) {
+__device__ __forceinline__ void dft8(f2 (&v)[8]) {
   const float s = 0.70710678118654752f;
-  float2 a0 = cadd(v[0], v[4]), a4 = csub(v[0], v[4]);
-  float2 a1 = cadd(v[1], v[5]), t5 = csub(v[1], v[5]);
-  float2 a2 = cadd(v[2], v[6]), t6 = csub(v[2], v[6]);
-  float2 a3 = cadd(v[3], v[7]), t7 = csub(v[3], v[7]);
-  float2 a5 = make_float2(s * (t5.x + t5.y), s * (t5.y - t5.x));    // * W8^1 = s(1 - i)
-  float2 a6 = cmul_mi(t6);                                          // * W8^2 = -i
-  float2 a7 = make_float2(s * (-t7.x + t7.y), s * (-t7.y - t7.x));  // * W8^3 = s(-1 - i)
-  float2 b0 = cadd(a0, a2), b2 = csub(a0, a2);
-  float2 b1 = cadd(a1, a3), b3 = cmul_mi(csub(a1, a3));
-  float2 b4 = cadd(a4, a6), b6 = csub(a4, a6);
-  float2 b5 = cadd(a5, a7), b7 = cmul_mi(csub(a5, a7));
-  v[0] = cadd(b0, b1); v[4] = csub(b0, b1);
-  v[2] = cadd(b2, b3); v[6] = csub(b2, b3);
-  v[1] = cadd(b4, b5); v[5] = csub(b4, b5);
-  v[3] = cadd(b6, b7); v[7] = csub(b6, b7);
+  const f2 a0 = v[0] + v[4], a4 = v[0] - v[4];
+  const f2 a1 = v[1] + v[5], t5 = v[1] - v[5];
+  const f2 a2 = v[2] + v[6], t6 = v[2] - v[6];
+  const f2 a3 = v[3] + v[7], t7 = v[3] - v[7];
+  const f2 a5 = s * (t5 + t5.yx * f2{1.f, -1.f});   // * W8^1 = s(1 - i)
+  const f2 a6 = mul_mi(t6);                         // * W8^2 = -i
+  const f2 a7 = s * (t7.yx * f2{1.f, -1.f} - t7);   // * W8^3 = s(-1 - i)
+  const f2 b0 = a0 + a2, b2 = a0 - a2;
+  const f2 b1 = a1 + a3, b3 = mul_mi(a1 - a3);
+  const f2 b4 = a4 + a6, b6 = a4 - a6;
+  const f2 b5 = a5 + a7, b7 = mul_mi(a5 - a7);
+  v[0] = b0 + b1; v[4] = b0 - b1;
+  v[2] = b2 + b3; v[6] = b2 - b3;
+  v[1] = b4 + b5; v[5] = b4 - b5;
+  v[3] = b6 + b7; v[7] = b6 - b7;
 }
+
+// Stockham buffer swizzle: entry i at i ^ ((i >> 3) & 7).  The reads (lane + 64 r) stay one contiguous
+// 256-entry span per half wave (conflict-free ds_read_b64); the first pass's writes (8 consecutive
+// entries per lane) spread over 16 banks pairs instead of 2 (1- to 2-way instead of 8-way).
+__device__ __forceinline__ int swz(int i) { return i ^ ((i >> 3) & 7); }
 
 __device__ __forceinline__ int reflect_idx(int n, int T) {
   if (n < 0) n = -n;
@@ -66,150 +83,212 @@ __device__ __forceinline__ int reflect_idx(int n, int T) {
   return n;
 }
 
-constexpr int MAX_NNZ = 1536;  // band weights staged in LDS (htk, 128 mels at n_fft 1024: 1,008)
+constexpr int MAX_NNZ = 2048;  // band weights staged in LDS (htk, 128 mels at n_fft 1024: 1,008 + group padding)
+constexpr float DB_PER_LOG2 = 3.0102999566398120f;  // 10 log10(2)
+// W16^q = exp(-2 pi i q / 16)
+__constant__ const f2 W16[8] = {{1.f, 0.f},
+                                {0.92387953251128674f, -0.38268343236508977f},
+                                {0.70710678118654752f, -0.70710678118654752f},
+                                {0.38268343236508977f, -0.92387953251128674f},
+                                {0.f, -1.f},
+                                {-0.38268343236508977f, -0.92387953251128674f},
+                                {-0.70710678118654752f, -0.70710678118654752f},
+                                {-0.92387953251128674f, -0.38268343236508977f}};
 
-__global__ __launch_bounds__(256) void fft_mel_db_kernel(const float* __restrict__ wav, int64_t ld, int T,
-                                                         int frames, int n_mels, MelTables tb,
-                                                         float* __restrict__ out, float* __restrict__ blockmax) {
+__global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) void fft_mel_db_kernel(const float* __restrict__ wav, int64_t ld, int T,
+                                                            int frames, int nbm, int nitems, int n_mels,
+                                                            MelTables tb, float* __restrict__ out,
+                                                            float* __restrict__ blockmax) {
   __shared__ float seg[SEG];
-  __shared__ float2 buf[4][NC];          // one in-place Stockham buffer per wave
+  __shared__ f2 buf[LW][NC];             // one in-place Stockham buffer per wave
   __shared__ float tile[NMEL_MAX][FB + 1];
   __shared__ float bw[MAX_NNZ];
   __shared__ int bs[NMEL_MAX], bl[NMEL_MAX], bo[NMEL_MAX];
-  __shared__ float redmax[4];
+  __shared__ float redmax[LW];
+  __shared__ int w_lds_s;
 
-  const int b = blockIdx.y;
-  const int f0 = blockIdx.x * FB;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const float* x = wav + (int64_t)b * ld;
 
-  // mel band table into LDS (the per-band loops below then touch no global memory)
-  const int nnz = tb.band_off[n_mels - 1] + tb.band_len[n_mels - 1];
-  const bool w_lds = nnz <= MAX_NNZ;  // block-uniform
-  if (w_lds)
-    for (int i = t; i < nnz; i += 256) bw[i] = tb.band_w[i];
-  for (int m = t; m < n_mels; m += 256) { bs[m] = tb.band_start[m]; bl[m] = tb.band_len[m]; bo[m] = tb.band_off[m]; }
-  // coalesced segment load with reflect padding
-  const int s0 = f0 * HOP - WIN / 2;
-  for (int i = t; i < SEG; i += 256) {
-    const int n = s0 + i;
-    float v = 0.f;
-    if (n >= -(NFFT / 2) && n < T + NFFT / 2) v = x[reflect_idx(n, T)];  // valid reflect range (T > 512)
-    seg[i] = v;
+  // mel band table into LDS (the per-band loops below then touch no global memory), each band widened
+  // to whole 16-B aligned groups of 4 bins with zero weights, so the band loop reads 4 bins and their
+  // 4 weights with one ds_read_b128 each (a table too large for LDS is read from global memory one
+  // weight at a time)
+  if (t == 0) {
+    int acc = 0;
+    for (int m = 0; m < n_mels; ++m) {
+      const int ks = tb.band_start[m], len = tb.band_len[m];
+      bs[m] = ks & ~3;                                  // 16-B aligned first bin
+      bl[m] = ((ks & 3) + len + 3) & ~3;                // whole 4-bin groups
+      bo[m] = acc;
+      acc += bl[m];
+    }
+    w_lds_s = acc <= MAX_NNZ;
+  }
+  __syncthreads();
+  const bool w_lds = w_lds_s;  // block-uniform
+  if (w_lds) {
+    for (int m = wave; m < n_mels; m += LW) {
+      const int lead = tb.band_start[m] & 3, len = tb.band_len[m], src = tb.band_off[m];
+      for (int i = lane; i < bl[m]; i += 64)
+        bw[bo[m] + i] = (i >= lead && i < lead + len) ? tb.band_w[src + i - lead] : 0.f;
+    }
+  } else {
+    for (int m = t; m < n_mels; m += LNT) {
+      bs[m] = tb.band_start[m];
+      bl[m] = tb.band_len[m];
+      bo[m] = tb.band_off[m];
+    }
   }
   // loop-invariant per-lane constants: window taps, stage twiddles, real-split twiddles
-  float2 win[4];
+  f2 win[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int u = 2 * (lane + 64 * r);
-    win[r] = u < WIN ? make_float2(tb.window[u], tb.window[u + 1]) : make_float2(0.f, 0.f);
+    win[r] = u < WIN ? f2{tb.window[u], tb.window[u + 1]} : f2{0.f, 0.f};
   }
-  float2 tw1[8], tw2[8], tws[8];
+  f2 tw1[8], tw2[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     tw1[r] = tb.tw512[((lane % 8) * (NC / 64) * r) & (NC - 1)];
     tw2[r] = tb.tw512[(lane * (NC / 512) * r) & (NC - 1)];
-    tws[r] = tb.tw1024[lane + 64 * r];
   }
-  __syncthreads();
+  // real-split twiddles W1024^(lane + 64 q) = W1024^lane * W16^q (one per lane in registers)
+  f2 tws0 = tb.tw1024[lane];
 
-  const float* bwp = w_lds ? bw : tb.band_w;
-  float lmax = -INFINITY;
-  float2* d = buf[wave];
-  for (int fi = wave; fi < FB; fi += 4) {
-    const int f = f0 + fi;
-    if (f >= frames) break;  // wave-uniform
-    // stage 0 (Ns = 1) reads z[j + 64 r] straight from the segment, z[n] = 0 for n >= 200
-    {
-      float2 v[8];
+  // the reflect-padded input segment of chunk `it` into registers (coalesced 4-B loads)
+  auto seg_load = [&](int it, float (&r)[SPT]) __attribute__((always_inline)) {
+    const int b = it / nbm;
+    const int s0 = (it - b * nbm) * FB * HOP - WIN / 2;
+    const float* x = wav + (int64_t)b * ld;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int n = lane + 64 * r;
-        if (r < 4 && n < WIN / 2) {
-          const float2 xv = *reinterpret_cast<const float2*>(&seg[fi * HOP + 2 * n]);
-          v[r] = make_float2(xv.x * win[r].x, xv.y * win[r].y);
-        } else {
-          v[r] = make_float2(0.f, 0.f);
+    for (int j = 0; j < SPT; ++j) {
+      const int i = t + LNT * j;
+      const int n = s0 + i;
+      r[j] = (i < SEG && n >= -(NFFT / 2) && n < T + NFFT / 2) ? x[reflect_idx(n, T)] : 0.f;  // T > 512
+    }
+  };
+
+  f2* d = buf[wave];
+  float pre[SPT];
+  int it = blockIdx.x;
+  if (it < nitems) seg_load(it, pre);
+  for (; it < nitems; it += gridDim.x) {
+    __syncthreads();  // the previous chunk's segment and tile reads are done (tables visible, 1st pass)
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int i = t + LNT * j;
+      if (i < SEG) seg[i] = pre[j];
+    }
+    __syncthreads();
+    if (it + (int)gridDim.x < nitems) seg_load(it + gridDim.x, pre);  // in flight under this chunk
+    const int b = it / nbm;
+    const int f0 = (it - b * nbm) * FB;
+    float lmax = -INFINITY;
+#pragma unroll 1
+    for (int k = 0; k < FB / LW; ++k) {
+      const int fi = wave * (FB / LW) + k;
+      if (f0 + fi >= frames) break;  // wave-uniform
+      // stage 0 (Ns = 1) reads z[j + 64 r] straight from the segment, z[n] = 0 for n >= 200
+      {
+        f2 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int n = lane + 64 * r;
+          if (r < 4 && n < WIN / 2)
+            v[r] = *reinterpret_cast<const f2*>(&seg[fi * HOP + 2 * n]) * win[r];
+          else
+            v[r] = f2{0.f, 0.f};
         }
+        dft8(v);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[swz(lane * 8 + r)] = v[r];
       }
-      dft8(v);
+      wave_sync();
+      // stages 1 (Ns = 8) and 2 (Ns = 64), in place: every lane's reads land before any lane's writes
+      // (one wave, program order), so the single buffer needs no ping-pong
 #pragma unroll
-      for (int r = 0; r < 8; ++r) d[lane * 8 + r] = v[r];
-    }
-    wave_sync();
-    // stages 1 (Ns = 8) and 2 (Ns = 64), in place: every lane's reads land before any lane's writes
-    // (one wave, program order), so the single buffer needs no ping-pong
+      for (int st = 1; st < 3; ++st) {
+        const int Ns = st == 1 ? 8 : 64;
+        f2 v[8];
+        const int jm = lane % Ns;
 #pragma unroll
-    for (int st = 1; st < 3; ++st) {
-      const int Ns = st == 1 ? 8 : 64;
-      float2 v[8];
-      const int jm = lane % Ns;
+        for (int r = 0; r < 8; ++r) {
+          const f2 a = d[swz(lane + 64 * r)];
+          v[r] = r ? cmul(a, st == 1 ? tw1[r] : tw2[r]) : a;
+        }
+        dft8(v);
+        wave_sync();
+        const int idxD = (lane / Ns) * Ns * 8 + jm;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float2 a = d[lane + 64 * r];
-        if (r) a = cmul(a, st == 1 ? tw1[r] : tw2[r]);
-        v[r] = a;
+        for (int r = 0; r < 8; ++r) d[swz(idxD + r * Ns)] = v[r];
+        wave_sync();
       }
-      dft8(v);
+      // Z in d (natural order). Real-FFT split -> power P[k] (k = 0..512), kept in registers, then
+      // written over the (consumed) spectrum as floats.  X[k] = 0.5 (e - i W^k o) with
+      // e = Z[k] + conj(Z[N-k]), o = Z[k] - conj(Z[N-k]); |X|^2 = 0.25 |e - i W^k o|^2.
+      float pk[8];
+      asm volatile("" : "+v"(tws0));  // derived per frame (not hoisted: registers)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = lane + 64 * q;
+        const f2 zk = d[swz(k)];
+        const f2 zc = d[swz((NC - k) & (NC - 1))] * f2{1.f, -1.f};
+        const f2 tq = q ? cmul(tws0, W16[q]) : tws0;
+        const f2 wo = cmul(tq, zk - zc);
+        const f2 X = (zk + zc) - wo.yx * f2{-1.f, 1.f};  // e - i wo = (e.x + wo.y, e.y - wo.x)
+        pk[q] = 0.25f * (X.x * X.x + X.y * X.y);
+      }
+      float pn = 0.f;
+      if (lane == 0) {
+        const f2 z0 = d[0];
+        const float xn = z0.x - z0.y;  // X[512]
+        pn = xn * xn;
+      }
       wave_sync();
-      const int idxD = (lane / Ns) * Ns * 8 + jm;
+      float* P = reinterpret_cast<float*>(d);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) d[idxD + r * Ns] = v[r];
+      for (int q = 0; q < 8; ++q) P[lane + 64 * q] = pk[q];
+      if (lane == 0) P[NC] = pn;
+      wave_sync();
+      for (int m = lane; m < n_mels; m += 64) {
+        const int ks = bs[m], kl = bl[m], off = bo[m];
+        float acc = 0.f;
+        if (w_lds) {
+          for (int i = 0; i < kl; i += 4) {  // zero weights outside the band (P stays finite there)
+            const f32x4 w4 = *reinterpret_cast<const f32x4*>(&bw[off + i]);
+            const f32x4 p4 = *reinterpret_cast<const f32x4*>(&P[ks + i]);
+            acc = fmaf(p4[0], w4[0], acc);
+            acc = fmaf(p4[1], w4[1], acc);
+            acc = fmaf(p4[2], w4[2], acc);
+            acc = fmaf(p4[3], w4[3], acc);
+          }
+        } else {
+          for (int i = 0; i < kl; ++i) acc = fmaf(P[ks + i], tb.band_w[off + i], acc);
+        }
+        // AmplitudeToDB (multiplier 10, amin 1e-10): the floor is the exact torch value (-100.0f), so
+        // an all-silent clip stays constant (std 0: no normalisation)
+        const float db = acc <= 1e-10f ? -100.f : DB_PER_LOG2 * __builtin_amdgcn_logf(acc);
+        tile[m][fi] = db;
+        lmax = fmaxf(lmax, db);
+      }
       wave_sync();
     }
-    // Z in d (natural order). Real-FFT split -> power P[k] (k = 0..512), kept in registers, then
-    // written over the (consumed) spectrum as floats
-    float pk[8];
-    float pn = 0.f;
+    lmax = wave_max(lmax);
+    if (lane == 0) redmax[wave] = lmax;
+    __syncthreads();
+    if (t == 0) {
+      float mx = redmax[0];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = lane + 64 * q;
-      const float2 zk = d[k];
-      const float2 zc = d[(NC - k) & (NC - 1)];
-      const float2 zcj = make_float2(zc.x, -zc.y);
-      const float2 e = cadd(zk, zcj);          // 2 * even part
-      const float2 o = csub(zk, zcj);          // 2i * odd part (before twiddle)
-      // X[k] = 0.5*(e - i W^k o)
-      const float2 wo = cmul(tws[q], o);
-      const float2 X = make_float2(0.5f * (e.x + wo.y), 0.5f * (e.y - wo.x));
-      pk[q] = X.x * X.x + X.y * X.y;
+      for (int w = 1; w < LW; ++w) mx = fmaxf(mx, redmax[w]);
+      blockmax[it] = mx;  // it = b * nbm + chunk
     }
-    if (lane == 0) {
-      const float2 z0 = d[0];
-      const float xn = z0.x - z0.y;  // X[512]
-      pn = xn * xn;
+    // tile store: rows of FB contiguous frames
+    const int nf = min(FB, frames - f0);
+    float* ob = out + (int64_t)b * n_mels * frames + f0;
+    for (int i = t; i < n_mels * FB; i += LNT) {
+      const int m = i / FB, fi = i % FB;
+      if (fi < nf) ob[(int64_t)m * frames + fi] = tile[m][fi];
     }
-    wave_sync();
-    float* P = reinterpret_cast<float*>(d);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) P[lane + 64 * q] = pk[q];
-    if (lane == 0) P[NC] = pn;
-    wave_sync();
-    for (int m = lane; m < n_mels; m += 64) {
-      const int ks = bs[m], kl = bl[m], off = bo[m];
-      float acc = 0.f;
-      for (int i = 0; i < kl; ++i) acc = fmaf(P[ks + i], bwp[off + i], acc);
-      // AmplitudeToDB (multiplier 10, amin 1e-10): the floor is the exact torch value (-100.0f; f32
-      // log10f is 1 ulp low there), so an all-silent clip stays constant (std 0: no normalisation)
-      const float db = acc <= 1e-10f ? -100.f : 10.f * log10f(acc);
-      tile[m][fi] = db;
-      lmax = fmaxf(lmax, db);
-    }
-    wave_sync();
-  }
-  lmax = wave_max(lmax);
-  if (lane == 0) redmax[wave] = lmax;
-  __syncthreads();
-  if (t == 0) {
-    blockmax[(int64_t)b * gridDim.x + blockIdx.x] =
-        fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
-  }
-  // coalesced tile store: rows of FB contiguous frames
-  const int nf = min(FB, frames - f0);
-  float* ob = out + (int64_t)b * n_mels * frames + f0;
-  for (int i = t; i < n_mels * FB; i += 256) {
-    const int m = i / FB, fi = i % FB;
-    if (fi < nf) ob[(int64_t)m * frames + fi] = tile[m][fi];
   }
 }
 
@@ -342,13 +421,17 @@ extern "C" int mia_logmel_fwd(const float* wav, int64_t B, int64_t T, int64_t ld
                 "logmel: bad shape B=%lld T=%lld", (long long)B, (long long)T);
   const int frames = (int)(1 + T / HOP);
   const int nbm = (int)cdiv(frames, FB);
+  const int64_t nitems = B * nbm;
+  MIA_CHECK_ARG(nitems < (1ll << 31), "logmel: too many frame chunks");
   float* blockmax = reinterpret_cast<float*>(workspace);
   double* partial = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + cdiv(B * nbm * 4, 16) * 16);
-  MelTables tb{window, reinterpret_cast<const float2*>(tw512), reinterpret_cast<const float2*>(tw1024),
+  MelTables tb{window, reinterpret_cast<const f2*>(tw512), reinterpret_cast<const f2*>(tw1024),
                band_start, band_len, band_off, band_w};
   hipStream_t s = as_stream(stream);
-  fft_mel_db_kernel<<<dim3(nbm, (unsigned)B), 256, 0, s>>>(wav, ld_wav, (int)T, frames, cfg->n_mels, tb, out,
-                                                         blockmax);
+  // three 4-wave workgroups per CU (LDS 43 KB, 152 VGPRs), persistent over the (clip, chunk) items
+  const unsigned grid = (unsigned)std::min<int64_t>(nitems, 3 * mia::cu_count());
+  fft_mel_db_kernel<<<grid, LNT, 0, s>>>(wav, ld_wav, (int)T, frames, nbm, (int)nitems, cfg->n_mels, tb, out,
+                                        blockmax);
   MIA_LAUNCH_CHECK("fft_mel_db");
   const int64_t per_clip = (int64_t)cfg->n_mels * frames;
   if (cfg->normalize) {
