@@ -716,16 +716,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 }
 
 // Query-parallel dQ.  One wave = 32 queries (query on the lane), 4 waves = 128 per block, sweeping
-// 64-key tiles of K and V (LDS-DMA, double-buffered): S'^T = K Q'^T - L2, dP'^T = V dO^T - delta with
-// the row constants as fifth k-steps (B-side fragments in registers), dQ^T += K^T dS^T with dS^T
-// straight from the accumulators.
+// 64-key tiles of K and V (LDS-DMA, 3-slot ring): S'^T = K Q'^T - L2, dP'^T = V dO^T - delta with the
+// row constants as per-lane f32 adds (the accumulator column is the lane's query), dQ^T += K^T dS^T
+// with dS^T straight from the accumulators.
 constexpr int BWD_Q = 128;
 
 // kvalid = keys of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask in one body, so
 // the ring's remainder tiles are the same code as its loop (per-tile TAIL copies spilled 76 VGPRs there)
 __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const bf16* V_, const bf16x8 (&qf)[4],
-                                        const bf16x8 (&gf)[4], bf16x8 one, bf16x8 lf, bf16x8 df_, int kvalid,
-                                        int lane) {
+                                        const bf16x8 (&gf)[4], float nl, float nd, int kvalid, int lane) {
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh) {
     const int kr = 32 * kh + (lane & 31);
@@ -736,17 +735,17 @@ __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const 
       sc = mfma(frag_row_sw(K_, kr, ks, lane), qf[ks], sc);
       dp = mfma(frag_row_sw(V_, kr, ks, lane), gf[ks], dp);
     }
-    sc = mfma(one, lf, sc);
-    dp = mfma(one, df_, dp);
+    // the lane's column is one query: its row constants are two per-lane scalars (VALU adds beside the
+    // other waves' MFMAs instead of two fifth-k-step MFMAs per key half)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r]);
+    for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r] + nl);
     if (kvalid < 64) {
       const int lim = kvalid - 32 * kh - 4 * (lane >> 5);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[r] = ((r & 3) + 8 * (r >> 2)) < lim ? sc[r] : 0.f;
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dp[r] *= sc[r];
+    for (int r = 0; r < 16; ++r) dp[r] = (dp[r] + nd) * sc[r];
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
       const bf16x8 dsf = acc_frag(dp, sk);
@@ -784,26 +783,24 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
     for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
     gf[ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
   }
-  // fifth-k-step B fragments of this lane's query (zero for a query past the end: p = 1, dS = 0)
-  bf16x8 lf, dlf;
+  // this lane's query's row constants -L2 and -delta in f32: the fragment rows' three bf16 parts summed
+  // (exact: split3 leaves 8 + 8 + 8 significant bits); zero for a query past the end (p = 1, dS = 0)
+  float nl = 0.f, nd = 0.f;
   {
     const bf16* fr = frag + ((int64_t)bh * 2 * N + (qv ? q : 0)) * 8;
-    lf = row_frag(fr);
-    dlf = row_frag(fr + (int64_t)N * 8);
-    if (!qv) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { lf[j] = (bf16)0.f; dlf[j] = (bf16)0.f; }
+    const bf16x8 lf = row_frag(fr), dlf = row_frag(fr + (int64_t)N * 8);
+    if (qv) {
+      nl = ((float)lf[0] + (float)lf[1]) + (float)lf[2];
+      nd = ((float)dlf[0] + (float)dlf[1]) + (float)dlf[2];
     }
   }
   settle(qf);
   settle(gf);
-  settle1(lf);
-  settle1(dlf);
+  asm volatile("" ::"v"(nl), "v"(nd));
   if (ntiles > 1) {
     kd.issue(Ks[1], tile_bytes, wave);
     vd.issue(Vs[1], tile_bytes, wave);
   }
-  const bf16x8 one = ones3(lane);
   f32x16 acc[2];
   acc[0] = zero16(); acc[1] = zero16();
   // one tile in slot P of the 3-slot ring: tile j + 2's DMA flies under this tile's work and tile j + 1's
@@ -815,7 +812,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
       kd.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
       vd.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
     }
-    dq_tile(acc, Ks[P], Vs[P], qf, gf, one, lf, dlf, N - j * 64, lane);
+    dq_tile(acc, Ks[P], Vs[P], qf, gf, nl, nd, N - j * 64, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

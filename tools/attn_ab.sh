@@ -1,0 +1,13 @@
+#!/bin/bash
+# attention backward A/B: product library vs tools/probe/libmia_<name>.so (bench_attn_bwd.py), then the
+# attention parity tests on the product library
+OUT=gpurun_out/attnab; mkdir -p $OUT
+for i in 1 2; do
+  for v in base "$@"; do
+    if [ $v = base ]; then LIBV=; else LIBV=$(realpath tools/probe/libmia_$v.so); fi
+    echo "== $v $i" >> $OUT/ab.log
+    MIAUDIO_LIB=$LIBV BATCH=256 ROUNDS=2 timeout -k 10 200 python -u tools/bench_attn_bwd.py >> $OUT/ab.log 2>&1 || exit 1
+  done
+done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_ast.py tests/test_gpu_fullsize.py -k "attention" > $OUT/tests.log 2>&1
+tail -3 $OUT/tests.log
