@@ -54,6 +54,16 @@ struct MArgs {
   uint8_t* mxs;       // ... and its scales [M][N / 32]
 };
 
+typedef unsigned mg_u32x4 __attribute__((ext_vector_type(4)));
+// The bf16 epilogue's 16-B stores (8 lanes = one whole 128-B line), non-temporal: the outputs (0.65-2.6 GB
+// at the AST shapes) are far larger than the Infinity Cache.  A/B at B = 256 (tools/gemm_ab.sh): qkv.fwd
+// 1.635 -> 1.57 ms, fc1.fwd (GELU_SAVE) 2.765 -> 2.60 ms, fc2.dgrad 3.11 -> 3.08 ms; AST step +1 %.  (The
+// f32 residual outputs leave the accumulators as 64-B halves of lines: non-temporal partial lines are
+// twice as slow, they stay default-policy.)
+__device__ __forceinline__ void mg_st16(void* p, uint4 v) {
+  __builtin_nontemporal_store(__builtin_bit_cast(mg_u32x4, v), reinterpret_cast<mg_u32x4*>(p));
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int64_t bytes) {
   const uint32_t n = bytes <= 0 ? 0u : (bytes >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
@@ -283,7 +293,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
       const bool ok = m < g.M && n < g.N;  // no early exit: the MX block exponent is a 4-lane exchange
       uint4 o = q;
       if constexpr (EPI == EPI_GELU_SAVE) {
-        if (ok) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n) = q;
+        if (ok) mg_st16(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n, q);
       }
       if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
         f32x4 v0 = unpack4(make_uint2(q.x, q.y)), v1 = unpack4(make_uint2(q.z, q.w));
@@ -319,7 +329,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
           }
         }
       }
-      if (ok) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n) = o;
+      if (ok) mg_st16(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n, o);
     }
     if constexpr (EPI == EPI_DGELU) {
       if (g.colsum_part) {
