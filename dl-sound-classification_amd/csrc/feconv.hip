@@ -430,6 +430,7 @@ template <bool STATS>
 __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
   constexpr int ROWB = 88, CPYB = 8 * ROWB;
   __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
+  __shared__ __attribute__((aligned(16))) char stage[4][2048];  // the item's 32 px x 64 B output run
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
   const int items = g.n * g.oh * g.nseg;
@@ -507,25 +508,36 @@ __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
       }
     const int seg = it % g.nseg, rest = it / g.nseg;
     const int oy = rest % g.oh, b = rest / g.oh;
-    const int ox = seg * 32 + o;
-    if (ox < g.ow) {
-      bf16* dst = g.y + (((int64_t)b * g.oh + oy) * g.ow + ox) * 32 + c0;
+    const int ox0 = seg * 32, ox = ox0 + o;
+    // as fe_conv1: the item's 32 output pixels x 64 B regrouped through the per-wave LDS image into two
+    // 1 KB runs of whole rows, stored non-temporal
+    char* stg = stage[wv];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint32_t w4[4];
+    for (int h = 0; h < 2; ++h) {
+      uint32_t w4[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int e = 8 * h + 2 * i;
-          const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
-          w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
-          if constexpr (STATS) {
+      for (int i = 0; i < 4; ++i) {
+        const int e = 8 * h + 2 * i;
+        const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
+        w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+        if constexpr (STATS) {
+          if (ox < g.ow) {
             const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
             s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
             s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
           }
         }
-        *reinterpret_cast<u32x4*>(dst + 16 * h) = u32x4{w4[0], w4[1], w4[2], w4[3]};
       }
+      const int k = (lane >> 5) + 2 * h;
+      *reinterpret_cast<u32x4*>(stg + o * 64 + ((k ^ ((o >> 1) & 3)) << 4)) = u32x4{w4[0], w4[1], w4[2], w4[3]};
+    }
+    wave_sync();
+    bf16* yrow = g.y + (((int64_t)b * g.oh + oy) * g.ow + ox0) * 32;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 16 * h + (lane >> 2), k = lane & 3;
+      const u32x4 q = *reinterpret_cast<const u32x4*>(stg + r * 64 + ((k ^ ((r >> 1) & 3)) << 4));
+      if (ox0 + r < g.ow) __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(yrow + r * 32 + 8 * k));
     }
   };
 

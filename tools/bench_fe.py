@@ -30,14 +30,20 @@ x = torch.randn(B, T, generator=g, device=dev) * 0.1
 w1 = (torch.randn(32, 64, generator=g, device=dev) * 0.1).to(torch.bfloat16)
 b1 = torch.randn(32, generator=g, device=dev) * 0.1
 y1c = torch.empty(B * W1, 32, dtype=torch.bfloat16, device=dev)
+H3, W3 = 64, 860  # trunk conv3 input (B, 64, 860) -> (B, 57, 853, 32)
+x3 = (torch.randn(B, H3, W3, generator=g, device=dev) * 0.5).to(torch.bfloat16)
+w3 = (torch.randn(32, 64, generator=g, device=dev) * 0.1).to(torch.bfloat16)
+b3 = torch.randn(32, generator=g, device=dev) * 0.1
+y3 = torch.empty(B * (H3 - 7) * (W3 - 7), 32, dtype=torch.bfloat16, device=dev)
 runs = {
+    "fe_conv3_fwd": lambda: K.fe_conv3_fwd(x3, w3, b3, y3, B, H3, W3, stats=True),
     "fe_conv1_fwd": lambda: K.fe_conv1_fwd(x, w1, b1, y1c, B, T, stats=True),
     "fe_conv2_fwd": lambda: K.fe_conv2_fwd(y1, sc, sh, w0, bias, y2, B, W1, W2),
     "fe_conv2_dgrad": lambda: K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2),
     "fe_conv2_wgrad": lambda: K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2),
     "dgrad+wgrad": lambda: (K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2), K.fe_conv2_wgrad(dy2, y1, sc, sh, dw, B, W1, W2)),
 }
-byts = {"fe_conv1_fwd": x.numel() * 4 + y1c.numel() * 2, "fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2,
+byts = {"fe_conv3_fwd": x3.numel() * 2 + y3.numel() * 2, "fe_conv1_fwd": x.numel() * 4 + y1c.numel() * 2, "fe_conv2_fwd": (y1.numel() + y2.numel()) * 2, "fe_conv2_dgrad": (dy2.numel() + da1.numel()) * 2,
         "fe_conv2_wgrad": (dy2.numel() + y1.numel()) * 2, "dgrad+wgrad": (2 * dy2.numel() + y1.numel() + da1.numel()) * 2}
 flop = 2.0 * B * W2 * 64 * 512
 want = set(sys.argv[1:])
@@ -61,6 +67,6 @@ for name, fn in runs.items():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    out = {"fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name)
+    out = {"fe_conv3_fwd": y3, "fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name)
     dg = f"digest {digest(out):x}" if out is not None else ""
     print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s  {dg}", flush=True)

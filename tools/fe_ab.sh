@@ -1,5 +1,11 @@
-set -e
-mkdir -p gpurun_out/feab
-
-LOGMEL_LIBS=tools/probe/libmia_logmel_old.so BATCH=256 timeout -k 10 120 python -u tools/bench_logmel.py > gpurun_out/feab/logmel.log 2>&1
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_logmel.py tests/test_gpu_envnet.py tests/test_gpu_e2e_bf16.py > gpurun_out/feab/tests.log 2>&1
+#!/bin/bash
+# frontend kernel A/B: tools/bench_fe.py on the product library and tools/probe/libmia_<name>.so builds
+OUT=gpurun_out/feab; mkdir -p $OUT
+for i in 1 2; do
+  for v in base "$@"; do
+    if [ $v = base ]; then LIBV=; else LIBV=$(realpath tools/probe/libmia_$v.so); fi
+    echo "== $v $i" >> $OUT/ab.log
+    MIAUDIO_LIB=$LIBV timeout -k 10 120 python -u tools/bench_fe.py ${KERNELS:-fe_conv3_fwd fe_conv1_fwd} >> $OUT/ab.log 2>&1 || exit 1
+  done
+done
+grep -v amdgpu $OUT/ab.log
