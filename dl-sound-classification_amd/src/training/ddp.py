@@ -25,7 +25,10 @@ never written on one GPU; src/miaudio/kernels.py::defer_weight_grad) crosses the
   45 MB per rank instead of a 1.38 GB f32 ring all-reduce -- and ``finish()`` defers the AVERAGED gradient
   (dY_all / world)^T X_all, K = world * B, to FusedAdam exactly as one GPU does.  Every rank runs the same
   sums-only and Adam GEMMs on identical operands, so the parameters stay identical bit for bit, and the
-  per-GPU program at N > 1 is the N = 1 program with K = world * B in those two GEMMs;
+  per-GPU program at N > 1 is the N = 1 program with K = world * B in those two GEMMs.  Above
+  ``materialise_k`` gathered rows (world >= 8 at B = 256) the averaged gradient is instead written once by
+  the same GEMM with its per-tile sums of squares (the deferred pair recomputes the product; at K = 2048
+  that is 5.06 against 4.27 ms per step) -- the same sums, so the same parameters;
 * ``"allreduce"``: FC1's gradient is materialised as 16 row chunks, each all-reduced as its GEMM is enqueued
   (above).
 
@@ -44,14 +47,22 @@ import torch
 import torch.distributed as dist
 
 BUCKET_BYTES = 64 << 20
+# Gathered rows K above which the averaged FC1 gradient is materialised by one GEMM (with per-tile sums of
+# squares) instead of deferred: the deferred form runs the product twice (sums-only GEMM in the backward,
+# the Adam GEMM in the step), the materialised form once plus a 1.38 GB write and read.  Measured on one
+# MI355X (tools/bench_fc1_update.py, EnvNet FC1 4096 x 84 480): K = 256 / 512 / 1024 / 2048 -> deferred
+# 1.93 / 2.22 / 2.98 / 5.06 ms, materialised 2.32 / 2.52 / 3.26 / 4.27 ms per update.
+MATERIALISE_K = 1536
 
 
 class GradAllReducer:
     def __init__(self, model: torch.nn.Module, world: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 broadcast_buffers: bool = True, fc1_exchange: str = "gather"):
+                 broadcast_buffers: bool = True, fc1_exchange: str = "gather",
+                 materialise_k: int = MATERIALISE_K):
         if fc1_exchange not in ("gather", "allreduce"):
             raise ValueError(f"fc1_exchange must be 'gather' or 'allreduce', not {fc1_exchange!r}")
         self.fc1_exchange = fc1_exchange
+        self.materialise_k = materialise_k
         self.model = model
         self.world = world or dist.get_world_size()
         self.params = [p for p in model.parameters() if p.requires_grad]
@@ -215,8 +226,17 @@ class GradAllReducer:
             from ..miaudio import kernels as K
             from ..miaudio import lib as L
             for param, dy_all, x_all, M, N, Kk in self.gathers:
-                K.defer_weight_grad(param, K.dense(dy_all, L.RC, Kk, M), K.dense(x_all, L.RC, Kk, N), M, N, Kk,
-                                    keep=(dy_all, x_all), tag="fc1.wgrad")
+                A, B = K.dense(dy_all, L.RC, Kk, M), K.dense(x_all, L.RC, Kk, N)
+                if Kk > self.materialise_k:
+                    # one GEMM (same main loop and sum order as the deferred pair) writes the gradient and
+                    # its per-tile sums of squares; FusedAdam then streams it like any other gradient
+                    dW = torch.empty(M, N, dtype=torch.float32, device=dy_all.device)
+                    sq = K.sqsum_slots(dW, M, N)
+                    K.gemm(A, B, K.epilogue(dW, N, sqsum=sq), M, N, Kk, L.BF16, tag="fc1.wgrad")
+                    param.grad = dW.view_as(param)
+                    K.tag_sqsum(param, dW, sq)
+                else:
+                    K.defer_weight_grad(param, A, B, M, N, Kk, keep=(dy_all, x_all), tag="fc1.wgrad")
             self.gathers.clear()
         for flat, tensors, copied in self.pending:
             if copied:

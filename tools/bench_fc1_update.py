@@ -1,0 +1,59 @@
+"""EnvNet FC1 (4096 x 84 480) weight update at K = world * 256 gathered rows: the deferred form (sums-only
+GEMM + the Adam GEMM that recomputes the product, what one GPU runs) against the materialised form (one
+GEMM writing the f32 gradient with per-tile sums of squares, then FusedAdam's streaming update), as the
+data-parallel gather form would run them at world = K / 256 (src/training/ddp.py).  HIP events on the
+launch stream, interleaved rounds.
+    python tools/bench_fc1_update.py [K ...]"""
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "dl-sound-classification_amd"))
+import torch  # noqa: E402
+
+from src.miaudio import kernels as K  # noqa: E402
+from src.miaudio import lib as L  # noqa: E402
+from src.training.optim import FusedAdam  # noqa: E402
+
+dev = torch.device("cuda:0")
+M, N = 4096, 84480
+Ks = [int(k) for k in sys.argv[1:]] or [256, 512, 1024, 2048]
+g = torch.Generator(device=dev).manual_seed(0)
+p = torch.nn.Parameter(torch.randn(M, N, generator=g, device=dev) * 0.01)
+opt = FusedAdam([p], lr=1e-4, weight_decay=1e-4, clip=1.0)
+
+
+def step(kind, dy, x, Kk):
+    A, B = K.dense(dy, L.RC, Kk, M), K.dense(x, L.RC, Kk, N)
+    if kind == "deferred":
+        K.defer_weight_grad(p, A, B, M, N, Kk, keep=(dy, x))
+    else:
+        dW = torch.empty(M, N, dtype=torch.float32, device=dev)
+        sq = K.sqsum_slots(dW, M, N)
+        K.gemm(A, B, K.epilogue(dW, N, sqsum=sq), M, N, Kk, L.BF16)
+        p.grad = dW
+        K.tag_sqsum(p, dW, sq)
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+
+
+for Kk in Ks:
+    dy = (torch.randn(Kk, M, generator=g, device=dev) * 0.01).to(torch.bfloat16)
+    x = torch.randn(Kk, N, generator=g, device=dev).to(torch.bfloat16)
+    res = {"deferred": [], "materialised": []}
+    for r in range(3):
+        for kind in res:
+            for _ in range(2):
+                step(kind, dy, x, Kk)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                step(kind, dy, x, Kk)
+            e1.record()
+            torch.cuda.synchronize()
+            res[kind].append(e0.elapsed_time(e1) / 5)
+    print(f"K={Kk:5d} (world {Kk // 256}): deferred {min(res['deferred']):.3f} ms  "
+          f"materialised {min(res['materialised']):.3f} ms", flush=True)
+    del dy, x
+    torch.cuda.empty_cache()
