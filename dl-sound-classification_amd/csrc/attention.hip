@@ -329,8 +329,10 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&s)[2], float d, bf16x8 (&
   }
 }
 
-// kvalid = keys of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask, so the ring's
-// last tiles are the loop's own code (per-tile TAIL copies spilled ~260 VGPRs in the remainder code)
+// kvalid = keys of the tile inside the sequence (>= 64: all): a wave-uniform mask that only the peeled first
+// tile (the sequence's last key tile: the kernel walks the keys backwards) passes at run time; the loop's
+// tiles pass 64, so no mask instruction is emitted there (as a run-time mask on every tile the compiler
+// if-converted it into 32 compares + 32 selects per tile)
 template <bool FIRST>
 __device__ __forceinline__ void fwd_softmax(f32x16 (&s)[2], FwdAcc& a, bf16x8 (&pf)[4], int kvalid, int lane) {
   if (kvalid < 64) {
@@ -394,8 +396,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
   TileDMA kdma, vdma;
   kdma.init(base + H * D, ldt, N, wave, lane);
   vdma.init(base + 2 * H * D, ldt, N, wave, lane);
-  kdma.issue(Ks[0], 0, wave);
-  vdma.issue(Vs[0], 0, wave);
+  // key tiles in reverse order: the sequence's partial last tile is the peeled first tile (FIRST), so the
+  // key mask exists only there and the loop's tiles carry no mask instructions
+  kdma.issue(Ks[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
+  vdma.issue(Vs[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
   // a wave past the last query computes on zero queries (finite, never stored): no branch in the loop
   const int q = qb * FWD_Q + wave * 32 + (lane & 31);
   bf16x8 qf[4];
@@ -412,8 +416,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     for (int ks = 0; ks < 4; ++ks) *reinterpret_cast<bf16x8*>(qrow + 16 * ks) = qf[ks];
   }
   if (ntiles > 1) {
-    kdma.issue(Ks[1], tile_bytes, wave);
-    vdma.issue(Vs[1], tile_bytes, wave);
+    kdma.issue(Ks[1], (unsigned)(ntiles - 2) * tile_bytes, wave);
+    vdma.issue(Vs[1], (unsigned)(ntiles - 2) * tile_bytes, wave);
   }
   bf16x8 one;
 #pragma unroll
@@ -431,13 +435,14 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16* __restrict
     constexpr int P = decltype(slot)::value;
     constexpr int PN = (P + 2) % 3;
     const bool ahead = j + 2 < ntiles;
+    const int kt = ntiles - 1 - j;  // key tile
     if (ahead) {
-      kdma.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
-      vdma.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
+      kdma.issue(Ks[PN], (unsigned)(kt - 2) * tile_bytes, wave);
+      vdma.issue(Vs[PN], (unsigned)(kt - 2) * tile_bytes, wave);
     }
     fwd_qk(s, Ks[P], qf, one, a.mrow, lane);
     __builtin_amdgcn_s_setprio(1);  // the softmax's VALU issues ahead of the co-resident waves' MFMA streams
-    fwd_softmax<decltype(first)::value>(s, a, pf, N - j * 64, lane);
+    fwd_softmax<decltype(first)::value>(s, a, pf, decltype(first)::value ? N - kt * 64 : 64, lane);
     __builtin_amdgcn_s_setprio(0);
     fwd_pv(a, Vs[P], pf, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j + 1's pieces have landed
@@ -721,8 +726,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 // with dS^T straight from the accumulators.
 constexpr int BWD_Q = 128;
 
-// kvalid = keys of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask in one body, so
-// the ring's remainder tiles are the same code as its loop (per-tile TAIL copies spilled 76 VGPRs there)
+// kvalid = keys of the tile inside the sequence (>= 64: all): a wave-uniform mask that only the peeled first
+// tile (the last key tile: the kernel walks the keys backwards) passes at run time; the loop passes 64
 __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const bf16* V_, const bf16x8 (&qf)[4],
                                         const bf16x8 (&gf)[4], float nl, float nd, int kvalid, int lane) {
 #pragma unroll
@@ -771,8 +776,9 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   TileDMA kd, vd;
   kd.init(base + H * D, ldt, N, wave, lane);
   vd.init(base + 2 * H * D, ldt, N, wave, lane);
-  kd.issue(Ks[0], 0, wave);
-  vd.issue(Vs[0], 0, wave);
+  // key tiles in reverse order (as the forward): only the peeled first tile can be partial
+  kd.issue(Ks[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
+  vd.issue(Vs[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
   const int q = qb * BWD_Q + wave * 32 + (lane & 31);
   const bool qv = q < N;
   bf16x8 qf[4], gf[4];
@@ -798,21 +804,22 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   settle(gf);
   asm volatile("" ::"v"(nl), "v"(nd));
   if (ntiles > 1) {
-    kd.issue(Ks[1], tile_bytes, wave);
-    vd.issue(Vs[1], tile_bytes, wave);
+    kd.issue(Ks[1], (unsigned)(ntiles - 2) * tile_bytes, wave);
+    vd.issue(Vs[1], (unsigned)(ntiles - 2) * tile_bytes, wave);
   }
   f32x16 acc[2];
   acc[0] = zero16(); acc[1] = zero16();
   // one tile in slot P of the 3-slot ring: tile j + 2's DMA flies under this tile's work and tile j + 1's
-  auto tile = [&](auto tail, auto slot, int j) __attribute__((always_inline)) {
+  auto tile = [&](auto first, auto slot, int j) __attribute__((always_inline)) {
     constexpr int P = decltype(slot)::value;
     constexpr int PN = (P + 2) % 3;
     const bool ahead = j + 2 < ntiles;
+    const int kt = ntiles - 1 - j;  // key tile
     if (ahead) {
-      kd.issue(Ks[PN], (unsigned)(j + 2) * tile_bytes, wave);
-      vd.issue(Vs[PN], (unsigned)(j + 2) * tile_bytes, wave);
+      kd.issue(Ks[PN], (unsigned)(kt - 2) * tile_bytes, wave);
+      vd.issue(Vs[PN], (unsigned)(kt - 2) * tile_bytes, wave);
     }
-    dq_tile(acc, Ks[P], Vs[P], qf, gf, nl, nd, N - j * 64, lane);
+    dq_tile(acc, Ks[P], Vs[P], qf, gf, nl, nd, decltype(first)::value ? N - kt * 64 : 64, lane);
     if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -820,7 +827,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 and the Q / dO fragments
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  ring3_guarded<0>(0, ntiles, tile);
+  tile(std::true_type{}, std::integral_constant<int, 0>{}, 0);
+  ring3_guarded<1>(1, ntiles, tile);
   if (!qv) return;
   bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D;
 #pragma unroll
