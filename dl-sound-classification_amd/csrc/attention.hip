@@ -591,7 +591,8 @@ __device__ __forceinline__ bf16x8 row_frag(const bf16* row) { return *reinterpre
 // registers over the whole sequence: no atomics, deterministic.
 constexpr int BWD_K = 128;
 
-// qvalid = queries of the tile inside the sequence (>= 64: all): a runtime, wave-uniform mask in one body
+// qvalid = queries of the tile inside the sequence (>= 64: all): a wave-uniform mask that only the peeled first
+// tile (the last query tile: the kernel walks the queries backwards) passes at run time
 __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
                                           const bf16* F_, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one,
                                           int qvalid, int lane) {
@@ -663,9 +664,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
   fd.init(frag + (int64_t)bh * 2 * N * 8, N);
-  qd.issue(Qs[0], 0, wave);
-  gd.issue(Gs[0], 0, wave);
-  fd.issue(Fs[0], 0, wave, lane);
+  // query tiles in reverse order: the partial last query tile is the peeled first tile, the only one that
+  // carries the query mask
+  qd.issue(Qs[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
+  gd.issue(Gs[0], (unsigned)(ntiles - 1) * tile_bytes, wave);
+  fd.issue(Fs[0], (unsigned)(ntiles - 1) * 64u, wave, lane);
   const int key = kb * BWD_K + wave * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
 #pragma unroll
@@ -678,14 +681,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   const bf16x8 one = ones3(lane);
   f32x16 dk[2], dv[2];
   dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-  auto tile = [&](auto tail, auto par, int j) __attribute__((always_inline)) {
+  auto tile = [&](auto first, auto par, int j) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
+    const int qt = ntiles - 1 - j;  // query tile
     if (j + 1 < ntiles) {
-      qd.issue(Qs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
-      gd.issue(Gs[P ^ 1], (unsigned)(j + 1) * tile_bytes, wave);
-      fd.issue(Fs[P ^ 1], (unsigned)(j + 1) * 64u, wave, lane);
+      qd.issue(Qs[P ^ 1], (unsigned)(qt - 1) * tile_bytes, wave);
+      gd.issue(Gs[P ^ 1], (unsigned)(qt - 1) * tile_bytes, wave);
+      fd.issue(Fs[P ^ 1], (unsigned)(qt - 1) * 64u, wave, lane);
     }
-    dkdv_tile(dk, dv, Qs[P], Gs[P], Fs[P], kf, vf, one, N - j * 64, lane);
+    dkdv_tile(dk, dv, Qs[P], Gs[P], Fs[P], kf, vf, one, decltype(first)::value ? N - qt * 64 : 64, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -695,9 +699,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   using P1 = std::integral_constant<int, 1>;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int j = 0; j < ntiles; j += 2) {  // no remainder code (see ring3_guarded)
-    tile(F{}, P0{}, j);
-    if (j + 1 < ntiles) tile(F{}, P1{}, j + 1);
+  tile(T{}, P0{}, 0);
+  for (int j = 1; j < ntiles; j += 2) {  // no remainder code (see ring3_guarded)
+    tile(F{}, P1{}, j);
+    if (j + 1 < ntiles) tile(F{}, P0{}, j + 1);
   }
   if (key >= N) return;
   bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
