@@ -7,7 +7,7 @@ mkdir -p $OUT
 ( while sleep 45; do date +%T >> $OUT/heartbeat.txt; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-LEGS=${LEGS:-"envnet ast"}
+LEGS=${LEGS:-"envnet ast ast-fp8"}
 if [ "${BENCH:-1}" = 1 ]; then
   timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
 fi
