@@ -765,8 +765,9 @@ __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const 
   }
 }
 
-__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                             const bf16* __restrict__ frag, bf16* __restrict__ dqkv,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ out,
+                                                             const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                             bf16* __restrict__ frag, bf16* __restrict__ dqkv,
                                                              int N, int H, int nqb, float scale, float scale_log2) {
   __shared__ __attribute__((aligned(1024))) bf16 Ks[3][64 * 64];
   __shared__ __attribute__((aligned(1024))) bf16 Vs[3][64 * 64];
@@ -787,22 +788,35 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(const bf16* __restr
   const int q = qb * BWD_Q + wave * 32 + (lane & 31);
   const bool qv = q < N;
   bf16x8 qf[4], gf[4];
+  float dsum = 0.f;  // this lane's half of delta = sum_d dO * O
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const bf16x8 r = load_frag_global(base + (int64_t)q * ldt, ks, lane, qv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[ks][j] = (bf16)((float)r[j] * scale_log2);
     gf[ks] = load_frag_global(dout + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
+    const bf16x8 o = load_frag_global(out + ((int64_t)b * N + q) * ldo + hd * D, ks, lane, qv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum = fmaf((float)o[j], (float)gf[ks][j], dsum);
   }
-  // this lane's query's row constants -L2 and -delta in f32: the fragment rows' three bf16 parts summed
-  // (exact: split3 leaves 8 + 8 + 8 significant bits); zero for a query past the end (p = 1, dS = 0)
+  // this lane's query's row constants -L2 = -lse log2 e and -delta in f32 (the prep pass's job, done here:
+  // this kernel runs before dK/dV and leaves their fragment rows, three bf16 parts each, for it);
+  // zero for a query past the end (p = 1, dS = 0)
   float nl = 0.f, nd = 0.f;
   {
-    const bf16* fr = frag + ((int64_t)bh * 2 * N + (qv ? q : 0)) * 8;
-    const bf16x8 lf = row_frag(fr), dlf = row_frag(fr + (int64_t)N * 8);
+    dsum += __shfl_xor(dsum, 32, 64);
     if (qv) {
-      nl = ((float)lf[0] + (float)lf[1]) + (float)lf[2];
-      nd = ((float)dlf[0] + (float)dlf[1]) + (float)dlf[2];
+      nl = -lse[(int64_t)bh * N + q] * LOG2E;
+      nd = -dsum;
+      if (lane < 32) {
+        bf16x8 f0, f1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { f0[j] = (bf16)0.f; f1[j] = (bf16)0.f; }
+        split3(nl, f0);
+        split3(nd, f1);
+        *reinterpret_cast<bf16x8*>(frag + ((int64_t)bh * 2 * N + q) * 8) = f0;
+        *reinterpret_cast<bf16x8*>(frag + ((int64_t)(bh * 2 + 1) * N + q) * 8) = f1;
+      }
     }
   }
   settle(qf);
@@ -1404,11 +1418,16 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
   bf16* qs = (bf16*)work;
   bf16* frag = qs + rows * D;
   const float scale_log2 = scale * LOG2E;
-  attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
-                                                                     (const bf16*)dout, lse, qs, frag, B, N, H,
-                                                                     scale_log2, q_ready ? 0 : 1);
-  MIA_LAUNCH_CHECK("attn_bwd_prep");
-  if (fused && fb_ok(N)) {
+  const bool one_pass = fused && fb_ok(N);
+  // the prep pass: Q' when the forward did not leave it, the row-constant fragments for the one-pass
+  // form (the two-kernel form's dQ kernel computes its own and writes them for dK/dV)
+  if (!q_ready || one_pass) {
+    attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
+                                                                       (const bf16*)dout, lse, qs, frag, B, N, H,
+                                                                       scale_log2, q_ready ? 0 : 1);
+    MIA_LAUNCH_CHECK("attn_bwd_prep");
+  }
+  if (one_pass) {
     const int nkb = (int)cdiv(N, FB_K);
     MIA_CHECK_ARG((int64_t)nkb * B * H < (1ll << 31) && (int64_t)cdiv(N, 64) * FB_TILE < (1ll << 31),
                   "attn_bwd: grid too large");
@@ -1425,12 +1444,12 @@ static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, con
     return 0;
   }
   const int nkb = (int)cdiv(N, BWD_K), nqb = (int)cdiv(N, BWD_Q);
+  attn_bwd_dq_kernel<<<(unsigned)(nqb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout,
+                                                             lse, frag, (bf16*)dqkv, N, H, nqb, scale, scale_log2);
+  MIA_LAUNCH_CHECK("attn_bwd_dq");
   attn_bwd_dkdv_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag,
                                                                (bf16*)dqkv, N, H, nkb, 1.f / LOG2E);
   MIA_LAUNCH_CHECK("attn_bwd_dkdv");
-  attn_bwd_dq_kernel<<<(unsigned)(nqb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, frag, (bf16*)dqkv,
-                                                             N, H, nqb, scale, scale_log2);
-  MIA_LAUNCH_CHECK("attn_bwd_dq");
   return 0;
 }
 
