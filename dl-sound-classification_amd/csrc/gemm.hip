@@ -2176,7 +2176,14 @@ extern "C" int64_t mia_gemm_workspace_bytes_ex(const MiaOperand* A, const MiaOpe
                                                int64_t M, int64_t N, int64_t K, int32_t compute_dtype,
                                                int32_t split_k) {
   if (!A || !B || !E) return 0;
-  if (mgemm::mg_ok(*A, *B, *E, M, N, K, compute_dtype)) return mgemm::mg_workspace_bytes(M, N, K, E->colsum != nullptr);
+  if (mgemm::mg_ok(*A, *B, *E, M, N, K, compute_dtype))
+    return mgemm::mg_workspace_bytes(M, N, K, E->colsum != nullptr, E->a_colsum != nullptr);
+  if (E->a_colsum) {  // the GEMM's own workspace, then the column-sum pass over A
+    MiaEpilogue e = *E;
+    e.a_colsum = nullptr;
+    return cdiv(mia_gemm_workspace_bytes_ex(A, B, &e, M, N, K, compute_dtype, split_k), 256) * 256 +
+           (int64_t)MIA_COLSUM_MAXBLK * M * 4;
+  }
   int64_t b = mia_gemm_workspace_bytes(M, N, split_k);
   if (E->colsum) b = colsum_ws_offset(M, N, split_k) + (int64_t)MIA_COLSUM_MAXBLK * N * 4;
   return b;
@@ -2190,6 +2197,19 @@ extern "C" int mia_gemm(const MiaOperand* A, const MiaOperand* B, const MiaEpilo
     return mgemm::mg_run(*A, *B, *E, M, N, K, workspace, as_stream(stream));
   MIA_CHECK_ARG(!E->mx_q, "gemm: an MX-fp8 output copy needs the 256x256 kernel (bf16 dense operands, "
                 "plain / GELU / GELU_SAVE bf16 output, ldc == N, N %% 32 == 0)");
+  if (E->a_colsum) {  // other paths: the GEMM, then a column-sum pass over the k-by-m A
+    MIA_CHECK_ARG(A->kind == MIA_OP_DENSE && A->layout == MIA_LAYOUT_RC && A->pre == MIA_PRE_NONE &&
+                      (A->dtype == MIA_BF16 || A->dtype == MIA_F32) && A->rows >= K && A->cols == M,
+                  "gemm: a_colsum needs a dense k-by-m (RC) A without pre-op");
+    MIA_CHECK_ARG(workspace || M == 0 || K == 0, "gemm a_colsum: needs the workspace of mia_gemm_workspace_bytes_ex");
+    MiaEpilogue e = *E;
+    e.a_colsum = nullptr;
+    if (int r = mia_gemm(A, B, &e, M, N, K, compute_dtype, split_k, workspace, stream)) return r;
+    if (M == 0) return 0;
+    void* ws = static_cast<char*>(workspace) +
+               cdiv(mia_gemm_workspace_bytes_ex(A, B, &e, M, N, K, compute_dtype, split_k), 256) * 256;
+    return mia_colsum(A->ptr, A->dtype, K, (int32_t)M, A->ld, E->a_colsum, ws, stream);
+  }
   if (E->colsum) {
     MIA_CHECK_ARG(!E->sqsum && !E->accumulate && !E->rm_inner && E->ldc >= N &&
                       (E->dtype == MIA_BF16 || E->dtype == MIA_F32),

@@ -192,7 +192,7 @@ hipError_t wgrad8_launch(const W8Args& a, hipStream_t s);
 bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
            int compute);
 int mg_split(int64_t M, int64_t N, int64_t K);
-int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum);
+int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum, int a_colsum = 0);
 int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64_t M, int64_t N, int64_t K,
            void* workspace, hipStream_t s);
 

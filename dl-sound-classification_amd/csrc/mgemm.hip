@@ -50,6 +50,7 @@ struct MArgs {
   int64_t ldaux;
   float* ws;          // EPI_SLAB: [split][M][N] f32
   float* colsum_part; // EPI_DGELU with colsum: [nbm][N] f32
+  float* acs_part;    // A-operand column sums (RC A only): [split][M] f32, written by the bn == 0 tiles
   uint8_t* mxq;       // optional MX-fp8 copy of a bf16 output: e4m3 [M][N] (row stride N) ...
   uint8_t* mxs;       // ... and its scales [M][N / 32]
 };
@@ -371,7 +372,19 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
   }
 }
 
-template <int LA, int LB, int EPI>
+// sum of the 8 bf16 of a fragment added to c (v_dot2_f32_bf16 against ones: exact products, f32 adds)
+__device__ __forceinline__ float frag_sum(bf16x8 f, float c) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 one2 = {(__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_fdot2_f32_bf16(bf2{f[2 * j], f[2 * j + 1]}, one2, c, false);
+  return c;
+}
+
+// ACS (RC A operand, the split-K weight gradients): also the column sums over k of A -- the bias gradient of
+// the linear -- from the K-tiles in LDS: wave (wr, wc) sums rows 16 wc .. 16 wc + 15 and 64 + 16 wc .. of its
+// 128-row half (the four wc waves read the same A rows), two extra transposed fragment reads per k-step
+template <int LA, int LB, int EPI, bool ACS = false>
 __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
   __shared__ __attribute__((aligned(1024))) char smem[MG_LDS];
   const int lane = threadIdx.x & 63;
@@ -424,6 +437,7 @@ __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
   const int bhalf = wc >> 1;  // B half-tile holding this wave's 64 columns, at column 64 * (wc & 1)
   const int bcol = 64 * (wc & 1);
   bf16x8 af[2][4], bfr[2][4];
+  float acs0 = 0.f, acs1 = 0.f;  // ACS: this lane's partial column sums (8 k of rows 16 wc + (lane & 15), +64)
   for (int t = 0; t < nk; ++t) {
     const char* cur = (t & 1) ? st1 : st0;
     const char* ah = cur + wr * MG_HALF;  // the wave's 128 rows are A half-tile wr
@@ -435,6 +449,13 @@ __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
       for (int i = 0; i < 4; ++i) af[ks][i] = frag<LA>(ah, 16 * i, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[ks][j] = frag<LB>(bh, bcol + 16 * j, ks, lane);
+    }
+    if constexpr (ACS) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        acs0 = frag_sum(frag<LA>(ah, 16 * wc, ks, lane), acs0);
+        acs1 = frag_sum(frag<LA>(ah, 64 + 16 * wc, ks, lane), acs1);
+      }
     }
     if (t + 1 < nk) {  // K-tile t+1's A -> the other stage (its previous contents, K-tile t-1, are read)
       la.issue((t & 1) ? st0 : st1, t + 1, wave);
@@ -483,6 +504,18 @@ __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two halves
+  if constexpr (ACS) {
+    // the four lane groups (lane >> 4) hold different k of the same rows: fixed-order butterfly
+    acs0 += __shfl_xor(acs0, 16, 64);
+    acs0 += __shfl_xor(acs0, 32, 64);
+    acs1 += __shfl_xor(acs1, 16, 64);
+    acs1 += __shfl_xor(acs1, 32, 64);
+    if (bn == 0 && lane < 16) {
+      const int64_t m = m0 + wr * 128 + 16 * wc + lane;
+      if (m < g.M) g.acs_part[(int64_t)z * g.M + m] = acs0;
+      if (m + 64 < g.M) g.acs_part[(int64_t)z * g.M + m + 64] = acs1;
+    }
+  }
   mg_epilogue<EPI>(g, acc, smem, wave, lane, bm, z, m0, n0);
 }
 
@@ -513,6 +546,10 @@ template __global__ void mgemm_kernel<1, 1, 2>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 3>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 4>(MArgs);
 template __global__ void mgemm_kernel<1, 1, 5>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 5, true>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 5, true>(MArgs);
+template __global__ void mgemm_kernel<1, 1, 0, true>(MArgs);
+template __global__ void mgemm_kernel<1, 0, 0, true>(MArgs);
 
 // ---------------------------------------------------------------- MX-fp8 (OCP e4m3fn, E8M0 per 32 K)
 // Forward block linears under trainer.precision=fp8-mixed (north_star config 5; the reference has no fp8
@@ -715,6 +752,16 @@ __global__ __launch_bounds__(256) void mg_splitk_reduce_kernel(const float* __re
   }
 }
 
+// A-operand column sums: the split-K partials in slice order (deterministic)
+__global__ __launch_bounds__(256) void mg_acs_reduce_kernel(const float* __restrict__ part, int split, int64_t M,
+                                                            float* __restrict__ out) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float acc = 0.f;
+  for (int z = 0; z < split; ++z) acc += part[(int64_t)z * M + m];
+  out[m] = acc;
+}
+
 __global__ __launch_bounds__(256) void mg_colsum_final_kernel(const double* __restrict__ part2, int N, float* out) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < N) out[c] = (float)colsum_slices(part2, N, c);
@@ -723,6 +770,13 @@ __global__ __launch_bounds__(256) void mg_colsum_final_kernel(const double* __re
 template <int LA, int LB>
 hipError_t launch_epi(const MArgs& a, int epi, hipStream_t s) {
   const unsigned grid = (unsigned)((int64_t)a.nbm * a.nbn * a.split);
+  if constexpr (LA == MG_RC) {
+    if (a.acs_part) {  // A-operand column sums: split-K slabs or an unsplit f32 output
+      if (epi == EPI_SLAB) mgemm_kernel<LA, LB, EPI_SLAB, true><<<grid, MG_NT, 0, s>>>(a);
+      else mgemm_kernel<LA, LB, EPI_PLAIN, true><<<grid, MG_NT, 0, s>>>(a);
+      return hipGetLastError();
+    }
+  }
   switch (epi) {
     case EPI_PLAIN: mgemm_kernel<LA, LB, EPI_PLAIN><<<grid, MG_NT, 0, s>>>(a); break;
     case EPI_GELU: mgemm_kernel<LA, LB, EPI_GELU><<<grid, MG_NT, 0, s>>>(a); break;
@@ -778,6 +832,8 @@ bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   if (B.layout == MIA_LAYOUT_KC) { if (B.rows != N || B.cols < K || K % MG_BK) return false; }
   else if (B.rows < K || B.cols != N || N % 8) return false;
   if (cdiv(M, MG_BM) * cdiv(N, MG_BN) >= (1ll << 24)) return false;
+  // A-operand column sums: a k-by-m A and a plain output (the weight gradients)
+  if (E.a_colsum && (A.layout != MIA_LAYOUT_RC || mg_epi_kind(E, N) != EPI_PLAIN)) return false;
   return mg_epi_kind(E, N) >= 0;
 }
 
@@ -798,13 +854,14 @@ static void mg_geometry(int64_t M, int64_t N, int64_t K, int& split, int64_t& kp
   split = (int)cdiv(K, kper);
 }
 
-int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum) {
+int64_t mg_workspace_bytes(int64_t M, int64_t N, int64_t K, int colsum, int a_colsum) {
   int split;
   int64_t kper;
   mg_geometry(M, N, K, split, kper);
   int64_t b = split > 1 ? (int64_t)split * M * N * 4 : 0;
   b = cdiv(b, 256) * 256;
   if (colsum) b += cdiv(cdiv(M, MG_BM) * N * 4, 256) * 256 + colsum_part2_bytes((int)N);
+  if (a_colsum) b += cdiv((int64_t)split * M * 4, 256) * 256;
   return b;
 }
 
@@ -821,7 +878,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   a.out = E.ptr; a.ldc = E.ldc; a.out_f32 = E.dtype == MIA_F32;
   a.bias = E.bias; a.aux = E.aux; a.ldaux = E.ldaux;
   a.mxq = reinterpret_cast<uint8_t*>(E.mx_q); a.mxs = reinterpret_cast<uint8_t*>(E.mx_scales);
-  const int need_ws = a.split > 1 || E.colsum;
+  const int need_ws = a.split > 1 || E.colsum || E.a_colsum;
   MIA_CHECK_ARG(!need_ws || workspace, "gemm: the 256x128 path needs the workspace of mia_gemm_workspace_bytes_ex");
   char* ws = reinterpret_cast<char*>(workspace);
   int kind = epi;
@@ -836,6 +893,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
     a.colsum_part = reinterpret_cast<float*>(ws);
     ws += cdiv((int64_t)a.nbm * N * 4, 256) * 256;
   }
+  if (E.a_colsum) a.acs_part = reinterpret_cast<float*>(ws);  // after the slabs (plain epilogue: no colsum)
   hipError_t err;
   const int la = A.layout, lb = B.layout;
   if (la == MIA_LAYOUT_KC && lb == MIA_LAYOUT_KC) err = launch_epi<MG_KC, MG_KC>(a, kind, s);
@@ -848,6 +906,10 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
     const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
     mg_splitk_reduce_kernel<<<blocks, 256, 0, s>>>(a.ws, a.split, M, N, E.ptr, E.ldc, E.dtype == MIA_F32, E.bias);
     MIA_LAUNCH_CHECK("mgemm splitk reduce");
+  }
+  if (E.a_colsum) {
+    mg_acs_reduce_kernel<<<(unsigned)cdiv(M, 256), 256, 0, s>>>(a.acs_part, a.split, M, E.a_colsum);
+    MIA_LAUNCH_CHECK("mgemm a_colsum");
   }
   if (E.colsum && kind == EPI_DGELU) {
     double* part2 = reinterpret_cast<double*>(ws);

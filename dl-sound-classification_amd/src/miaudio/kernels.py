@@ -65,12 +65,13 @@ def conv(t: torch.Tensor, layout: int, n, h, w, c, oh, ow, kh, kw, sh=1, sw=1, p
 
 def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=None, ldaux: int = 0,
              accumulate: bool = False, alpha: float = 1.0, act_scale: float = 1.0,
-             rowmap=None, sqsum=None, colsum=None, mx=None) -> L.MiaEpilogue:
+             rowmap=None, sqsum=None, colsum=None, mx=None, a_colsum=None) -> L.MiaEpilogue:
     """Output descriptor of a GEMM.  ``sqsum``: optional f64 tensor of ``mia_gemm_sqsum_slots(M, N)``
     entries that receives the per-tile sums of squares of a plain f32 output (see ``sqsum_slots``).
     ``colsum``: optional f32 (N,) tensor receiving the column sums of the stored output (the bias
     gradient of the linear whose dy this output is).  ``mx``: optional MXTensor (mx_empty) receiving an
-    MX-fp8 copy of a bf16 output (256x256 kernels only)."""
+    MX-fp8 copy of a bf16 output (256x256 kernels only).  ``a_colsum``: optional f32 (M,) tensor receiving
+    the column sums over k of a k-by-m (RC) A operand -- the bias gradient of a weight-gradient GEMM's dy."""
     e = L.MiaEpilogue()
     e.ptr = out.data_ptr()
     e.dtype = L.dtype_code(out)
@@ -90,7 +91,8 @@ def epilogue(out: torch.Tensor, ldc: int, act: int = L.ACT_NONE, bias=None, aux=
     e.colsum = L.ptr(colsum)
     if mx is not None:  # MXTensor receiving the MX-fp8 copy of the bf16 output
         e.mx_q, e.mx_scales = mx.q.data_ptr(), mx.scales.data_ptr()
-    e._keep = (out, bias, aux, sqsum, colsum, mx)
+    e.a_colsum = L.ptr(a_colsum)
+    e._keep = (out, bias, aux, sqsum, colsum, mx, a_colsum)
     return e
 
 

@@ -44,7 +44,7 @@ class MiaEpilogue(C.Structure):
                 ("ldc", i64), ("rm_inner", i64), ("rm_outer", i64), ("rm_istride", i64),
                 ("rm_offset", i64), ("bias", vp), ("aux", vp), ("ldaux", i64),
                 ("alpha", f32), ("act_scale", f32), ("sqsum", vp), ("colsum", vp), ("mx_q", vp),
-                ("mx_scales", vp)]
+                ("mx_scales", vp), ("a_colsum", vp)]
 
 
 class MiaMelCfg(C.Structure):

@@ -81,10 +81,11 @@ def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.
     if cd == L.BF16 and dy.dtype == torch.float32:
         dy = K.cast(dy, torch.bfloat16)  # bf16 GEMM operands (f32 accumulation inside)
     dW = torch.empty(Nf, Kf, dtype=torch.float32, device=dy.device)
-    K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf), Nf, Kf, M, cd,
-           tag=tag + ".wgrad")
-    if db is None:
-        db = K.colsum(dy, M, Nf)
+    a_cs = None
+    if db is None:  # the weight-gradient GEMM sums dy's columns from the A tiles it reads
+        db = a_cs = torch.empty(Nf, dtype=torch.float32, device=dy.device)
+    K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf, a_colsum=a_cs),
+           Nf, Kf, M, cd, tag=tag + ".wgrad")
     if dx_out is not None:
         K.gemm(K.dense(dy, L.KC, M, Nf), K.dense(W, L.RC, Nf, Kf),
                K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf,

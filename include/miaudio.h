@@ -89,6 +89,11 @@ typedef struct MiaEpilogue {
    * kernels (path 7, mia_gemm_mxfp8) with a plain / GELU / GELU_SAVE bf16 output, ldc == N, N % 32 == 0. */
   void* mx_q;
   void* mx_scales;
+  /* Optional (NULL = off): a_colsum[m] = sum over k of a k-by-m (MIA_LAYOUT_RC) dense A operand -- the bias
+   * gradient of the linear whose weight gradient dW = dy^T x this GEMM is (A = dy), summed inside the
+   * 256x256 kernel's main loop from the A fragments it already reads (split-K partials reduced in a fixed
+   * order); any other path gets a column-sum pass over A.  Needs the workspace of mia_gemm_workspace_bytes_ex. */
+  float* a_colsum;
 } MiaEpilogue;
 
 /* Implicit-GEMM on MFMA (bf16: v_mfma_f32_32x32x16_bf16 / 16x16x32; f32: v_mfma_f32_32x32x2_f32).

@@ -542,6 +542,32 @@ def test_mgemm_wgrad_split_k(cuda, odt, M, N, Kd):
     assert rel(out.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("lb", [L.RC, L.KC])
+@pytest.mark.parametrize("M,N,Kd", [(2304, 768, 16384 + 40), (768 + 8, 768, 421120 // 8), (520, 264, 300)])
+def test_gemm_a_colsum(cuda, lb, M, N, Kd):
+    """MiaEpilogue.a_colsum (the bias gradient of a weight-gradient GEMM dW = dy^T x, A = dy k-by-m):
+    summed inside the 256x256 kernel from the A tiles (split-K partials in slice order; M not a multiple
+    of the tile, a K tail that is not a multiple of 64) and, on the other paths (a small shape), a
+    column-sum pass over A -- vs float64 sums of A, the GEMM output unchanged, bit-identical per call."""
+    if lb == L.KC:
+        Kd -= Kd % 64  # a k-contiguous B takes whole 64-k tiles
+    a, b, A, Bo, g = _big_operands(cuda, L.RC, lb, M, N, Kd, 23)
+    big = M >= 768
+    assert (L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1) == 7) == big
+    out = torch.empty(M, N, dtype=torch.float32, device=cuda)
+    ref_out = torch.empty_like(out)
+    K.gemm(A, Bo, K.epilogue(ref_out, N), M, N, Kd, L.BF16)
+    res = []
+    for _ in range(2):
+        cs = torch.full((M,), float("nan"), device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, a_colsum=cs), M, N, Kd, L.BF16)
+        torch.cuda.synchronize()
+        res.append(cs)
+    assert torch.equal(out, ref_out)
+    assert torch.equal(res[0], res[1])
+    assert rel(res[0], a.double().sum(1)) < 1e-5
+
+
 @pytest.mark.parametrize("case", ["dact_gelu", "plain"])
 def test_mgemm_output_colsum(cuda, case):
     """MiaEpilogue.colsum on both routes: fused into the 256x256 kernel's dGELU epilogue (AST fc1 bias
