@@ -1691,7 +1691,8 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   }
   // the same full-tile staging for a bf16 output with optional bias / ReLU (AST qkv forward and the
   // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
-  const bool save = g.e.act == MIA_ACT_GELU_SAVE;
+  const bool save = g.e.act == MIA_ACT_GELU_SAVE || g.e.act == MIA_ACT_GELU_SAVE_D;
+  const bool save_d = g.e.act == MIA_ACT_GELU_SAVE_D;
   const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
                        (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU || g.e.act == MIA_ACT_GELU ||
                         (save && g.e.aux_dtype == MIA_BF16 && (g.e.ldaux & 7) == 0 &&
@@ -1736,9 +1737,13 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 #pragma unroll
       for (int c = 0; c < 8; ++c) v[c] += bv[c];
-      if (save)  // GELU_SAVE: the pre-activation goes to aux (MLP fc1, read back by the backward)
+      if (save) {  // GELU_SAVE(_D): the pre-activation or gelu' goes to aux (MLP fc1, read by the backward)
+        float d[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) d[c] = save_d ? gelu_erf_grad((float)(bf16)v[c]) : v[c];  // gelu' of bf16 u
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(const_cast<char*>(g.e.aux)) + (m0 + row) * g.e.ldaux +
-                                  n0 + col) = pack(v);
+                                  n0 + col) = pack(d);
+      }
 #pragma unroll
       for (int c = 0; c < 8; ++c) v[c] = relu ? fmaxf(v[c], 0.f) : (gelu ? gelu_erf(v[c]) : v[c]);
       *reinterpret_cast<uint4*>(out + (m0 + row) * g.e.ldc + n0 + col) = pack(v);
@@ -1972,7 +1977,8 @@ static int gemm_tile(const MiaOperand* A, const MiaOperand* B, const MiaEpilogue
   if (int r = check_operand(*B, "B")) return r;
   MIA_CHECK_ARG(E->ptr != nullptr, "gemm: output is null");
   MIA_CHECK_ARG(compute_dtype == MIA_F32 || compute_dtype == MIA_BF16, "gemm: compute dtype");
-  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU || E->act == MIA_ACT_ADD_AUX || E->act == MIA_ACT_GELU_SAVE)
+  if (E->act == MIA_DACT_NZ || E->act == MIA_DACT_GELU || E->act == MIA_ACT_ADD_AUX || E->act == MIA_ACT_GELU_SAVE ||
+      E->act == MIA_ACT_GELU_SAVE_D || E->act == MIA_DACT_MUL)
     MIA_CHECK_ARG(E->aux != nullptr, "gemm: this epilogue needs aux");
   if (split_k < 1) split_k = 1;
   if (split_k > 1) MIA_CHECK_ARG(workspace != nullptr, "gemm: split_k needs workspace");

@@ -62,6 +62,11 @@ static __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int
       st_elem(const_cast<char*>(e.aux), e.aux_dtype, m * e.ldaux + n, v);
       v = gelu_erf(v);
       break;
+    case MIA_ACT_GELU_SAVE_D:
+      st_elem(const_cast<char*>(e.aux), e.aux_dtype, m * e.ldaux + n, gelu_erf_grad(v));
+      v = gelu_erf(v);
+      break;
+    case MIA_DACT_MUL: v *= ld_elem(e.aux, e.aux_dtype, m * e.ldaux + n); break;
     default: break;
   }
   int64_t prow = m;
@@ -120,7 +125,7 @@ static __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, i
   if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
   const int64_t idx = prow * e.ldc + n0;
   const bool uses_aux = e.act == MIA_DACT_NZ || e.act == MIA_DACT_GELU || e.act == MIA_ACT_ADD_AUX ||
-                        e.act == MIA_ACT_GELU_SAVE;
+                        e.act == MIA_ACT_GELU_SAVE || e.act == MIA_ACT_GELU_SAVE_D || e.act == MIA_DACT_MUL;
   const int64_t aidx = m * e.ldaux + n0;
   const bool fast = n0 + 16 <= N && !e.accumulate &&
                     ((idx * (e.dtype == MIA_BF16 ? 2 : 4)) & 15) == 0 &&
@@ -156,6 +161,13 @@ static __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, i
     st16(const_cast<char*>(e.aux), e.aux_dtype, aidx, o);
 #pragma unroll
     for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
+  } else if (e.act == MIA_ACT_GELU_SAVE_D) {
+    float d[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) d[c] = gelu_erf_grad(o[c]);
+    st16(const_cast<char*>(e.aux), e.aux_dtype, aidx, d);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) o[c] = gelu_erf(o[c]);
   } else if (uses_aux) {
     float a[16];
     ld16(e.aux, e.aux_dtype, aidx, a);
@@ -165,6 +177,9 @@ static __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, i
     } else if (e.act == MIA_DACT_GELU) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) o[c] *= gelu_erf_grad(a[c]);
+    } else if (e.act == MIA_DACT_MUL) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) o[c] *= a[c];
     } else {
 #pragma unroll
       for (int c = 0; c < 16; ++c) o[c] += a[c];

@@ -32,7 +32,8 @@ constexpr int MG_STAGE = 4 * MG_HALF;          // A0 A1 B0 B1
 constexpr int MG_LDS = 2 * MG_STAGE;
 
 enum { MG_KC = MIA_LAYOUT_KC, MG_RC = MIA_LAYOUT_RC };
-enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_GELU_SAVE = 2, EPI_ADD_AUX = 3, EPI_DGELU = 4, EPI_SLAB = 5 };
+enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_GELU_SAVE = 2, EPI_ADD_AUX = 3, EPI_DGELU = 4, EPI_SLAB = 5, EPI_GELU_SAVE_D = 6,
+       EPI_DMUL = 7 };
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_vp;
@@ -220,10 +221,36 @@ __device__ __forceinline__ f2 gelu_grad2(f2 x) {
   const f2 c = {x.x >= 0.f ? 1.f - he.x : he.x, x.y >= 0.f ? 1.f - he.y : he.y};  // Phi(x)
   return pfma(x * 0.39894228040143268f, e, c);
 }
+// gelu(x) of a pair and, into d, gelu'(x) = Phi(x) + x phi(x), both from gelu_grad2's Abramowitz-Stegun
+// erfc, whose exp(-x^2 / 2) is phi's: one reciprocal and one exp per element for the pair of outputs
+// (|error| <= 7.5e-8 absolute in Phi: relative to gelu(x) that is < 1e-4 for x > -3.4, where gelu
+// has |values| > 1e-3; the erfc form above keeps the tails relative for the GELU-only epilogues)
+__device__ __forceinline__ f2 gelu_and_grad2(f2 x, f2& d) {
+  const f2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f2 dd = pfma(z, f2{0.3275911f, 0.3275911f}, f2{1.f, 1.f});
+  const f2 t = {__builtin_amdgcn_rcpf(dd.x), __builtin_amdgcn_rcpf(dd.y)};
+  f2 p = f2{0.5f * 1.061405429f, 0.5f * 1.061405429f};
+  p = pfma(p, t, f2{0.5f * -1.453152027f, 0.5f * -1.453152027f});
+  p = pfma(p, t, f2{0.5f * 1.421413741f, 0.5f * 1.421413741f});
+  p = pfma(p, t, f2{0.5f * -0.284496736f, 0.5f * -0.284496736f});
+  p = pfma(p, t, f2{0.5f * 0.254829592f, 0.5f * 0.254829592f});
+  const f2 a = -(z * z) * L2E;
+  const f2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};  // exp(-x^2 / 2)
+  const f2 he = p * t * e;                                                  // 0.5 erfc(|x| / sqrt 2)
+  const f2 c = {x.x >= 0.f ? 1.f - he.x : he.x, x.y >= 0.f ? 1.f - he.y : he.y};  // Phi(x)
+  d = pfma(x * 0.39894228040143268f, e, c);
+  return x * c;
+}
 // v * gelu'(u) / gelu(v) on 4 values in place
 __device__ __forceinline__ void gelu4(f32x4& v) {
   const f2 a = gelu2(f2{v[0], v[1]}), b = gelu2(f2{v[2], v[3]});
   v = f32x4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ void gelu_d4(f32x4& v, f32x4& d) {
+  f2 da, db;
+  const f2 a = gelu_and_grad2(f2{v[0], v[1]}, da), b = gelu_and_grad2(f2{v[2], v[3]}, db);
+  v = f32x4{a.x, a.y, b.x, b.y};
+  d = f32x4{da.x, da.y, db.x, db.y};
 }
 __device__ __forceinline__ void dgelu4(f32x4& v, f32x4 u) {
   const f2 a = gelu_grad2(f2{u[0], u[1]}), b = gelu_grad2(f2{u[2], u[3]});
@@ -253,12 +280,14 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
-    if (EPI != EPI_SLAB && EPI != EPI_DGELU && g.bias && n < g.N)
+    if (EPI != EPI_SLAB && EPI != EPI_DGELU && EPI != EPI_DMUL && g.bias && n < g.N)
       bias4[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
     else
       bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bool bf_out = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU || (EPI == EPI_PLAIN && !g.out_f32);
+  constexpr bool DG = EPI == EPI_DGELU || EPI == EPI_DMUL;  // backward epilogues (aux read, column sums)
+  const bool bf_out = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_GELU_SAVE_D || DG ||
+                      (EPI == EPI_PLAIN && !g.out_f32);
   if (!bf_out) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -309,21 +338,32 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
       if constexpr (EPI == EPI_GELU_SAVE) {
         if (ok) mg_st16(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n, q);
       }
-      if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
+      if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_GELU_SAVE_D || DG) {
         f32x4 v0 = unpack4(make_uint2(q.x, q.y)), v1 = unpack4(make_uint2(q.z, q.w));
-        if constexpr (EPI == EPI_DGELU) {
+        if constexpr (DG) {
           const uint4 u = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)
                              : make_uint4(0, 0, 0, 0);
           const f32x4 u0 = unpack4(make_uint2(u.x, u.y)), u1 = unpack4(make_uint2(u.z, u.w));
-          dgelu4(v0, u0);
-          dgelu4(v1, u1);
+          if constexpr (EPI == EPI_DGELU) {
+            dgelu4(v0, u0);
+            dgelu4(v1, u1);
+          } else {  // the saved gelu'(u)
+            v0 *= u0;
+            v1 *= u1;
+          }
+        } else if constexpr (EPI == EPI_GELU_SAVE_D) {
+          f32x4 d0, d1;
+          gelu_d4(v0, d0);
+          gelu_d4(v1, d1);
+          const uint2 e0 = pack4(d0), e1 = pack4(d1);
+          if (ok) mg_st16(reinterpret_cast<bf16*>(const_cast<void*>(g.aux)) + m * g.ldaux + n, make_uint4(e0.x, e0.y, e1.x, e1.y));
         } else {
           gelu4(v0);
           gelu4(v1);
         }
         const uint2 p0 = pack4(v0), p1 = pack4(v1);
         o = make_uint4(p0.x, p0.y, p1.x, p1.y);
-        if constexpr (EPI == EPI_DGELU) {
+        if constexpr (DG) {
           if (ok) {
             const f32x4 w0 = unpack4(p0), w1 = unpack4(p1);
 #pragma unroll
@@ -331,7 +371,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
           }
         }
       }
-      if constexpr (EPI != EPI_DGELU) {
+      if constexpr (!DG) {
         if (g.mxq) {  // MX-fp8 copy of the stored bf16 values (the next MX GEMM's A operand)
           const f32x4 w0 = unpack4(make_uint2(o.x, o.y)), w1 = unpack4(make_uint2(o.z, o.w));
           const float v8[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
@@ -345,7 +385,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
       }
       if (ok) mg_st16(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n, o);
     }
-    if constexpr (EPI == EPI_DGELU) {
+    if constexpr (DG) {
       if (g.colsum_part) {
         // column sums of the stored values: lanes with equal (lane & 7) hold the same 8 columns
 #pragma unroll
@@ -783,6 +823,8 @@ hipError_t launch_epi(const MArgs& a, int epi, hipStream_t s) {
     case EPI_GELU_SAVE: mgemm_kernel<LA, LB, EPI_GELU_SAVE><<<grid, MG_NT, 0, s>>>(a); break;
     case EPI_ADD_AUX: mgemm_kernel<LA, LB, EPI_ADD_AUX><<<grid, MG_NT, 0, s>>>(a); break;
     case EPI_DGELU: mgemm_kernel<LA, LB, EPI_DGELU><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_GELU_SAVE_D: mgemm_kernel<LA, LB, EPI_GELU_SAVE_D><<<grid, MG_NT, 0, s>>>(a); break;
+    case EPI_DMUL: mgemm_kernel<LA, LB, EPI_DMUL><<<grid, MG_NT, 0, s>>>(a); break;
     default: mgemm_kernel<LA, LB, EPI_SLAB><<<grid, MG_NT, 0, s>>>(a); break;
   }
   return hipGetLastError();
@@ -798,7 +840,8 @@ namespace mgemm {
 int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
   if (E.accumulate || E.rm_inner || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
   if (E.mx_q && (!E.mx_scales || E.dtype != MIA_BF16 || E.ldc != N || N % 32 || E.colsum ||
-                 !(E.act == MIA_ACT_NONE || E.act == MIA_ACT_GELU || E.act == MIA_ACT_GELU_SAVE)))
+                 !(E.act == MIA_ACT_NONE || E.act == MIA_ACT_GELU || E.act == MIA_ACT_GELU_SAVE ||
+                   E.act == MIA_ACT_GELU_SAVE_D)))
     return -1;
   const bool bf = E.dtype == MIA_BF16, f32 = E.dtype == MIA_F32;
   if ((E.ldc & 3) || E.ldc < N || (reinterpret_cast<uintptr_t>(E.ptr) & (bf ? 7 : 15)) != 0) return -1;
@@ -812,6 +855,8 @@ int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
     case MIA_ACT_GELU_SAVE: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.colsum ? EPI_GELU_SAVE : -1;
     case MIA_ACT_ADD_AUX: return f32 && aux_ok && E.aux_dtype == MIA_F32 && !E.colsum ? EPI_ADD_AUX : -1;
     case MIA_DACT_GELU: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.bias ? EPI_DGELU : -1;
+    case MIA_ACT_GELU_SAVE_D: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.colsum ? EPI_GELU_SAVE_D : -1;
+    case MIA_DACT_MUL: return bf && aux_ok && E.aux_dtype == MIA_BF16 && !E.bias ? EPI_DMUL : -1;
     default: return -1;
   }
 }
@@ -911,7 +956,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
     mg_acs_reduce_kernel<<<(unsigned)cdiv(M, 256), 256, 0, s>>>(a.acs_part, a.split, M, E.a_colsum);
     MIA_LAUNCH_CHECK("mgemm a_colsum");
   }
-  if (E.colsum && kind == EPI_DGELU) {
+  if (E.colsum && (kind == EPI_DGELU || kind == EPI_DMUL)) {
     double* part2 = reinterpret_cast<double*>(ws);
     colsum_pass1(a.colsum_part, a.nbm, (int)N, N, part2, s);
     mg_colsum_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, s>>>(part2, (int)N, E.colsum);
@@ -955,8 +1000,8 @@ extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, 
   MIA_CHECK_ARG(N % 4 == 0 && (E->dtype != MIA_BF16 || N % 8 == 0) && cdiv(M, MG_BM) * cdiv(N, MG_BN) < (1ll << 24),
                 "gemm_mxfp8: N must be a multiple of 4 (of 8 for a bf16 output)");
   const int epi = mgemm::mg_epi_kind(*E, N);
-  MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_ADD_AUX,
-                "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE / f32 residual (row-major, aligned)");
+  MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_GELU_SAVE_D || epi == EPI_ADD_AUX,
+                "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE(_D) / f32 residual (row-major, aligned)");
   MArgs g;
   memset(&g, 0, sizeof(g));
   g.a = reinterpret_cast<const bf16*>(a);
@@ -974,6 +1019,7 @@ extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, 
     case EPI_PLAIN: mxgemm_kernel<EPI_PLAIN><<<grid, MG_NT, 0, s>>>(g, x); break;
     case EPI_GELU: mxgemm_kernel<EPI_GELU><<<grid, MG_NT, 0, s>>>(g, x); break;
     case EPI_GELU_SAVE: mxgemm_kernel<EPI_GELU_SAVE><<<grid, MG_NT, 0, s>>>(g, x); break;
+    case EPI_GELU_SAVE_D: mxgemm_kernel<EPI_GELU_SAVE_D><<<grid, MG_NT, 0, s>>>(g, x); break;
     default: mxgemm_kernel<EPI_ADD_AUX><<<grid, MG_NT, 0, s>>>(g, x); break;
   }
   MIA_LAUNCH_CHECK("gemm_mxfp8");

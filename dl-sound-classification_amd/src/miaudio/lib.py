@@ -23,6 +23,7 @@ OP_DENSE, OP_CONV, OP_CONVROW = 0, 1, 2
 KC, RC = 0, 1
 PRE_NONE, PRE_AFFINE, PRE_AFFINE_RELU, PRE_GELU = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_GELU, DACT_NZ, DACT_GELU, ACT_ADD_AUX, ACT_GELU_SAVE = 0, 1, 2, 3, 4, 5, 6
+ACT_GELU_SAVE_D, DACT_MUL = 7, 8
 
 vp = C.c_void_p
 i32 = C.c_int32

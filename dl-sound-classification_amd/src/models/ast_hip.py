@@ -4,9 +4,9 @@ Reference op sequence: src/models/ast.py:50-63 + timm 1.0.16 Block (pre-LN, qkv 
 SDPA, proj, LN, fc1, exact-erf GELU, fc2), LN eps 1e-6, sigmoid head on the CLS token.
 HBM layout per block (T = B*1645 tokens, D = 768): residual stream x (T, 768) f32; LN outputs,
 qkv (T, 3, 12, 64), attention output (T, 12, 64) and fc1 pre-activation (T, 3072) in the compute
-dtype.  fc1's epilogue writes both gelu(u) (fc2's operand) and the pre-activation u
-(MIA_ACT_GELU_SAVE); the fc1 backward applies gelu'(u) in the epilogue of the fc2 dgrad GEMM
-(MIA_DACT_GELU); residual adds are GEMM epilogues (MIA_ACT_ADD_AUX / accumulate).  In bf16 mode the
+dtype.  fc1's epilogue writes both gelu(u) (fc2's operand) and the derivative gelu'(u)
+(MIA_ACT_GELU_SAVE_D; u itself has no other reader); the fc1 backward multiplies it in the epilogue of
+the fc2 dgrad GEMM (MIA_DACT_MUL); residual adds are GEMM epilogues (MIA_ACT_ADD_AUX / accumulate).  In bf16 mode the
 linear weights are cast to bf16 once per step and every GEMM operand is bf16, so the projections run
 on the LDS-DMA dense kernel (mia_gemm path 5).
 """
@@ -183,14 +183,14 @@ class ASTFunction(torch.autograd.Function):
             xm = torch.empty(Tt, D, dtype=torch.float32, device=dev)
             lin(a, aq, 1, wproj, bproj, xm, "proj.fwd", act=L.ACT_ADD_AUX, aux=x)
             h2, m2, r2, h2q = _ln(xm, g2, b2, tdt, Tt, D, mx=mx)
-            u = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)   # fc1 pre-activation
+            gd = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)  # gelu'(u), u = fc1's pre-activation
             gu = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)  # gelu(u)
             guq = K.mx_empty(Tt, w1.shape[0], dev) if mx else None
-            lin(h2, h2q, 2, w1, bb1, gu, "fc1.fwd", act=L.ACT_GELU_SAVE, aux=u, mx=guq)
+            lin(h2, h2q, 2, w1, bb1, gu, "fc1.fwd", act=L.ACT_GELU_SAVE_D, aux=gd, mx=guq)
             xo = torch.empty(Tt, D, dtype=torch.float32, device=dev)
             lin(gu, guq, 3, w2, bb2, xo, "fc2.fwd", act=L.ACT_ADD_AUX, aux=xm)
             del hq, aq, h2q, guq
-            saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, u=u,
+            saved_blocks.append(dict(x=x, m1=m1, r1=r1, h=h, qkv=qkv, a=a, lse=lse, xm=xm, m2=m2, r2=r2, h2=h2, gd=gd,
                                      gu=gu, attn_work=aw))
             x = xo
         # final norm only matters for the CLS rows (ast.py:62-63 takes x[:, 0])
@@ -250,7 +250,7 @@ class ASTFunction(torch.autograd.Function):
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
             db1_ = torch.empty(w1.shape[0], dtype=torch.float32, device=dev)  # fc1 bias grad = colsum(du)
-            dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_GELU, dact_aux=sb["u"],
+            dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_MUL, dact_aux=sb["gd"],
                                     tag="fc2", db=db_next, dx_colsum=db1_)
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
             dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1", db=db1_)

@@ -33,7 +33,7 @@ enum { MIA_OP_DENSE = 0, MIA_OP_CONV = 1, MIA_OP_CONVROW = 2 };
 enum { MIA_LAYOUT_KC = 0, MIA_LAYOUT_RC = 1 };
 enum { MIA_PRE_NONE = 0, MIA_PRE_AFFINE = 1, MIA_PRE_AFFINE_RELU = 2, MIA_PRE_GELU = 3 };
 enum { MIA_ACT_NONE = 0, MIA_ACT_RELU = 1, MIA_ACT_GELU = 2, MIA_DACT_NZ = 3, MIA_DACT_GELU = 4,
-       MIA_ACT_ADD_AUX = 5, MIA_ACT_GELU_SAVE = 6 };
+       MIA_ACT_ADD_AUX = 5, MIA_ACT_GELU_SAVE = 6, MIA_ACT_GELU_SAVE_D = 7, MIA_DACT_MUL = 8 };
 
 /* A GEMM operand = a logical 2-D source S[i][j] whose j axis is contiguous in memory.
  *  DENSE   : S[i][j] = ptr[i*ld + j], i < rows, j < cols (zero outside).
@@ -63,7 +63,9 @@ typedef struct MiaOperand {
  *   DACT_NZ  : v *= (aux[m][n] != 0) * act_scale   (ReLU+dropout backward from saved output)
  *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation)
  *   ADD_AUX  : v += aux[m][n]                       (residual connection into a new tensor)
- *   GELU_SAVE: aux[m][n] = v; v = gelu(v)          (MLP fc1: keeps the pre-activation for the backward) */
+ *   GELU_SAVE: aux[m][n] = v; v = gelu(v)          (MLP fc1: keeps the pre-activation for the backward)
+ *   GELU_SAVE_D: aux[m][n] = gelu'(v); v = gelu(v) (MLP fc1: keeps the derivative the backward needs)
+ *   DACT_MUL : v *= aux[m][n]                       (GELU backward from the saved derivative) */
 typedef struct MiaEpilogue {
   void* ptr;
   int32_t dtype, act, accumulate, aux_dtype;

@@ -375,7 +375,13 @@ def test_dgemm_path(cuda, la, lb, M, N, Kd, split):
     assert rel(out.cpu(), ref) < 1e-3
 
 
-@pytest.mark.parametrize("act", ["relu", "gelu_save", "dact_gelu", "add_aux"])
+def _gelu_grad(x):
+    x = x.double().requires_grad_(True)
+    F.gelu(x).backward(torch.ones_like(x))
+    return x.grad
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu_save", "dact_gelu", "add_aux", "gelu_save_d", "dact_mul"])
 def test_dgemm_epilogues(cuda, act):
     g = torch.Generator().manual_seed(5)
     M, N, Kd = 320, 256, 256
@@ -386,7 +392,8 @@ def test_dgemm_epilogues(cuda, act):
     out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
     z = a.double() @ w.double().t()
     taux = aux.to(cuda).clone()
-    code = {"relu": L.ACT_RELU, "gelu_save": L.ACT_GELU_SAVE, "dact_gelu": L.DACT_GELU, "add_aux": L.ACT_ADD_AUX}[act]
+    code = {"relu": L.ACT_RELU, "gelu_save": L.ACT_GELU_SAVE, "dact_gelu": L.DACT_GELU, "add_aux": L.ACT_ADD_AUX,
+            "gelu_save_d": L.ACT_GELU_SAVE_D, "dact_mul": L.DACT_MUL}[act]
     K.gemm(A, Bo, K.epilogue(out, N, act=code, aux=None if act == "relu" else taux, ldaux=N), M, N, Kd, L.BF16)
     torch.cuda.synchronize()
     if act == "relu":
@@ -394,13 +401,42 @@ def test_dgemm_epilogues(cuda, act):
     elif act == "gelu_save":
         ref = F.gelu(z)
         assert rel(taux.float().cpu(), z) < 1e-2  # pre-activation saved into aux
+    elif act == "gelu_save_d":
+        ref = F.gelu(z)
+        assert rel(taux.float().cpu(), _gelu_grad(z)) < 1e-2  # gelu'(pre-activation) saved into aux
     elif act == "dact_gelu":
-        x = aux.double().requires_grad_(True)
-        F.gelu(x).backward(torch.ones_like(x))
-        ref = z * x.grad
+        ref = z * _gelu_grad(aux)
+    elif act == "dact_mul":
+        ref = z * aux.double()
     else:
         ref = z + aux.double()
     assert rel(out.float().cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["gelu_save_d", "dact_mul"])
+@pytest.mark.parametrize("cd", [L.F32, L.BF16])
+def test_gelu_derivative_epilogues_generic(cuda, act, cd):
+    """GELU_SAVE_D / DACT_MUL on the generic tile kernel (f32 compute, f32 aux -- the AST f32 path -- and a
+    ragged bf16 shape): aux = gelu'(u), out = gelu(u); out = acc * aux."""
+    g = torch.Generator().manual_seed(9)
+    M, N, Kd = 130, 70, 40
+    dt = torch.float32 if cd == L.F32 else torch.bfloat16
+    a = torch.randn(M, Kd, generator=g).to(dt)
+    w = torch.randn(N, Kd, generator=g).to(dt)
+    aux = torch.randn(M, N, generator=g).to(dt)
+    taux = aux.to(cuda).clone()
+    out = torch.empty(M, N, dtype=dt, device=cuda)
+    code = L.ACT_GELU_SAVE_D if act == "gelu_save_d" else L.DACT_MUL
+    K.gemm(K.dense(a.to(cuda), L.KC, M, Kd), K.dense(w.to(cuda), L.KC, N, Kd), K.epilogue(out, N, act=code, aux=taux,
+           ldaux=N), M, N, Kd, cd)
+    torch.cuda.synchronize()
+    z = a.double() @ w.double().t()
+    tol = TOL[cd] if cd == L.BF16 else 1e-5
+    if act == "gelu_save_d":
+        assert rel(out.cpu(), F.gelu(z)) < tol
+        assert rel(taux.cpu(), _gelu_grad(z)) < tol
+    else:
+        assert rel(out.cpu(), z * aux.double()) < tol
 
 
 @pytest.mark.parametrize("n,oh,ow", [(2, 57, 853), (3, 10, 121), (1, 57, 129)])
@@ -470,13 +506,14 @@ def test_mgemm_ragged_n_not_multiple_of_8(cuda, odt):
     assert rel(out2.float(), ref) < (1e-5 if odt == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("case", ["plain_f32", "residual_f32", "bias_bf16", "gelu", "gelu_save", "dact_gelu"])
+@pytest.mark.parametrize("case", ["plain_f32", "residual_f32", "bias_bf16", "gelu", "gelu_save", "dact_gelu",
+                                  "gelu_save_d", "dact_mul"])
 def test_mgemm_epilogues(cuda, case):
     """The fused epilogues of the AST linears on the 256x256 kernel: f32 output, residual add into f32
     with bias (proj / fc2 forward), bias only (qkv forward), exact-erf GELU, GELU_SAVE with bias (fc1
     forward: gelu(u) and the saved u) and dGELU with the column sums of the stored values (fc2
     backward-data: times gelu'(u); the sums are fc1's bias gradient) -- vs float64 / fp32 torch."""
-    M, N, Kd = 8192 + 37, 768 if case != "dact_gelu" else 3072, 768
+    M, N, Kd = 8192 + 37, 768 if case not in ("dact_gelu", "dact_mul") else 3072, 768
     a, b, A, Bo, g = _big_operands(cuda, L.KC, L.KC, M, N, Kd, 11)
     z = a.float() @ b.float().t()
     bias = torch.randn(N, generator=g, device=cuda)
@@ -505,6 +542,19 @@ def test_mgemm_epilogues(cuda, case):
         ref = F.gelu(z + bias)
         torch.cuda.synchronize()
         assert rel(u.float(), z + bias) < 1e-2
+    elif case == "gelu_save_d":  # fc1 forward keeping gelu'(u) for the backward: gelu' of the bf16 u
+        d = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.ACT_GELU_SAVE_D, bias=bias, aux=d, ldaux=N), M, N, Kd, L.BF16)
+        ref = F.gelu(z + bias)
+        torch.cuda.synchronize()
+        assert rel(d.float(), _gelu_grad((z + bias).to(torch.bfloat16))) < 1e-2  # u may round to the next bf16
+    elif case == "dact_mul":  # fc2 backward-data times the saved gelu'(u), column sums of the stored values
+        d = (torch.rand(M, N, generator=g, device=cuda) * 1.2 - 0.1).to(torch.bfloat16)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        cs = torch.full((N,), float("nan"), device=cuda)
+        K.gemm(A, Bo, K.epilogue(out, N, act=L.DACT_MUL, aux=d, ldaux=N, colsum=cs), M, N, Kd, L.BF16)
+        ref = z.double() * d.double()
     else:
         u = (torch.randn(M, N, generator=g, device=cuda) * 2).to(torch.bfloat16)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)

@@ -52,7 +52,7 @@ def _to(cuda, *ts):
 
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (1000, 768, 768), (513, 2304, 768), (777, 768, 3072),
                                     (300, 3072, 768)])
-@pytest.mark.parametrize("epi", ["bf16_bias", "f32_plain", "f32_residual", "gelu_save", "gelu"])
+@pytest.mark.parametrize("epi", ["bf16_bias", "f32_plain", "f32_residual", "gelu_save", "gelu", "gelu_save_d"])
 def test_gemm_mxfp8_vs_float64(cuda, M, N, Kd, epi):
     g = torch.Generator().manual_seed(M + 3 * N + 7 * Kd)
     qa, sa, qb, sb = _mx_pair(M, N, Kd, g)
@@ -76,15 +76,23 @@ def test_gemm_mxfp8_vs_float64(cuda, M, N, Kd, epi):
     else:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
         u = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
-        act = L.ACT_GELU_SAVE if epi == "gelu_save" else L.ACT_GELU
-        K.gemm_mxfp8(A, B, K.epilogue(out, N, act=act, bias=bias.to(cuda), aux=u if epi == "gelu_save" else None,
-                                      ldaux=N if epi == "gelu_save" else 0))
+        act = {"gelu_save": L.ACT_GELU_SAVE, "gelu_save_d": L.ACT_GELU_SAVE_D}.get(epi, L.ACT_GELU)
+        saves = epi != "gelu"
+        K.gemm_mxfp8(A, B, K.epilogue(out, N, act=act, bias=bias.to(cuda), aux=u if saves else None,
+                                      ldaux=N if saves else 0))
         pre = (ref + bias.double()).to(torch.bfloat16).double()  # the Linear output rounds to bf16 first
         want = torch.nn.functional.gelu(pre)
         if epi == "gelu_save":
             torch.cuda.synchronize()
             du = (u.cpu().double() - pre).abs().max() / pre.abs().max()
             assert float(du) <= 2.0 ** -7, f"saved pre-activation off by {float(du):.3e}"  # one bf16 ulp
+        elif epi == "gelu_save_d":  # gelu'(u) of the bf16 pre-activation, rounded to bf16
+            torch.cuda.synchronize()
+            x = pre.clone().requires_grad_(True)
+            torch.nn.functional.gelu(x).backward(torch.ones_like(x))
+            dd = (u.cpu().double() - x.grad).abs().max() / x.grad.abs().max()
+            # u may round to the neighbouring bf16 (f32 accumulation order), gelu'' <= 0.49 amplifies it
+            assert float(dd) <= 1e-2, f"saved gelu' off by {float(dd):.3e}"
     torch.cuda.synchronize()
     got = out.cpu().double()
     err = float((got - want).abs().max() / want.abs().max())
