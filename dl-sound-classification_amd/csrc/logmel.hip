@@ -14,11 +14,13 @@
 // reflect-padded) while this chunk's 16 frames are computed (4 per wave), then committed to LDS
 // behind the chunk's tile store; the mel table, window taps and the twiddles of the three passes are
 // read once per workgroup (the real-split twiddles derived per frame from one per lane).  Each mel
-// band is widened in LDS to whole 16-B aligned groups of 4 bins with zero weights, so the band loop
-// reads 4 bins and 4 weights with one ds_read_b128 each.  The 128 x 16 dB tile is written back as
-// 128 rows of 16 contiguous frames.  Measured at B = 256 (tools/bench_logmel.py, tools/logmel_pmc.sh):
-// 0.75 -> 0.66 ms for the three passes; ~400 VALU and ~110 LDS instructions per frame, the band loop
-// ~36 % of the kernel and most of its LDS bank conflicts (lanes = bands read data-dependent bins).
+// band is widened to whole 16-B aligned groups of 4 bins with zero weights, so the band loop reads 4
+// bins and 4 weights with one ds_read_b128 each; the weights sit in LDS interleaved by lane (row =
+// group index, column = the lane's band), so a weight read is 64 consecutive 16-B chunks: the
+// per-band layout made them data-dependent and bank-conflicting (fft_mel_db 0.636 -> 0.528 ms, bit-
+// identical; padding the power spectrum the same way, or a wider Stockham swizzle: no further gain).
+// The 128 x 16 dB tile is written back as 128 rows of 16 contiguous frames.  Measured at B = 256
+// (tools/bench_logmel.py, tools/logmel_pmc.sh): ~400 VALU and ~110 LDS instructions per frame.
 // Per-clip top_db clamp + mean / unbiased-std normalisation need the clip max first, so two light
 // passes follow (stats over the dB tensor, which stays in the 256 MB Infinity Cache at batch 256,
 // then an in-place normalise).
@@ -77,13 +79,14 @@ __device__ __forceinline__ void dft8(f2 (&v)[8]) {
 // entries per lane) spread over 16 banks pairs instead of 2 (1- to 2-way instead of 8-way).
 __device__ __forceinline__ int swz(int i) { return i ^ ((i >> 3) & 7); }
 
+
 __device__ __forceinline__ int reflect_idx(int n, int T) {
   if (n < 0) n = -n;
   if (n >= T) n = 2 * (T - 1) - n;
   return n;
 }
 
-constexpr int MAX_NNZ = 2048;  // band weights staged in LDS (htk, 128 mels at n_fft 1024: 1,008 + group padding)
+constexpr int MAX_WROWS = 12;  // interleaved weight rows staged in LDS (htk, 128 mels at n_fft 1024: 3 + 7)
 constexpr float DB_PER_LOG2 = 3.0102999566398120f;  // 10 log10(2)
 // W16^q = exp(-2 pi i q / 16)
 __constant__ const f2 W16[8] = {{1.f, 0.f},
@@ -102,8 +105,11 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   __shared__ float seg[SEG];
   __shared__ f2 buf[LW][NC];             // one in-place Stockham buffer per wave
   __shared__ float tile[NMEL_MAX][FB + 1];
-  __shared__ float bw[MAX_NNZ];
+  // band weights interleaved by lane: row goff[pass] + i holds group i (4 bins) of band lane + 64 pass
+  // for all 64 lanes, so the band loop's weight reads are 64 consecutive 16-B chunks (conflict-free)
+  __shared__ f32x4 bwi[MAX_WROWS * 64];
   __shared__ int bs[NMEL_MAX], bl[NMEL_MAX], bo[NMEL_MAX];
+  __shared__ int goff[NMEL_MAX / 64 + 1];
   __shared__ float redmax[LW];
   __shared__ int w_lds_s;
 
@@ -114,23 +120,36 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   // 4 weights with one ds_read_b128 each (a table too large for LDS is read from global memory one
   // weight at a time)
   if (t == 0) {
-    int acc = 0;
-    for (int m = 0; m < n_mels; ++m) {
-      const int ks = tb.band_start[m], len = tb.band_len[m];
-      bs[m] = ks & ~3;                                  // 16-B aligned first bin
-      bl[m] = ((ks & 3) + len + 3) & ~3;                // whole 4-bin groups
-      bo[m] = acc;
-      acc += bl[m];
+    int rows = 0;
+    for (int p = 0; p * 64 < n_mels; ++p) {
+      goff[p] = rows;
+      int g = 0;
+      for (int m = 64 * p; m < n_mels && m < 64 * (p + 1); ++m) {
+        const int ks = tb.band_start[m], len = tb.band_len[m];
+        bs[m] = ks & ~3;                                  // 16-B aligned first bin
+        bl[m] = ((ks & 3) + len + 3) & ~3;                // whole 4-bin groups
+        g = max(g, bl[m] >> 2);
+      }
+      rows += g;
     }
-    w_lds_s = acc <= MAX_NNZ;
+    w_lds_s = rows <= MAX_WROWS;
   }
   __syncthreads();
   const bool w_lds = w_lds_s;  // block-uniform
   if (w_lds) {
-    for (int m = wave; m < n_mels; m += LW) {
+    for (int p = 0; p * 64 < n_mels; ++p) {
+      const int m = 64 * p + lane;
+      if (m >= n_mels) continue;
       const int lead = tb.band_start[m] & 3, len = tb.band_len[m], src = tb.band_off[m];
-      for (int i = lane; i < bl[m]; i += 64)
-        bw[bo[m] + i] = (i >= lead && i < lead + len) ? tb.band_w[src + i - lead] : 0.f;
+      for (int i = wave; 4 * i < bl[m]; i += LW) {
+        f32x4 w4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 4 * i + j;
+          w4[j] = (k >= lead && k < lead + len) ? tb.band_w[src + k - lead] : 0.f;
+        }
+        bwi[(goff[p] + i) * 64 + lane] = w4;
+      }
     }
   } else {
     for (int m = t; m < n_mels; m += LNT) {
@@ -254,8 +273,9 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         const int ks = bs[m], kl = bl[m], off = bo[m];
         float acc = 0.f;
         if (w_lds) {
+          const f32x4* wrow = bwi + goff[m >> 6] * 64 + lane;
           for (int i = 0; i < kl; i += 4) {  // zero weights outside the band (P stays finite there)
-            const f32x4 w4 = *reinterpret_cast<const f32x4*>(&bw[off + i]);
+            const f32x4 w4 = wrow[(i >> 2) * 64];
             const f32x4 p4 = *reinterpret_cast<const f32x4*>(&P[ks + i]);
             acc = fmaf(p4[0], w4[0], acc);
             acc = fmaf(p4[1], w4[1], acc);
