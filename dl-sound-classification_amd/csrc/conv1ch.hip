@@ -8,7 +8,9 @@
 //   Q_r[x][ky] = sum_{kx,co} dy[b][r][x-kx][co] * w[co][ky][kx]        (M = x, N = ky, K = (kx, co) = 256)
 // and dx[b][r+ky][x] += Q_r[x][ky].  A block owns one clip and 128 output columns and sweeps every
 // dY row once (each dY byte is read from HBM once); the 64 output rows x 128 columns accumulate in
-// LDS (f32, one writer per address, program order => deterministic) and are stored once as bf16.
+// LDS (f32, one writer per address, program order => deterministic; rows 129 floats apart so a dY row's
+// scatter into its 8 output rows is conflict-free: at 128 it was 8-way, 0.48 of the kernel's LDS cycles
+// in SQ_LDS_BANK_CONFLICT) and are stored once as bf16.
 // dY rows are register-staged two rows ahead (issue early, write late) into a 2-deep LDS ring whose
 // pixel stride (80 B) makes every 16-lane ds_read_b128 group conflict-free.  N = 8 of the MFMA's 32
 // columns carry data: the op is 58 GFLOP/step of real work, HBM-bound on the dY read either way.
@@ -21,6 +23,9 @@ constexpr int C1_BW = 128;                 // output columns per block
 constexpr int C1_SLOTS = C1_BW + C1_K - 1; // staged dY pixels per row
 constexpr int C1_PSB = 80;                 // LDS bytes per staged pixel (64 B data + 16 B skew)
 constexpr int C1_HMAX = 64;                // output rows held in LDS
+// output row stride in LDS: 129 floats, so the 8 kernel rows ky a dY row scatters into (lanes 0-7 of a
+// half wave, same column) fall on 8 different banks (a 128-float stride put all 8 on one bank: 8-way)
+constexpr int C1_OLD = C1_BW + 1;
 constexpr int C1_LD = (C1_SLOTS * 4 + 255) / 256;  // 16-B chunks per thread per row (3)
 
 struct C1Args {
@@ -32,12 +37,12 @@ struct C1Args {
 
 __global__ __launch_bounds__(256) void conv1ch_dgrad_kernel(C1Args g) {
   __shared__ __attribute__((aligned(16))) char rows[2][C1_SLOTS * C1_PSB];
-  __shared__ __attribute__((aligned(16))) float outs[C1_HMAX * C1_BW];
+  __shared__ __attribute__((aligned(16))) float outs[C1_HMAX * C1_OLD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / g.nchunk;
   const int w0 = (blockIdx.x - b * g.nchunk) * C1_BW;
 
-  for (int i = t; i < C1_HMAX * C1_BW; i += 256) outs[i] = 0.f;
+  for (int i = t; i < C1_HMAX * C1_OLD; i += 256) outs[i] = 0.f;
 
   // B fragments (whole K = 256 in registers): lane column n = ky, k = 16 ks + 8 (lane >> 5) + j
   // with kx = ks >> 1, co = 16 (ks & 1) + 8 (lane >> 5) + j.
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(256) void conv1ch_dgrad_kernel(C1Args g) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
     }
     if (ky < C1_K) {
-      float* o = outs + (r + ky) * C1_BW + 32 * wave + 4 * half;
+      float* o = outs + (r + ky) * C1_OLD + 32 * wave + 4 * half;
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[(i & 3) + 8 * (i >> 2)] += acc[i];
     }
@@ -118,7 +123,7 @@ __global__ __launch_bounds__(256) void conv1ch_dgrad_kernel(C1Args g) {
     const int y = q / (C1_BW / 4), x4 = (q - y * (C1_BW / 4)) * 4;
     const int x = w0 + x4;
     if (x >= g.wd) continue;
-    const float* o = outs + y * C1_BW + x4;
+    const float* o = outs + y * C1_OLD + x4;
     if (x + 4 <= g.wd) {
       bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
       *reinterpret_cast<bf16x4*>(dxb + (int64_t)y * g.wd + x) = v;
