@@ -1460,6 +1460,15 @@ __global__ __launch_bounds__(NT) void tile_sqsum_kernel(const float* __restrict_
   tile_sqsum_store(out + blockIdx.x, (double)sq, red);
 }
 
+// 16-B chunk swizzle of the k-contiguous (KC) 128 x 64 tile images: chunk c of row r sits at c ^ swz(r).
+// A 32-row fragment's ds_read_b128 lane groups ({0-3, 12-15, 20-27} and its complement) hold rows 8 and
+// 24 apart, which r & 7 maps to the same chunk of the same bank half (2-way conflicts); (r >> 1) & 7 gives
+// the 8 even and the 8 odd rows of each group distinct chunks
+#ifndef DG_SWZ
+#define DG_SWZ 0
+#endif
+__device__ __forceinline__ int dkc_swz(int r) { return DG_SWZ ? ((r >> 1) & 7) : (r & 7); }
+
 template <int L>
 struct DLoader {
   // per-lane source pointers for this wave's 4 DMA instructions of a tile, advanced per K-tile
@@ -1472,7 +1481,7 @@ struct DLoader {
       const int j = wave * 4 + i;
       if constexpr (L == MIA_LAYOUT_KC) {
         const int r = 8 * j + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
+        const int c = (lane & 7) ^ dkc_swz(r);
         int64_t row = r0 + r;
         if (row >= rows_or_cols) row = rows_or_cols - 1;
         src[i] = base + row * ld + kbeg + c * 8;
@@ -1501,7 +1510,7 @@ __device__ __forceinline__ bf16x8 dfrag(const char* tile, int rbase, int ks, int
   if constexpr (L == MIA_LAYOUT_KC) {
     const int rr = rbase + (lane & 31);
     const int c = 2 * ks + (lane >> 5);
-    return *reinterpret_cast<const bf16x8*>(tile + rr * 128 + ((c ^ (rr & 7)) * 16));
+    return *reinterpret_cast<const bf16x8*>(tile + rr * 128 + ((c ^ dkc_swz(rr)) * 16));
   } else {
     const int i16 = lane & 15, gq = lane >> 4;
     const int col = rbase + 16 * (gq & 1) + 4 * (i16 & 3);
