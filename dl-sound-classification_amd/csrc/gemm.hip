@@ -1464,10 +1464,7 @@ __global__ __launch_bounds__(NT) void tile_sqsum_kernel(const float* __restrict_
 // A 32-row fragment's ds_read_b128 lane groups ({0-3, 12-15, 20-27} and its complement) hold rows 8 and
 // 24 apart, which r & 7 maps to the same chunk of the same bank half (2-way conflicts); (r >> 1) & 7 gives
 // the 8 even and the 8 odd rows of each group distinct chunks
-#ifndef DG_SWZ
-#define DG_SWZ 0
-#endif
-__device__ __forceinline__ int dkc_swz(int r) { return DG_SWZ ? ((r >> 1) & 7) : (r & 7); }
+__device__ __forceinline__ int dkc_swz(int r) { return (r >> 1) & 7; }
 
 template <int L>
 struct DLoader {
