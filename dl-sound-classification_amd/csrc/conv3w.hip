@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
     it = it < items ? it : items - 1;
     const int seg = it % g.nseg, rest = it / g.nseg;
     const int oy = rest % g.oh, b = rest / g.oh;
-    const int l = lane < 40 ? lane : lane - 40;  // lanes 40..63 repeat lanes 0..23 (no divergent staging)
+    const int l = lane < 40 ? lane : lane - 40;  // lanes 40..63 load lanes 0..23's bytes (not staged)
     const int r = l / 5, q = l % 5;
     const int col = seg * 32 + 8 * q;
     const bf16* src = g.x + ((int64_t)b * g.h + oy + r) * g.wd;
