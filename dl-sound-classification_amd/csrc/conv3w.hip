@@ -34,7 +34,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p0, int stride) {
 }
 
 __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
-  constexpr int ROWB = 88, CPYB = 8 * ROWB;
+  constexpr int ROWB = 80, CPYB = 704;  // 80-B rows (conflict-free staging writes), copies 704 B apart (48 banks: conflict-free reads)
   __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
   __shared__ __attribute__((aligned(16))) char dyt[4][32 * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

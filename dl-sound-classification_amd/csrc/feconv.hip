@@ -418,7 +418,9 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
 // the 1 -> 32 channel 8x8 conv on the pooled frontend image).  Wave-persistent like conv1: the 4
 // weight fragments (32 channels x 64 taps) are the MFMA A operand; per (clip, output row, 32-px)
 // item the wave stages the 8 input rows x 40 samples it needs into a per-wave LDS strip as four
-// copies shifted by 0..3 samples (row pitch 88 B, copy pitch 8 rows), so every 8-sample B fragment
+// copies shifted by 0..3 samples (80-B rows, copies 704 B = 48 banks apart: conflict-free 16-B staging
+// writes and 8-B fragment reads; the 88-B pitch before cost 2-way staging conflicts, 0.305 -> 0.262 ms),
+// so every 8-sample B fragment
 // (k-step ks: kernel rows 2ks, 2ks+1 on the lane halves, kx = 0..7) is two aligned ds_read_b64 and
 // the 32 lanes of a half hit 32 distinct bank pairs; BN3 statistics accumulate in the epilogue.
 struct F3Args {
@@ -432,7 +434,7 @@ struct F3Args {
 
 template <bool STATS>
 __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
-  constexpr int ROWB = 88, CPYB = 8 * ROWB;
+  constexpr int ROWB = 80, CPYB = 704;  // 80-B rows (conflict-free staging writes), copies 704 B apart (48 banks: conflict-free reads)
   __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
   __shared__ __attribute__((aligned(16))) char stage[4][2048];  // the item's 32 px x 64 B output run
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
