@@ -56,13 +56,21 @@ __global__ __launch_bounds__(256) void conv1ch_dgrad_kernel(C1Args g) {
       bw[ks][j] = ky < C1_K ? (bf16)g.w[((co0 + j) * C1_K + ky) * C1_K + kx] : (bf16)0.f;
   }
 
+  // thread slot q -> (staged pixel s, 16-B chunk c): each 8-lane group of a ds_write_b128 takes the 4
+  // chunks of pixels p and p + 4 (80 B x 4 = 320 B = 16 banks apart: conflict-free; pixels p, p + 1 were
+  // 2-way), a wave still loads 16 consecutive pixels
+  auto slot_of = [](int q, int& s, int& c) __attribute__((always_inline)) {
+    const int gq = q >> 3, j = q & 7;
+    s = (gq >> 2) * 8 + (gq & 3) + 4 * (j >> 2);
+    c = j & 3;
+  };
   const bf16* dyb = g.dy + (int64_t)b * g.oh * g.ow * C1_C;
   auto load_row = [&](int r, uint4 (&reg)[C1_LD]) __attribute__((always_inline)) {
     const bf16* src = dyb + (int64_t)r * g.ow * C1_C;
 #pragma unroll
     for (int i = 0; i < C1_LD; ++i) {
-      const int q = t + 256 * i;
-      const int s = q >> 2, c = q & 3;
+      int s, c;
+      slot_of(t + 256 * i, s, c);
       const int px = w0 - (C1_K - 1) + s;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (r < g.oh && s < C1_SLOTS && px >= 0 && px < g.ow)
@@ -73,8 +81,8 @@ __global__ __launch_bounds__(256) void conv1ch_dgrad_kernel(C1Args g) {
   auto store_row = [&](char* dst, const uint4 (&reg)[C1_LD]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < C1_LD; ++i) {
-      const int q = t + 256 * i;
-      const int s = q >> 2, c = q & 3;
+      int s, c;
+      slot_of(t + 256 * i, s, c);
       if (s < C1_SLOTS) *reinterpret_cast<uint4*>(dst + s * C1_PSB + c * 16) = reg[i];
     }
   };
