@@ -136,6 +136,8 @@ def build_envnet_step(args, dev, rank, world, B):
     ddp = GradAllReducer(model, world, fc1_exchange=args.fc1_exchange) if world > 1 else None
 
     def step():
+        if ddp is not None:
+            ddp.begin_step()
         x, y, _ = bc_mix(wav, labels, 50, gen=g)
         z = model(x.view(x.shape[0], 1, -1))
         loss, dz, _ = K.soft_ce(z, y, input_sigmoid=False)
@@ -297,11 +299,13 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
         if ddp is not None:
-            mine = torch.tensor([ddp.exposed_ms() or 0.0], device=dev)
+            mine = torch.tensor([ddp.exposed_ms() or 0.0, ddp.backward_ms() or 0.0], device=dev)
             every = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(every, mine)
             nbytes = sum(p.numel() * p.element_size() for p in ddp.params)
-            comm = {"exposed_ms_per_step": [round(float(v), 3) for v in every],
+            comm = {"exposed_ms_per_step": [round(float(v[0]), 3) for v in every],
+                    "exposed_from": "end of the backward's last compute kernel (compute-stream event)",
+                    "fwd_bwd_ms_per_step": [round(float(v[1]), 3) for v in every],
                     "allreduce_bytes_per_step": nbytes - ddp.last_gathered_param_bytes,
                     "allgather_bytes_per_rank_per_step": ddp.last_gathered_bytes,
                     "chunks_per_step": ddp.last_chunks, "fc1_exchange": ddp.fc1_exchange,
@@ -354,6 +358,9 @@ def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_c
     return out
 
 
+CPU_WARMUP = 2  # BASELINE.md §3 / SURVEY.md §8(d): 2 warm-up and >= 5 timed steps
+
+
 def cpu_baseline_envnet(threads: int, batch: int, steps: int):
     """Oracle (CPU restatement of the reference path) timed on this host: BC-mix + fwd + loss + bwd +
     clip + Adam (kind "port")."""
@@ -389,7 +396,8 @@ def cpu_baseline_envnet(threads: int, batch: int, steps: int):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    one()
+    for _ in range(CPU_WARMUP):
+        one()
     t0 = time.perf_counter()
     for i in range(steps):
         one()
@@ -397,11 +405,11 @@ def cpu_baseline_envnet(threads: int, batch: int, steps: int):
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
             "sample": f"oracle EnvNet-v2 f32 train step (BC-mix, fwd, loss, bwd, clip, Adam), batch {batch}, "
-                      f"{steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work on {threads} threads "
-                      f"of {cpu_model()}"}
+                      f"{steps} timed steps after {CPU_WARMUP} warm-ups, {dt:.1f} s of CPU work on {threads} threads "
+                      f"of {cpu_model()}", "warmup": CPU_WARMUP, "steps": steps}
 
 
-def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 3):
+def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 5):
     """Oracle AST train step on this host with the feature path included: log-mel of the waveform
     (ASTPreprocessor restatement), SpecAugment + Mixup per clip, fwd, loss, bwd, clip, Adam."""
     sys.path.insert(0, str(REPO))
@@ -436,7 +444,8 @@ def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 3):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    one()
+    for _ in range(CPU_WARMUP):
+        one()
     t0 = time.perf_counter()
     for i in range(steps):
         one()
@@ -444,8 +453,46 @@ def cpu_baseline_ast(threads: int, batch: int = 2, steps: int = 3):
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
             "sample": f"oracle AST f32 train step (log-mel, SpecAugment+Mixup, fwd, loss, bwd, clip, Adam), "
-                      f"batch {batch}, {steps} timed steps after 1 warm-up, {dt:.1f} s of CPU work on {threads} "
-                      f"threads of {cpu_model()}"}
+                      f"batch {batch}, {steps} timed steps after {CPU_WARMUP} warm-ups, {dt:.1f} s of CPU work on "
+                      f"{threads} threads of {cpu_model()}", "warmup": CPU_WARMUP, "steps": steps}
+
+
+def hbm_calibration(dev, gib: int = 2, iters: int = 5):
+    """This box's HBM streaming rate, measured in this process: a 2 GiB -> 2 GiB float4 copy
+    (``mia_stream_copy``: 4 groups in flight per thread, non-temporal), read + write bytes over the HIP-event
+    time on the launch stream.  Boxes differ (the fused FC1 Adam GEMM streamed the same bytes at 6.1 TB/s on
+    one box and 5.0-5.3 on others), so HBM-bound kernels report ``frac_vs_box`` = achieved / this rate beside
+    ``frac`` = achieved / the 8 TB/s spec."""
+    from src.miaudio import lib as L
+    n = gib << 30
+    src = torch.empty(n, dtype=torch.uint8, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    lib, s = L.load(), L.stream_ptr()
+    for _ in range(2):
+        L.check(lib.mia_stream_copy(src.data_ptr(), dst.data_ptr(), n, s), "stream_copy")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(torch.cuda.current_stream())
+    for _ in range(iters):
+        L.check(lib.mia_stream_copy(src.data_ptr(), dst.data_ptr(), n, s), "stream_copy")
+    e1.record(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"kernel": "stream_copy_kernel (mia_stream_copy)", "copy_bytes": n, "traffic_bytes": 2 * n,
+            "ms": round(ms, 4), "gbs": round(2 * n / (ms * 1e-3) / 1e9, 1),
+            "frac_of_spec": round(2 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def add_box_fraction(leg: dict, box_gbs: float):
+    """frac_vs_box beside frac for every HBM-bound figure of a leg."""
+    for key in ("roofline", "dominant_kernel"):
+        r = leg.get(key)
+        if r and r.get("unit") == "GB/s":
+            r["frac_vs_box"] = round(r["achieved"] / box_gbs, 4)
+    fp = leg.get("frontend_path")
+    if fp:
+        fp["frac_vs_box"] = round(fp["achieved_gbs"] / box_gbs, 4)
 
 
 def free_leg():
@@ -464,6 +511,8 @@ def main():
     check_world(args.gpus, dist.get_world_size() if world > 1 else 1)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    calib = hbm_calibration(dev)
+    log(f"HBM calibration: {calib['gbs']} GB/s streaming copy on this box")
     results = {}
     if args.model in ("both", "envnet"):
         log("EnvNet-v2 leg: building")
@@ -507,12 +556,15 @@ def main():
         log(f"AST fp8-mixed: {results['ast_fp8']['value']} clips/s")
         del step
         free_leg()
+    for leg in results.values():
+        add_box_fraction(leg, calib["gbs"])
     out = results.get("envnet") or results.get("ast") or results["ast_fp8"]
     if "envnet" in results and "ast" in results:
         out = dict(results["envnet"])
         out["ast"] = results["ast"]
     if "ast_fp8" in results and out is not results["ast_fp8"]:
         out["ast_fp8"] = results["ast_fp8"]
+    out["hbm_calibration"] = calib
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads, why = cpu_threads()
         log(f"CPU baseline threads: {threads} ({why})")
@@ -520,7 +572,7 @@ def main():
             log(f"CPU baseline EnvNet-v2 B=4 on {threads} threads")
             b4 = cpu_baseline_envnet(threads, batch=4, steps=8)
             log(f"CPU baseline EnvNet-v2 B=16: B=4 gave {b4['value']} clips/s")
-            b16 = cpu_baseline_envnet(threads, batch=16, steps=2)
+            b16 = cpu_baseline_envnet(threads, batch=16, steps=5)
             out["cpu_baseline"] = dict(b4, samples=[b4, b16], threads_rule=why)
         if "ast" in results:
             target = out["ast"] if "envnet" in results else out

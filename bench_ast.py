@@ -34,6 +34,8 @@ def build_ast_step(args, dev, rank, world, B, compute=None):
     logmel = GpuLogMel(44_100, 128, True, 0.0, 0.5)
 
     def step():
+        if ddp is not None:
+            ddp.begin_step()
         spec = logmel(wav)
         spec, y = spec_augment_mixup(spec, labels, 50, 192, 48, 0.5, 0.25, gen=g)
         probs = model(spec)

@@ -1377,6 +1377,10 @@ static bool fb_ok(int32_t N) {
   return nkb == 1 || nt - FB_LAG * (nkb - 1) >= 2;
 }
 
+// the part of the bf16 workspace the forward fills (mia_attn_fwd_save_q) and the two-kernel backward reads:
+// Q' + the fragment rows (the one-pass form's flags and running dQ sums follow it)
+extern "C" int64_t mia_attn_saved_q_bytes(int32_t B, int32_t N, int32_t H) { return fb_flags_offset(B, N, H); }
+
 extern "C" int64_t mia_attn_bwd_workspace_bytes(int32_t dtype, int32_t B, int32_t N, int32_t H) {
   const int64_t rows = (int64_t)B * N * H;
   if (dtype == MIA_F32) return rows * 4;  // delta

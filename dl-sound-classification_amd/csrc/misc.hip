@@ -743,3 +743,32 @@ extern "C" int mia_spec_augment_mixup(const float* spec, const float* pool, floa
   MIA_LAUNCH_CHECK("spec_augment_mixup");
   return 0;
 }
+
+// ------------------------------------------------------------------------------ box calibration
+// Streaming copy dst <- src of n16 16-B groups (bench.py's same-process HBM calibration: the rate this box's
+// HBM reaches for a plain read + write stream, next to which a kernel's achieved GB/s is judged).  Four
+// groups in flight per thread, non-temporal loads and stores (the stream is touched once), grid-stride.
+__global__ __launch_bounds__(256) void stream_copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                          int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 256 * u < n16) v[u] = __builtin_nontemporal_load(src + i + 256 * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 256 * u < n16) __builtin_nontemporal_store(v[u], dst + i + 256 * u);
+  }
+}
+
+extern "C" int mia_stream_copy(const void* src, void* dst, int64_t bytes, mia_stream_t stream) {
+  MIA_CHECK_ARG(src && dst && bytes > 0 && bytes % 16 == 0, "stream_copy: bytes must be a positive multiple of 16");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0,
+                "stream_copy: 16-B aligned pointers");
+  const int64_t n16 = bytes / 16;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n16, 1024), (int64_t)mia::cu_count() * 16);
+  stream_copy_kernel<<<grid, 256, 0, as_stream(stream)>>>((const f32x4*)src, (f32x4*)dst, n16);
+  MIA_LAUNCH_CHECK("stream_copy");
+  return 0;
+}

@@ -29,6 +29,7 @@ from src.training.lite import CSVLogger, EarlyStopping, ModelCheckpoint, Trainer
 from src.utils.config import Cfg, compose, instantiate, to_container  # noqa: E402
 
 _DM_KEYS = ("root", "fold", "val_split")
+LAST_TRAINER = None  # the Trainer of the latest train() call (tests read its device / process group)
 
 
 def fix_seed(seed: int) -> None:
@@ -80,6 +81,8 @@ def train(cfg) -> dict:
     logger = CSVLogger(save_dir=os.path.join(ROOT, "outputs"),
                        experiment_name=cfg.get("logging", {}).get("experiment_name", "default"))
     trainer = Trainer(**to_container(cfg.trainer), logger=logger, callbacks=build_callbacks(cfg))
+    global LAST_TRAINER
+    LAST_TRAINER = trainer
     trainer.fit(lit, datamodule=datamodule, ckpt_path=cfg.get("ckpt_path"))
     out = trainer.test(ckpt_path="best", datamodule=datamodule)
     if trainer.is_global_zero:
@@ -87,8 +90,27 @@ def train(cfg) -> dict:
     return out[0]
 
 
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """``trainer.devices=N`` without a launcher: start one process per device through
+    torch.distributed.run on this node (rendezvous on 127.0.0.1), as Lightning's DDP strategy re-launches
+    the script per rank (reference train.py:190-194).  Runs before this process touches the GPU."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
 def main(argv=None):
-    cfg = compose(os.path.join(ROOT, "configs"), "training", list(sys.argv[1:] if argv is None else argv))
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cfg = compose(os.path.join(ROOT, "configs"), "training", argv)
+    devices = cfg.trainer.get("devices", 1)
+    if isinstance(devices, int) and devices > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(devices, argv))
     return train(cfg)
 
 

@@ -150,5 +150,9 @@ class ASTModel(nn.Module):
             x = self._logmel(x.reshape(x.shape[0], -1))
         if x.dim() == 4:
             x = x[:, 0]
+        params = self.param_list()
+        # grad mode is off inside an autograd.Function's forward: read it here, so an inference forward
+        # (validation / test under no_grad) skips the backward's saved-Q' workspace
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
         with torch.autocast("cuda", enabled=False):
-            return ASTFunction.apply(self, x, self._compute_code(), *self.param_list())
+            return ASTFunction.apply(self, x, self._compute_code(), grad, *params)

@@ -96,7 +96,7 @@ def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.
 
 class ASTFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model, spec, compute: int, *params):
+    def forward(ctx, model, spec, compute: int, grad: bool, *params):
         if not spec.is_cuda:
             raise RuntimeError("ASTModel runs on the MI355X HIP kernels only (input is on CPU)")
         mx = compute == L.MXFP8  # fp8-mixed: block linears' forward GEMMs on MX-fp8 operands
@@ -164,9 +164,10 @@ class ASTFunction(torch.autograd.Function):
             # bf16 training: the forward also writes Q' (the scaled query operand) into the backward's
             # attention workspace, so the backward's prep pass neither re-reads q nor rewrites Q'
             aw = None
-            if cd == L.BF16 and ATTN_SAVE_Q and any(ctx.needs_input_grad):
-                aw = torch.empty(int(L.load().mia_attn_bwd_workspace_bytes(cd, B, N, Hh)), dtype=torch.uint8,
-                                 device=dev)
+            if cd == L.BF16 and ATTN_SAVE_Q and grad:
+                # Q' + the row-constant fragments only (what the two-kernel backward reads); the one-pass
+                # backward's running dQ sums are the backward's own transient workspace
+                aw = torch.empty(int(L.load().mia_attn_saved_q_bytes(B, N, Hh)), dtype=torch.uint8, device=dev)
             with K.probe("attn.fwd", 4.0 * B * Hh * N * N * (D // Hh), (qkv.numel() + a.numel()) * qkv.element_size()):
                 if aw is not None:
                     L.check(L.load().mia_attn_fwd_save_q(qkv.data_ptr(), a.data_ptr(), lse.data_ptr(),
@@ -315,4 +316,4 @@ class ASTFunction(torch.autograd.Function):
         grads[3] = dpos
         emit(0, 4)
         ctx.s = None
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)

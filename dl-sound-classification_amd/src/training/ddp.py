@@ -37,9 +37,13 @@ dtype, issued after the gradient exchange.  torch DDP broadcasts rank 0's buffer
 each forward; the values it sends there (rank 0's statistics after the previous step's forward) are
 the ones sent here at the end of that previous step, so every forward sees the same buffers.
 
-``timing`` (a list, or None): when set, ``finish()`` appends one (compute done, exchange done) HIP
-event pair per step; ``exposed_ms()`` turns them into the communication time the backward did not
-hide (bench.py reports it per rank).
+``timing`` (a list, or None): when set, ``begin_step()`` (called before the forward) records a step-start
+HIP event and ``finish()`` appends one (step start, compute done, exchange done) triple per step.  "Compute
+done" is an event recorded on the compute stream when ``finish()`` is entered, before it enqueues anything:
+it completes when the backward's last compute kernel does.  ``exposed_ms()`` is then the time the exchange
+ran past the end of the backward (what the backward did not hide), and ``backward_ms()`` the forward +
+backward time of the step with the exchange running beside it -- compared with the same figure at N = 1 it
+shows how much the concurrent collectives slowed the compute itself (bench.py reports both per rank).
 """
 from __future__ import annotations
 
@@ -164,13 +168,19 @@ class GradAllReducer:
         from ..miaudio import kernels as K
         if id(param) not in self.index or id(param) in self.done or not K.defers_to_fused_adam(param):
             return False
+        if param.grad is not None:  # an accumulated gradient is there: materialise and add, as one GPU does
+            return False
+        if self.world & (self.world - 1):
+            # dY / world is exact in bf16 only for a power-of-two world; otherwise the f32 all-reduce path
+            # (no extra rounding) carries this gradient
+            return False
         B, M = dy.shape
         N = x.shape[1]
         dy_all = torch.empty(self.world * B, M, dtype=dy.dtype, device=dy.device)
         x_all = torch.empty(self.world * B, N, dtype=x.dtype, device=x.device)
 
         def run():
-            dys = dy * (1.0 / self.world)  # exact in bf16 for a power-of-two world
+            dys = dy * (1.0 / self.world)  # exact in bf16: the world is a power of two (checked above)
             self._all_gather(dy_all, dys)
             self._all_gather(x_all, x)
             return dys
@@ -191,11 +201,27 @@ class GradAllReducer:
         self.gathered_param_bytes += param.numel() * 4
         return True
 
+    def begin_step(self):
+        """Record the step-start event (timing on, CUDA only); call before the forward."""
+        self._t_start = None
+        if self.cuda and self.timing is not None:
+            self._t_start = torch.cuda.Event(enable_timing=True)
+            self._t_start.record(torch.cuda.current_stream())
+
     def exposed_ms(self):
-        """Mean over the recorded steps of the time the exchange ran past the end of the backward."""
+        """Mean over the recorded steps of the time the exchange ran past the end of the backward's last
+        compute kernel."""
         if not self.timing:
             return None
-        ts = [max(0.0, e0.elapsed_time(e1)) for e0, e1 in self.timing]
+        ts = [max(0.0, e0.elapsed_time(e1)) for _, e0, e1 in self.timing]
+        return sum(ts) / len(ts)
+
+    def backward_ms(self):
+        """Mean over the recorded steps of step start -> the backward's last compute kernel (None unless every
+        step called begin_step)."""
+        if not self.timing or any(s is None for s, _, _ in self.timing):
+            return None
+        ts = [s.elapsed_time(e0) for s, e0, _ in self.timing]
         return sum(ts) / len(ts)
 
     def finish(self):
@@ -219,7 +245,8 @@ class GradAllReducer:
         if t0 is not None:
             t1 = torch.cuda.Event(enable_timing=True)
             t1.record(self.stream)
-            self.timing.append((t0, t1))
+            self.timing.append((getattr(self, "_t_start", None), t0, t1))
+            self._t_start = None
         if self.cuda:
             torch.cuda.current_stream().wait_stream(self.stream)
         if self.gathers:

@@ -156,8 +156,14 @@ class Trainer:
     def __init__(self, max_epochs=1, accelerator="auto", precision=32, devices=1, log_every_n_steps=50,
                  gradient_clip_val=0.0, logger=None, callbacks=None, limit_train_batches=None,
                  limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, fc1_exchange="gather",
-                 **unused):
+                 dist_backend="nccl", **unused):
         self.fc1_exchange = str(fc1_exchange)  # DDP: how FC1's deferred weight gradient crosses ranks (ddp.py)
+        # DDP process-group backend: "nccl" (= RCCL over xGMI, the product path, one GPU per rank) or "gloo"
+        # (ranks may share a GPU: the one-GPU rehearsal of configs 4/5's data-parallel legs; GPU tensors cross
+        # through host memory, so it is never the benched path)
+        self.dist_backend = str(dist_backend)
+        if self.dist_backend not in ("nccl", "gloo"):
+            raise ValueError(f"trainer.dist_backend must be 'nccl' or 'gloo', not {dist_backend!r}")
         self.max_epochs = int(max_epochs)
         self.gradient_clip_val = float(gradient_clip_val or 0.0)
         self.precision = str(precision)
@@ -178,11 +184,18 @@ class Trainer:
         use_gpu = accelerator in ("gpu", "cuda") or (accelerator == "auto" and torch.cuda.is_available())
         if accelerator == "cpu":
             use_gpu = False
-        self.device = torch.device("cuda", self.local_rank) if use_gpu else torch.device("cpu")
+        gpu_index = self.local_rank
+        if use_gpu and self.dist_backend == "gloo":
+            # rehearsal: more ranks than GPUs share them round-robin (RCCL refuses two ranks on one device)
+            gpu_index %= max(1, torch.cuda.device_count())
+        self.device = torch.device("cuda", gpu_index) if use_gpu else torch.device("cpu")
         if self.world > 1 and not dist.is_initialized():
             if use_gpu:
                 torch.cuda.set_device(self.device)
-                dist.init_process_group("nccl", device_id=self.device)
+                if self.dist_backend == "nccl":
+                    dist.init_process_group("nccl", device_id=self.device)
+                else:
+                    dist.init_process_group("gloo")
             else:
                 dist.init_process_group("gloo")
         self.is_global_zero = self.rank == 0

@@ -476,9 +476,11 @@ int mia_attn_bwd(const void* qkv, const void* out, const void* dout, const float
                  void* dqkv, void* work, int32_t dtype, int32_t B, int32_t N, int32_t H,
                  float scale, mia_stream_t stream);
 /* Training form (bf16): mia_attn_fwd_save_q is mia_attn_fwd (q8 / s8 NULL) or mia_attn_fwd_mx (both
- * set) that also writes the backward's scaled query operand Q' into `work` (a workspace of
- * mia_attn_bwd_workspace_bytes, kept from the forward to the backward); mia_attn_bwd_saved_q is
- * mia_attn_bwd (bf16) on such a workspace: its prep pass neither re-reads q nor rewrites Q'. */
+ * set) that also writes the backward's scaled query operand Q' into `work` (at least
+ * mia_attn_saved_q_bytes: Q' + the row-constant fragments, kept from the forward to the backward; the
+ * one-pass backward's flags and running sums are not part of it); mia_attn_bwd_saved_q is the two-kernel
+ * mia_attn_bwd (bf16) on such a workspace: neither re-reads q nor rewrites Q'. */
+int64_t mia_attn_saved_q_bytes(int32_t B, int32_t N, int32_t H);
 int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void* q8, void* s8, void* work, int32_t B,
                         int32_t N, int32_t H, float scale, mia_stream_t stream);
 int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
@@ -550,6 +552,12 @@ int mia_spec_augment_mixup(const float* spec, const float* pool, float* out, int
                            int32_t T, const int32_t* t0, const int32_t* tlen, const int32_t* f0,
                            const int32_t* flen, const int32_t* partner, const float* lam,
                            mia_stream_t stream);
+
+/* dst <- src (`bytes`, a multiple of 16, 16-B aligned): a plain streaming copy, non-temporal.  Not on the
+ * training path: bench.py times it in the same process as the box's HBM calibration (read + write GB/s of
+ * a 2 GB stream), so a kernel's achieved bandwidth can be read against both the 8 TB/s spec and the rate
+ * this box's HBM actually streams at (`frac_vs_box`). */
+int mia_stream_copy(const void* src, void* dst, int64_t bytes, mia_stream_t stream);
 
 const char* mia_last_error_string(void);
 int mia_device_arch(char* buf, int32_t len); /* gcnArchName of the current device */
