@@ -30,6 +30,28 @@ def _s():
     return L.stream_ptr()
 
 
+_ATTN_ERR: dict = {}
+
+
+def attn_err_word(device) -> torch.Tensor:
+    """The sticky error word of the one-pass attention backward on ``device`` (mia_attn_bwd_onepass: a bounded
+    hand-off wait that gave up sets it; the library never clears it)."""
+    key = str(device)
+    w = _ATTN_ERR.get(key)
+    if w is None:
+        w = _ATTN_ERR[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return w
+
+
+def check_attention_errors() -> None:
+    """Raise if any one-pass attention backward since start-up gave up a hand-off wait (its dQ was invalid).
+    Host sync: call at epoch ends / the end of a benchmark, not per step."""
+    for key, w in _ATTN_ERR.items():
+        if int(w.item()) != 0:
+            raise RuntimeError(f"attention backward on {key}: a dQ hand-off wait timed out (mia_attn_bwd_onepass); "
+                               "the gradients of that step are invalid")
+
+
 # ------------------------------------------------------------------------------------ GEMM
 def dense(t: torch.Tensor, layout: int, rows: int, cols: int, ld: int | None = None,
           pre: int = L.PRE_NONE, scale=None, shift=None, dtype: int | None = None) -> L.MiaOperand:

@@ -118,6 +118,8 @@ SIGNATURES = {
     "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_workspace_bytes": (C.c_int64, [i32, i32, i32, i32]),
     "mia_attn_saved_q_bytes": (C.c_int64, [i32, i32, i32]),
+    "mia_attn_bwd_chain_bytes": (C.c_int64, [i32, i32, i32]),
+    "mia_attn_bwd_onepass": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),
     "mia_attn_fwd_save_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_saved_q": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_two_pass": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),

@@ -70,6 +70,9 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
 
 
 ATTN_SAVE_Q = True  # bf16 training: the attention forward writes Q' for the backward (mia_attn_fwd_save_q)
+# bf16 training backward: the one-pass kernel (mia_attn_bwd_onepass, no S / dP recompute) or the two-kernel
+# form (mia_attn_bwd_saved_q); tools flip this for A/B runs
+ATTN_ONEPASS = True
 
 
 def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None,
@@ -266,7 +269,14 @@ class ASTFunction(torch.autograd.Function):
             work = sb["attn_work"]
             with K.probe("attn.bwd", 8.0 * B * Hh * N * N * (D // Hh),  # 2x fwd, recompute not credited
                          (2 * dqkv.numel() + 2 * da.numel()) * dqkv.element_size()):
-                if work is not None:  # Q' already written by the forward
+                if work is not None and ATTN_ONEPASS:  # Q' already written by the forward
+                    chain = torch.empty(int(L.load().mia_attn_bwd_chain_bytes(B, N, Hh)), dtype=torch.uint8, device=dev)
+                    L.check(L.load().mia_attn_bwd_onepass(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
+                                                          sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(),
+                                                          chain.data_ptr(), K.attn_err_word(dev).data_ptr(), B, N, Hh,
+                                                          s["scale"], 1, L.stream_ptr()), "mia_attn_bwd_onepass")
+                    del chain
+                elif work is not None:
                     L.check(L.load().mia_attn_bwd_saved_q(sb["qkv"].data_ptr(), sb["a"].data_ptr(), da.data_ptr(),
                                                           sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), B, N,
                                                           Hh, s["scale"], L.stream_ptr()), "mia_attn_bwd_saved_q")

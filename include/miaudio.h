@@ -495,6 +495,20 @@ int mia_attn_bwd_two_pass(const void* qkv, const void* out, const void* dout, co
 int mia_attn_bwd_fused(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                        void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
                        mia_stream_t stream);
+/* The default bf16 training backward: one pass, no recompute (S, dP, dS once per tile; dV, dK in registers;
+ * dQ = dS K summed over the 128-key blocks of each (b, h) by an ordered hand-off of running f32 sums:
+ * bit-reproducible).  Replaces F.scaled_dot_product_attention's backward inside timm's Attention
+ * (reference src/models/ast.py:60-61).
+ * saved: mia_attn_saved_q_bytes (Q' -- already there when q_ready, from mia_attn_fwd_save_q -- and the
+ *   row-constant fragments, written here); chain: mia_attn_bwd_chain_bytes of scratch for this call only
+ *   (hand-off flags + running sums; both 256-B aligned).
+ * err: a caller-owned u32, zero before the first call and never cleared by the library: a bounded hand-off
+ *   wait that gave up sets it to 1 (that call's dQ is invalid; every later call's waits give up at once).
+ *   Check it at a convenient sync point; no wait ever hangs the GPU. */
+int64_t mia_attn_bwd_chain_bytes(int32_t B, int32_t N, int32_t H);
+int mia_attn_bwd_onepass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                         void* saved, void* chain, uint32_t* err, int32_t B, int32_t N, int32_t H, float scale,
+                         int32_t q_ready, mia_stream_t stream);
 /* Byte offset in the bf16 workspace of a u32 error word: 0 after a fused backward = every dQ hand-off
  * matched; non-zero = a bounded wait gave up and that call's dQ is not valid. */
 int64_t mia_attn_bwd_error_offset(int32_t B, int32_t N, int32_t H);

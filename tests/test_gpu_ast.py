@@ -331,3 +331,51 @@ def test_attention_bwd_fused_vs_two_pass(cuda, B, N, H):
             assert rel(d[i], ref) < 6e-2, (name, "qkv"[i], rel(d[i], ref))
     # the two forms differ only in summation order (and the f32 path of dS into dQ)
     print(f"fused vs two-pass max rel {rel(res['fused'].float(), res['two'].float()):.3g}")
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 1645, 3), (1, 300, 2), (3, 1000, 2), (1, 2050, 1), (2, 777, 2), (4, 64, 3),
+                                   (1, 128, 2), (1, 129, 1), (1, 385, 2), (2, 37, 1)])
+def test_attention_bwd_onepass_vs_two_pass(cuda, B, N, H):
+    """The default training backward (mia_attn_bwd_onepass: S, dP, dS once per tile; dQ summed over the 128-key
+    blocks by the ordered hand-off of running sums) against float64 and the two-kernel form: within the bf16
+    bounds of test_attention_fwd_bwd, bit-identical from call to call (fixed summation order), the sticky
+    error word still 0 (every bounded hand-off wait matched), nothing written outside dqkv.  The shapes cover
+    the rotation lags 3 (N 385), 2 (N 1645, the benched length), 1 (N 300, 2050: 2 does not fit) and a single
+    key block (N <= 128)."""
+    g = torch.Generator().manual_seed(N * 5 + H)
+    qkv = (torch.randn(B, N, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B, N, H * 64, generator=g).to(torch.bfloat16)
+    q, k, v, o = _attn_ref(qkv, B, N, H)
+    o.backward(dout.double().view(B, N, H, 64).permute(0, 2, 1, 3))
+    lib, s = L.load(), L.stream_ptr()
+    tq, td = qkv.to(cuda), dout.to(cuda)
+    out = torch.empty(B, N, H * 64, dtype=torch.bfloat16, device=cuda)
+    lse = torch.empty(B, H, N, device=cuda)
+    saved = torch.full((int(lib.mia_attn_saved_q_bytes(B, N, H)),), 255, dtype=torch.uint8, device=cuda)
+    L.check(lib.mia_attn_fwd_save_q(tq.data_ptr(), out.data_ptr(), lse.data_ptr(), None, None, saved.data_ptr(), B, N,
+                                    H, 0.125, s), "fwd_save_q")
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    res = {}
+    for name in ("one", "one2", "two"):
+        full = torch.full((B * N * 3 * H * 64 + 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        dq = full[:B * N * 3 * H * 64]
+        if name == "two":
+            L.check(lib.mia_attn_bwd_saved_q(tq.data_ptr(), out.data_ptr(), td.data_ptr(), lse.data_ptr(),
+                                             dq.data_ptr(), saved.data_ptr(), B, N, H, 0.125, s), "two")
+        else:
+            chain = torch.full((int(lib.mia_attn_bwd_chain_bytes(B, N, H)),), 255, dtype=torch.uint8, device=cuda)
+            L.check(lib.mia_attn_bwd_onepass(tq.data_ptr(), out.data_ptr(), td.data_ptr(), lse.data_ptr(),
+                                             dq.data_ptr(), saved.data_ptr(), chain.data_ptr(), err.data_ptr(), B, N,
+                                             H, 0.125, 1, s), "onepass")
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert torch.isnan(full[-64:].float()).all()
+        res[name] = dq.view(B, N, 3, H, 64).clone()
+    assert torch.equal(res["one"], res["one2"])
+    for name in ("one", "two"):
+        d = res[name].permute(2, 0, 3, 1, 4)
+        for i, ref in enumerate((q.grad, k.grad, v.grad)):
+            assert rel(d[i], ref) < 6e-2, (name, "qkv"[i], rel(d[i], ref))
+    e = rel(res["one"].float(), res["two"].float())
+    print(f"one-pass vs two-pass max rel {e:.3g}")
+    assert e < 5e-3, e

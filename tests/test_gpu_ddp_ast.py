@@ -56,6 +56,14 @@ def _worker(rank, world, port, compute, q):
         step()
         plain = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         m.zero_grad(set_to_none=True)
+        step()  # the same step again: the plain gradients must be bit-reproducible (else nothing below can hold)
+        nondet = [n for n, p in m.named_parameters() if not torch.equal(p.grad, plain[n])]
+        m.zero_grad(set_to_none=True)
+        same_init = []
+        for n, p in m.named_parameters():  # identical initial weights on both ranks (the reducer broadcasts rank 0's)
+            parts = [torch.empty_like(p.detach(), device="cpu") for _ in range(world)]
+            dist.all_gather(parts, p.detach().cpu())
+            same_init.append(torch.equal(parts[0], parts[1]))
         opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4, clip=1.0)
         red = GradAllReducer(m, world)
         step()
@@ -78,11 +86,11 @@ def _worker(rank, world, port, compute, q):
             parts = [torch.empty_like(v) for _ in range(world)]
             dist.all_gather(parts, v)
             same.append(torch.equal(parts[0], parts[1]))
-        q.put((rank, red.last_fired, len(plain), nz, mism, all(same), None))
+        q.put((rank, red.last_fired, len(plain), nz, mism, all(same), (nondet[:5], all(same_init)), None))
         dist.destroy_process_group()
     except Exception:
         import traceback
-        q.put((rank, 0, 0, 0, [], False, traceback.format_exc()))
+        q.put((rank, 0, 0, 0, [], False, None, traceback.format_exc()))
 
 
 @pytest.mark.timeout(600)
@@ -101,8 +109,11 @@ def test_grad_allreducer_ast_two_ranks(compute):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for r, (fired, nparam, nz, mism, same, err) in res.items():
+    for r, (fired, nparam, nz, mism, same, diag, err) in res.items():
         assert err is None, (r, err)
+        nondet, same_init = diag
+        assert not nondet, f"rank {r}: plain AST {compute} gradients differ between two identical steps: {nondet}"
+        assert same_init, f"rank {r}: the ranks built different initial weights"
         assert fired > 0, "no gradient left through _grad_ready inside the AST backward"
         assert nparam > 20 and nz > nparam // 2, (nparam, nz)
         assert not mism, (r, mism[:5])

@@ -160,6 +160,23 @@ def test_attention_benched_grid_b256_h12(cuda):
     assert int(work[off:off + 4].view(torch.int32).item()) == 0
     e = float((dq2.float() - dq.float()).abs().max() / dq.float().abs().max())
     assert e < 5e-3, e
+    # the default training backward (one pass, 13 key blocks of 128 per (b, h) handing dQ on at lag 2): the
+    # sticky error word still 0, bit-identical from call to call, the two-kernel result up to summation order
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    chain = torch.empty(int(lib.mia_attn_bwd_chain_bytes(B, N, H)), dtype=torch.uint8, device=cuda)
+    ones = []
+    for _ in range(2):
+        d1 = torch.full_like(qkv, float("nan"))
+        L.check(lib.mia_attn_bwd_onepass(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+                                         d1.data_ptr(), work.data_ptr(), chain.data_ptr(), err.data_ptr(), B, N, H,
+                                         0.125, 1, s), "bwd_onepass")
+        ones.append(d1)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(ones[0], ones[1])
+    e = float((ones[0].float() - dq.float()).abs().max() / dq.float().abs().max())
+    assert e < 5e-3, e
+    del chain, ones
     qkv4 = qkv.view(B, N, 3, H, 64)
     for b, h in [(0, 0), (1, 11), (97, 5), (128, 0), (200, 7), (255, 11)]:
         q, k, v = (qkv4[b, :, i, h].double().requires_grad_(True) for i in range(3))

@@ -24,11 +24,17 @@ lib, s = L.load(), L.stream_ptr()
 work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H)), dtype=torch.uint8, device=dev)
 L.check(lib.mia_attn_fwd_save_q(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), None, None, work.data_ptr(), B, N, H,
                                 D ** -0.5, s), "fwd")
-dq = {k: torch.empty_like(qkv) for k in ("fused", "two")}
+dq = {k: torch.empty_like(qkv) for k in ("fused", "two", "one")}
+chain = torch.empty(int(lib.mia_attn_bwd_chain_bytes(B, N, H)), dtype=torch.uint8, device=dev)
+err = torch.zeros(1, dtype=torch.int32, device=dev)
 
 
 def run(name):
-    if name == "fused":
+    if name == "one":
+        L.check(lib.mia_attn_bwd_onepass(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+                                         dq[name].data_ptr(), work.data_ptr(), chain.data_ptr(), err.data_ptr(), B, N,
+                                         H, D ** -0.5, 1, s), name)
+    elif name == "fused":
         L.check(lib.mia_attn_bwd_fused(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
                                        dq[name].data_ptr(), work.data_ptr(), B, N, H, D ** -0.5, 1, s), name)
     else:
@@ -45,9 +51,11 @@ torch.cuda.synchronize()
 print("fused error word", int(work[off:off + 4].view(torch.int32).item()), flush=True)
 d = (dq["fused"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
 print(f"fused vs two-pass: max |d| / max {float(d):.3g}", flush=True)
+d = (dq["one"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
+print(f"one-pass vs two-pass: max |d| / max {float(d):.3g}, error word {int(err.item())}", flush=True)
 flop = 8.0 * B * H * N * N * D  # 2x the forward, recompute not credited
 for r in range(ROUNDS):
-    for name in ("two", "fused"):
+    for name in os.environ.get("VARIANTS", "two,fused,one").split(","):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(ITERS):
