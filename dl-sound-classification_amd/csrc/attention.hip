@@ -16,285 +16,9 @@
 
 #include <type_traits>
 
+#include "attn_common.h"
+
 namespace {
-
-constexpr int D = 64;
-constexpr int LROW = 72;  // LDS row stride in bf16 (144 B): conflict-free ds_read_b128 rows
-// Stride of a tile read ONLY transposed (forward V): 96 bf16 = 48 dwords puts the 4 rows of one
-// ds_read_b64_tr_b16 group on disjoint 16-bank windows (rows 0..3 -> banks 0, 48, 32, 16); at the
-// 36-dword LROW stride rows r and r + 2 overlap by 8 banks (2-way conflicts, SQ_LDS_BANK_CONFLICT).
-constexpr int VROW = 96;
-constexpr float LOG2E = 1.4426950408889634f;
-
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-// 64 rows x 64 bf16 from global (row stride `ld` elements) into LDS [64][LROW]; rows >= nvalid -> 0
-__device__ __forceinline__ void stage64(bf16* lds, const bf16* g, int64_t ld, int nvalid, int t) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int c = t + 256 * s;
-    const int row = c >> 3, c16 = c & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row < nvalid) v = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
-    *reinterpret_cast<uint4*>(lds + row * LROW + c16 * 8) = v;
-  }
-}
-
-__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int sw_off(int r, int col) { return r * 64 + (((col >> 3) ^ swz(r)) << 3) + (col & 7); }
-
-// Register-staged tile copy, split so the global loads of tile t+1 fly under tile t's MFMAs
-// (issue early / write late): 64 rows x 64 bf16 = 2 x 16 B per thread.
-struct Stage64 {
-  uint4 v[2];
-  // rows >= nvalid re-read the last valid row (finite data; the scores of such keys are masked to
-  // -inf so their V rows meet p = 0): an unconditional load keeps hipcc from branching around it
-  __device__ __forceinline__ void load(const bf16* g, int64_t ld, int nvalid, int t) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = t + 256 * s;
-      const int row = min(c >> 3, nvalid - 1), c16 = c & 7;
-      v[s] = *reinterpret_cast<const uint4*>(g + row * ld + c16 * 8);
-    }
-  }
-  __device__ __forceinline__ void store_sw(bf16* lds, int t) const {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = t + 256 * s;
-      const int r = c >> 3;
-      *reinterpret_cast<uint4*>(lds + r * 64 + (((c & 7) ^ swz(r)) << 3)) = v[s];
-    }
-  }
-  template <int ROW = LROW>
-  __device__ __forceinline__ void store(bf16* lds, int t) const {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = t + 256 * s;
-      *reinterpret_cast<uint4*>(lds + (c >> 3) * ROW + (c & 7) * 8) = v[s];
-    }
-  }
-};
-
-// Row fragment: tile[row][16ks + 8h + j], j = 0..7 (A operand rows / B operand columns).
-__device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int ks, int lane) {
-  return *reinterpret_cast<const bf16x8*>(lds + row * LROW + ks * 16 + 8 * (lane >> 5));
-}
-
-// Transposed fragment in the accumulator k-order: element j = tile[k0 + 8(j>>2) + 4h + (j&3)][c0 + (lane&31)]
-// (two ds_read_b64_tr_b16: 4 consecutive tile rows x 16 columns per 16-lane group).
-template <int ROW = LROW>
-__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int k0, int c0, int lane) {
-  const int i16 = lane & 15, g = lane >> 4, h = lane >> 5;
-  const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
-  const int r = k0 + 4 * h + (i16 >> 2);
-  const bf16* p0 = lds + r * ROW + col;
-  const bf16* p1 = p0 + 8 * ROW;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(p1));
-  s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, c);
-}
-
-// Swizzled [rows][64] bf16 tile for a tile read BOTH as rows (ds_read_b128) and transposed
-// (ds_read_b64_tr_b16): 16-B chunk c of row r sits at chunk c ^ swz(r).  Rows r, r + 1 use opposite
-// bank halves (128-B rows); over the 8 same-parity rows of a ds_read_b128 16-lane group swz takes 8
-// distinct values, and rows r, r + 2 of a transposed read differ in swz bit 2, so their 4-chunk
-// column blocks land in opposite 64-B halves: both kinds of read are conflict-free, no padding.
-
-__device__ __forceinline__ bf16x8 frag_row_sw(const bf16* lds, int row, int ks, int lane) {
-  return *reinterpret_cast<const bf16x8*>(lds + sw_off(row, ks * 16 + 8 * (lane >> 5)));
-}
-
-__device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* lds, int k0, int c0, int lane) {
-  const int i16 = lane & 15, g = lane >> 4, h = lane >> 5;
-  const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
-  const int r = k0 + 4 * h + (i16 >> 2);
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(lds + sw_off(r, col)));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MIA_LDS s16x4*)(lds + sw_off(r + 8, col)));
-  s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, c);
-}
-
-// Make the compiler wait for global loads of loop-invariant fragments HERE (before the tile loop): otherwise
-// it re-checks them with a vmcnt at the loop head of every iteration, and vmcnt also counts the loop's
-// own in-flight tile DMAs (lds_dma16), so every tile would wait for its successor's load.
-template <int n>
-__device__ __forceinline__ void settle(const bf16x8 (&f)[n]) {
-#pragma unroll
-  for (int i = 0; i < n; ++i) asm volatile("" ::"v"(f[i]));
-}
-__device__ __forceinline__ void settle1(const bf16x8& f) { asm volatile("" ::"v"(f)); }
-
-// accumulator registers 8s..8s+7 -> bf16 operand fragment
-__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
-  bf16x8 f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (bf16)a[8 * s + j];
-  return f;
-}
-
-__device__ __forceinline__ bf16x8 load_frag_global(const bf16* row, int ks, int lane, bool valid) {
-  if (!valid) {
-    bf16x8 z;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-    return z;
-  }
-  return *reinterpret_cast<const bf16x8*>(row + ks * 16 + 8 * (lane >> 5));
-}
-
-// v_max3_f32 as one instruction: fmaxf on MFMA results otherwise gets a canonicalising v_max per
-// operand (IEEE mode) and no max3 fusion
-__device__ __forceinline__ float max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-// max(x[lane], x[lane ^ 32]) without an LDS round trip (v_permlane32_swap exchanges the halves)
-__device__ __forceinline__ float half_exchange_max(float x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
-}
-__device__ __forceinline__ float half_exchange_sum(float x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-}
-
-// row index of accumulator register r for this lane half
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
-
-// ------------------------------------------------------------------------------ forward
-// XCD-aware block order: consecutive work items (the query blocks of one (b, h), which stream the
-// same K/V) land on ONE XCD so K/V come from that XCD's L2, not from HBM once per XCD.  Blocks are
-// dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so slot s of XCD x
-// takes work item x * (total / 8) + s.  Pure speed mapping: any placement gives the same result.
-__device__ __forceinline__ int xcd_work_item(int L, int total) {
-  return (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
-}
-
-// Tiles s0 .. ntiles - 1 of a 3-slot ring with no remainder code: the last round's second and third
-// tiles are guarded inside the loop (wave-uniform branches), so every tile is the loop's own code and
-// register allocation (straight-line remainder copies spilled)
-template <int S0, class Body>
-__device__ __forceinline__ void ring3_guarded(int s0, int ntiles, Body&& body) {
-  using F = std::false_type;
-  using C0 = std::integral_constant<int, S0 % 3>;
-  using C1 = std::integral_constant<int, (S0 + 1) % 3>;
-  using C2 = std::integral_constant<int, (S0 + 2) % 3>;
-  for (int j = s0; j < ntiles; j += 3) {
-    body(F{}, C0{}, j);
-    if (j + 1 < ntiles) body(F{}, C1{}, j + 1);
-    if (j + 2 < ntiles) body(F{}, C2{}, j + 2);
-  }
-}
-
-// Tiles s0 .. ntiles - 1 of a 3-slot LDS ring (K/V or Q/dO tiles arrive by LDS-DMA two tiles ahead of
-// their use), slot = tile % 3 as a compile-time constant (tile s0's slot is S0 % 3, so every LDS address
-// is base + immediate); the last tile is the TAIL form when `tail`.  body(tail_t, slot_t, j).
-template <int S0, class Body>
-__device__ __forceinline__ void ring3(int s0, int ntiles, bool tail, Body&& body) {
-  using T = std::true_type;
-  using F = std::false_type;
-  using C0 = std::integral_constant<int, S0 % 3>;
-  using C1 = std::integral_constant<int, (S0 + 1) % 3>;
-  using C2 = std::integral_constant<int, (S0 + 2) % 3>;
-  int j = s0;
-  for (; j + 3 < ntiles; j += 3) {
-    body(F{}, C0{}, j);
-    body(F{}, C1{}, j + 1);
-    body(F{}, C2{}, j + 2);
-  }
-  const int r = ntiles - j;
-  if (r == 1) {
-    if (tail) body(T{}, C0{}, j);
-    else body(F{}, C0{}, j);
-  } else if (r == 2) {
-    body(F{}, C0{}, j);
-    if (tail) body(T{}, C1{}, j + 1);
-    else body(F{}, C1{}, j + 1);
-  } else if (r == 3) {
-    body(F{}, C0{}, j);
-    body(F{}, C1{}, j + 1);
-    if (tail) body(T{}, C2{}, j + 2);
-    else body(F{}, C2{}, j + 2);
-  }
-}
-
-// Forward structure (the loop is vector-issue bound at head dim 64, so the design is a VALU diet):
-//  * one wave = 32 queries (query on the lane), 4 waves = 128 queries per block, <= 168 registers so
-//    three waves share each SIMD and one wave's softmax issues beside the others' MFMAs;
-//  * K / V tiles arrive by LDS-DMA (global_load_lds_dwordx4, no staging registers, no ds_write),
-//    double-buffered: tile j+1 is requested before tile j is computed;
-//  * Q is pre-scaled by scale * log2(e) (bf16) and the running max m is rounded UP to a
-//    bf16-representable value, so "- m" rides the QK^T MFMA chain as a fifth k-step
-//    (ones column of K x (-m) row of Q): the scores leave the MFMA as s - m, p = exp2(.) directly;
-//  * the running max is not recomputed per tile: m only has to keep every p finite and O in range,
-//    so a tile whose exp-sum stays <= 2^16 (each p <= 2^16) is accepted as is, and only a tile that
-//    exceeds it (or the first tile) takes the wave-uniform rare path that computes the tile max,
-//    moves m, rescales O / l and recomputes the tile's p.
-constexpr int FWD_Q = 128;
-constexpr float FWD_SUM_LIMIT = 65536.f;
-
-typedef __attribute__((address_space(3))) void* lds_vp;
-typedef const __attribute__((address_space(1))) void* glb_vp;
-
-// 16 B per lane from a buffer into LDS (buffer_load_dwordx4 ... lds, M0 = the wave's LDS destination) as
-// inline asm: issued through the builtin, the compiler treats the in-flight DMA as a possible writer of
-// every LDS location and puts vmcnt(0) in front of the next ds_read -- in these kernels the NEXT tile's
-// DMA, so every tile waited for its successor's load.  Here the kernels' own counted vmcnt + barrier
-// order the DMA against its readers (each issue site says which), and M0 is saved and restored.
-__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, const void* lds, unsigned voff, unsigned soff) {
-  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_vp)lds);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(a), "v"(voff), "s"(rsrc), "s"(soff)
-      : "memory");
-}
-
-// x rounded toward +inf to a bf16-representable float (its negation is exact in bf16)
-__device__ __forceinline__ float bf16_ceil(float x) {
-  unsigned u = __builtin_bit_cast(unsigned, x);
-  if (!(u & 0x80000000u)) u += 0xFFFFu;
-  return __builtin_bit_cast(float, u & 0xFFFF0000u);
-}
-
-// One 64-row x 64-col bf16 tile (8 KB, sw_off layout) by LDS-DMA: 8 pieces of 1 KB = 8 rows each,
-// wave w issues pieces 2w and 2w + 1; lane i of a piece fills 16-B slot (i & 7) of row 8p + (i >> 3),
-// i.e. it loads chunk (i & 7) ^ swz(row) of that row (the swizzle rides the SOURCE address).  Buffer
-// loads: the per-lane byte offset is fixed, the tile start rides soffset (no VALU per tile), and rows
-// past the sequence end fall outside the descriptor's range and read as zeros (their keys are masked,
-// their V rows meet p = 0).
-struct TileDMA {
-  __amdgpu_buffer_rsrc_t rsrc;
-  unsigned voff[2];
-  __device__ __forceinline__ void init(const bf16* g, int64_t ld, int N, int wave, int lane) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(((int64_t)(N - 1) * ld + 64) * 2), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = 8 * (2 * wave + i) + (lane >> 3);
-      voff[i] = (unsigned)((r * (int)ld + ((lane & 7) ^ swz(r)) * 8) * 2);
-    }
-  }
-  __device__ __forceinline__ void issue(bf16* tile, unsigned row0_bytes, int wave) const {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) lds_dma16(rsrc, tile + (2 * wave + i) * 512, voff[i], row0_bytes);
-  }
-};
 
 // S^T - m for one 64-key tile: [key half] accumulators (rows = keys, lane column = query)
 __device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const bf16* K_, const bf16x8 (&qf)[4], bf16x8 one,
@@ -499,90 +223,6 @@ template __global__ void attn_fwd_kernel<false>(const bf16*, bf16*, float*, int,
 template __global__ void attn_fwd_kernel<true>(const bf16*, bf16*, float*, int, int, int, float, uint8_t*, uint8_t*,
                                                bf16*);
 
-// ------------------------------------------------------------------------------ backward
-// Both backward kernels recompute P from the SAME MFMA operands the forward used (Q' = bf16(q * scale
-// * log2 e) against K), so P sums to one exactly as the forward's lse normalised it.  The per-query
-// row constants ride the MFMA chains as a fifth k-step, each split into three bf16 parts (exact to
-// f32): S' = Q'K^T - L2 (L2 = lse * log2 e) gives p = exp2(S') directly, and dP' = dO V^T - delta
-// gives dS = p * dP' with one multiply.
-//
-// prep: per (b, q, h) row, Q' (B, N, H, 64) bf16 and the fragment rows (B*H, 2, N, 8) bf16:
-// part 0 = [-L2 (3 parts), 0 x 5], part 1 = [-delta (3 parts), 0 x 5], delta = sum_d dO * O.
-// 8 lanes per row.
-// x = h + m + l (three bf16 parts, exact to f32 rounding) into elements 0..2 of f
-__device__ __forceinline__ void split3(float x, bf16x8& f) {
-  const bf16 h = (bf16)x;
-  const float r1 = x - (float)h;
-  const bf16 m = (bf16)r1;
-  f[0] = h;
-  f[1] = m;
-  f[2] = (bf16)(r1 - (float)m);
-}
-
-__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ out,
-                                                            const bf16* __restrict__ dout, const float* __restrict__ lse,
-                                                            bf16* __restrict__ qs, bf16* __restrict__ frag, int B,
-                                                            int N, int H, float scale_log2, int write_qs) {
-  const int64_t rows = (int64_t)B * N * H;
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-  const int part = threadIdx.x & 7;
-  if (i >= rows) return;  // whole 8-lane groups leave together
-  const int hd = (int)(i % H);
-  const int64_t bq = i / H;
-  const int q = (int)(bq % N), b = (int)(bq / N);
-  const bf16x8 o = *reinterpret_cast<const bf16x8*>(out + i * D + part * 8);
-  const bf16x8 g = *reinterpret_cast<const bf16x8*>(dout + i * D + part * 8);
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s = fmaf((float)o[j], (float)g[j], s);
-  if (write_qs) {  // (skipped when the forward wrote Q': mia_attn_fwd_save_q)
-    const bf16x8 qv = *reinterpret_cast<const bf16x8*>(qkv + (bq * 3 * H + hd) * D + part * 8);
-    bf16x8 qsc;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qsc[j] = (bf16)((float)qv[j] * scale_log2);
-    *reinterpret_cast<bf16x8*>(qs + i * D + part * 8) = qsc;
-  }
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  s += __shfl_xor(s, 4);
-  if (part < 2) {
-    const int64_t bhh = (int64_t)b * H + hd;
-    const float x = part == 0 ? -lse[bhh * N + q] * LOG2E : -s;
-    bf16x8 f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (bf16)0.f;
-    split3(x, f);
-    *reinterpret_cast<bf16x8*>(frag + ((bhh * 2 + part) * N + q) * 8) = f;
-  }
-}
-
-// ones fragment for the fifth k-step: elements 0..2 of the low lane half = 1
-__device__ __forceinline__ bf16x8 ones3(int lane) {
-  bf16x8 f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (bf16)0.f;
-  if (lane < 32) { f[0] = (bf16)1.f; f[1] = (bf16)1.f; f[2] = (bf16)1.f; }
-  return f;
-}
-
-// The fragment rows of 64 queries by LDS-DMA into [part][64][8]: waves 0 and 1 issue part 0 / 1
-// (1 KB each, 16-B rows: the per-lane row reads are conflict-free).  Past the sequence end part 0
-// reads part 1's rows (finite; those queries are masked) and part 1 reads zeros.
-struct FragDMA {
-  __amdgpu_buffer_rsrc_t rsrc;
-  unsigned part_bytes;
-  __device__ __forceinline__ void init(const bf16* g, int N) {
-    part_bytes = (unsigned)N * 16;
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)(2 * part_bytes), 0x00020000);
-  }
-  __device__ __forceinline__ void issue(bf16* tile, unsigned row0, int wave, int lane) const {
-    if (wave < 2) lds_dma16(rsrc, tile + wave * 512, (unsigned)wave * part_bytes + lane * 16, row0 * 16);
-  }
-};
-
-// A fifth-k-step fragment row read by every lane: the high lane half carries k = 8..15, which meet
-// the zero half of the ones fragment, so its (finite) copy of the row contributes nothing.
-__device__ __forceinline__ bf16x8 row_frag(const bf16* row) { return *reinterpret_cast<const bf16x8*>(row); }
 
 // Key-parallel dK / dV.  One wave = 32 keys (key on the lane), 4 waves = 128 keys per block; the
 // block sweeps 64-query tiles of Q', dO and their fragment rows (LDS-DMA, double-buffered).  With
@@ -900,17 +540,6 @@ constexpr int FBL_R = FBL_S + 2 * 32768;        // [4][4096 B] key-half partials
 constexpr int FBL_FL = FBL_R + 4 * FB_SUB;      // [4] int LDS flags: partial of step j ready (j + 1)
 constexpr int FBL_BYTES = FBL_FL + 64;
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ unsigned fb_ld_flag(const unsigned* p) {
-  unsigned v;
-  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void fb_st_flag(unsigned* p, unsigned v) {
-  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-
 // wave-uniform: poll `flag` until it reads `want` (bounded; a timeout sets the error word, and once it is
 // set every later wait of the launch gives up at once, so a broken chain still drains the grid quickly)
 __device__ __forceinline__ void fb_wait(const unsigned* flag, unsigned want, unsigned* err) {
@@ -1193,292 +822,6 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(const bf16* __restr
       const uint4 v = *reinterpret_cast<const uint4*>(stg + sw_off(r, c * 8));
       if (k < N) *reinterpret_cast<uint4*>(dqkv + ((int64_t)b * N + k) * ldt + (1 + which) * H * D + hd * D + c * 8) = v;
     }
-  }
-}
-
-// ------------------------------------------------------------------------------ one-pass backward (chain)
-// The default bf16 backward.  One 4-wave workgroup per (b, h, 128-key block), two workgroups per CU (LDS
-// 68 KB, <= 256 VGPRs: each SIMD runs one wave of each of two independent workgroups, so one's softmax /
-// hand-off issues beside the other's MFMAs).  Per 64-query tile each wave (32 keys, key on the lane)
-// computes S and dP ONCE (Q' and dO row fragments from LDS against its K / V rows in registers, the row
-// constants as a fifth k-step), P and dS = P (dP - delta), accumulates dV^T += dO^T P and dK^T += Q'^T dS in
-// registers and writes dS^T (bf16) into an LDS image; after the step's one barrier wave w computes the dQ^T
-// sub-tile (d half w & 1, query half w >> 1) of the tile over the block's 128 keys (K^T fragments in
-// registers, dS^T from the image): 5 GEMM units per tile, no recompute.
-//
-// dQ sums over the key blocks of one (b, h) by an ORDERED HAND-OFF of running f32 sums (no float atomics:
-// bit-reproducible).  Block kb walks the query tiles rotated by lag * kb; a tile's contributions are added
-// in the order of the steps at which the blocks reach it; the first stores its partial, the last writes bf16
-// dQ.  Each wave owns its sub-tile's link: its `sc1` stores of the running sum (16 B per lane) are published
-// by an `sc1` flag store in the MIDDLE of the next step, behind a vmcnt wait that the step's own loads need
-// anyway (no wait for the store acknowledgement on the critical path); the successor block polls the flag
-// with an `sc1` load issued with its tile DMA at the start of the step that needs the sum, checks it in the
-// middle of that step and loads the sum (`sc1`, to registers) for the dQ phase after the barrier
-// (MI355X_MICROARCH.md, visibility table row 1: one storing wave per flag, every byte stored and loaded
-// `sc1`, the store drained before its flag).  With a lag of >= 2 steps between consecutive contributions
-// the sum is published a step before it is polled; at a lag of 1 (sequence lengths where 2 does not fit) the
-// successor waits about half a step.  A block only waits for a contribution made at an earlier step (the
-// first contribution of a tile is made at the step where it has no predecessor), the blocks of one (b, h)
-// are consecutive work items of one XCD and the workgroups are dispatched in order, so a wait always ends;
-// it is bounded anyway (CB_SPIN_TICKS of the 100 MHz counter): a timeout sets the caller's sticky error word
-// and every later wait of any call gives up at once instead of hanging the GPU.
-// Rows past the sequence end read as zeros everywhere (K / V / Q' / dO by the descriptors' ranges, the row
-// constants per part): such a key meets K = V = 0, such a query p = 1 and dP' = 0, so dS = 0 there, nothing
-// is masked and nothing past the end is stored.
-constexpr int CB_K = 128;                      // keys per workgroup: 4 waves x 32
-constexpr int CB_SUB = 4096;                   // one 32 x 32 f32 dQ^T sub-tile in register order
-constexpr int CB_TILE = 4 * CB_SUB;            // the four sub-tiles of a 64-query tile
-constexpr unsigned long long CB_SPIN_TICKS = 20000000ull;  // 200 ms at 100 MHz
-constexpr int CBL_Q = 0;                       // [2][64][64] bf16 Q' tiles (sw_off)
-constexpr int CBL_G = CBL_Q + 2 * 8192;        // [2][64][64] bf16 dO tiles (sw_off)
-constexpr int CBL_F = CBL_G + 2 * 8192;        // [2][2 parts][64][8] bf16 fifth-k-step rows
-constexpr int CBL_S = CBL_F + 2 * 2048;        // [2][128][64] bf16 dS^T (sw_off); slot 1 holds K in the prologue
-constexpr int CBL_BYTES = CBL_S + 2 * 16384;   // 69 632 B: two workgroups per CU
-
-// the row-constant fragments of 64 queries by LDS-DMA, one descriptor per part (rows past N read zeros in
-// both parts): waves 0 / 1 issue part 0 / 1
-struct FragDMA2 {
-  __amdgpu_buffer_rsrc_t rsrc;
-  __device__ __forceinline__ void init(const bf16* g, int N, int wave) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(g + (int64_t)(wave & 1) * N * 8), 0, N * 16, 0x00020000);
-  }
-  __device__ __forceinline__ void issue(bf16* tile, unsigned row0, int wave, int lane) const {
-    if (wave < 2) lds_dma16(rsrc, tile + wave * 512, lane * 16, row0 * 16);
-  }
-};
-
-__device__ __forceinline__ int cb_tile(int j, int kb, int nt, int lag) {
-  int t = (j - lag * kb) % nt;
-  return t < 0 ? t + nt : t;
-}
-// position of block kb in tile T's chain: the blocks that reach T at an earlier step
-__device__ __forceinline__ int cb_pos(int kb, int T, int nkb, int nt, int lag) {
-  auto step = [&](int k) { return (T + lag * k) % nt; };
-  const int mine = step(kb);
-  int p = 0;
-  for (int k = 0; k < nkb; ++k) p += step(k) < mine;
-  return p;
-}
-
-__device__ __forceinline__ unsigned cb_load_flag(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, 0, off, 16);  // sc1
-}
-
-// wave-uniform, bounded: until flag == want (a timeout, or an earlier one of any call, sets / reads *err)
-__device__ __forceinline__ void cb_spin(const unsigned* flag, unsigned want, unsigned* err) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (fb_ld_flag(flag) == want) return;
-    if (fb_ld_flag(err) != 0u) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > CB_SPIN_TICKS) {
-      fb_st_flag(err, 1u);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
-// S', dP' of 32 queries (half sq of the tile) x this wave's 32 keys -> P, dS; dV^T, dK^T MFMAs; dS^T -> LDS
-__device__ __forceinline__ void cb_half(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
-                                        const bf16* F_, bf16* dsT, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4],
-                                        bf16x8 one, int sq, int wave, int lane) {
-  const int qr = sq * 32 + (lane & 31);
-  const int krow = 32 * wave + (lane & 31);
-  f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), kf[0], zero16());
-  f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
-#pragma unroll
-  for (int ks = 1; ks < 4; ++ks) {
-    sc = mfma(frag_row_sw(Q_, qr, ks, lane), kf[ks], sc);
-    dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
-  }
-  sc = mfma(row_frag(F_ + qr * 8), one, sc);
-  dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float p = __builtin_amdgcn_exp2f(sc[r]);
-    sc[r] = p;
-    dp[r] *= p;
-  }
-#pragma unroll
-  for (int sk = 0; sk < 2; ++sk) {
-    const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
-    // dS^T[key][q]: elements 0..3 = queries 16 sk + 4h + 0..3, 4..7 = 16 sk + 8 + 4h + 0..3 (of this half)
-    const int qa = sq * 32 + 16 * sk + 4 * (lane >> 5);
-    *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa)) = bf16x4{df[0], df[1], df[2], df[3]};
-    *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      dv[dh] = mfma(frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane), pf, dv[dh]);
-      dk[dh] = mfma(frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane), df, dk[dh]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void attn_bwd_chain_kernel(const bf16* __restrict__ qkv,
-                                                                const bf16* __restrict__ dout,
-                                                                const bf16* __restrict__ qs,
-                                                                const bf16* __restrict__ frag,
-                                                                bf16* __restrict__ dqkv, float* chain,
-                                                                unsigned* flags, unsigned* err, int N, int H,
-                                                                int nkb, int lag, float scale, float dk_scale) {
-  __shared__ __attribute__((aligned(1024))) char lds[CBL_BYTES];
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int w = xcd_work_item(blockIdx.x, gridDim.x);  // the key blocks of one (b, h): consecutive, one XCD
-  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
-  const int nt = (N + 63) / 64;
-  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
-  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
-  bf16* const Kt = reinterpret_cast<bf16*>(lds + CBL_S + 16384);
-  // the block's 128 keys -> Kt (dS^T slot 1, first written at step 1, after every wave has read K): wave w
-  // loads its own 32 keys as 4 pieces of 8 rows; keys past N read as zeros
-  {
-    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = 32 * wave + 8 * i + (lane >> 3);
-      const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
-      lds_dma16(kr, Kt + (4 * wave + i) * 512, vo, (unsigned)((int64_t)(kb * CB_K + 32 * wave + 8 * i) * ldt * 2));
-    }
-  }
-  TileDMA qd, gd;
-  FragDMA2 fd;
-  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
-  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
-  fd.init(frag + (int64_t)bh * 2 * N * 8, N, wave);
-  auto Qb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_Q + P * 8192); };
-  auto Gb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_G + P * 8192); };
-  auto Fb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_F + P * 2048); };
-  {
-    const int T0 = cb_tile(0, kb, nt, lag);
-    qd.issue(Qb(0), (unsigned)T0 * tile_bytes, wave);
-    gd.issue(Gb(0), (unsigned)T0 * tile_bytes, wave);
-    fd.issue(Fb(0), (unsigned)T0 * 64u, wave, lane);
-  }
-  const int key = kb * CB_K + wave * 32 + (lane & 31);
-  bf16x8 vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
-  settle(vf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // K and tile 0 in LDS
-  const int dhw = wave & 1, qhw = wave >> 1;  // this wave's dQ^T sub-tile
-  bf16x8 kf[4], kt[8];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kf[ks] = frag_row_sw(Kt, 32 * wave + (lane & 31), ks, lane);
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) kt[ks] = frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane);
-  const bf16x8 one = ones3(lane);
-  f32x16 dk[2], dv[2];
-  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-  unsigned* const fl = flags + (int64_t)bh * nt * 4;
-  const __amdgpu_buffer_rsrc_t flr = __builtin_amdgcn_make_buffer_rsrc((void*)fl, 0, nt * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(chain + (int64_t)bh * nt * (CB_TILE / 4)), 0, nt * CB_TILE, 0x00020000);
-  const int last = nkb - 1;
-  bool pub = false;  // this wave stored a running sum last step: publish its flag in the middle of this step
-  int pub_T = 0;
-  unsigned pub_val = 0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K fragments in registers before slot 1 is reused
-  // one step; P = buffer parity (compile time: the loop is unrolled by 2)
-  auto step = [&](int j, auto par) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;
-    const int T = cb_tile(j, kb, nt, lag), pos = cb_pos(kb, T, nkb, nt, lag);
-    if (j + 1 < nt) {  // buffer P^1 was last read by step j - 1's body, before its barrier
-      const int T1 = cb_tile(j + 1, kb, nt, lag);
-      qd.issue(Qb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
-      gd.issue(Gb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
-      fd.issue(Fb(P ^ 1), (unsigned)T1 * 64u, wave, lane);
-    }
-    unsigned fv = 0;
-    if (pos > 0) fv = cb_load_flag(flr, (T * 4 + wave) * 4);  // this tile's predecessor (checked mid-step)
-    bf16* const dsT = reinterpret_cast<bf16*>(lds + CBL_S + P * 16384);
-    cb_half(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 0, wave, lane);
-    // mid-step: last step's running-sum stores are done (the poll needs this wait anyway): publish them;
-    // then this tile's predecessor, and its running sum into registers for the dQ phase
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
-    u32x4 run[4];
-    if (pos > 0) {
-      if (__builtin_expect(__builtin_amdgcn_readfirstlane(fv) != (unsigned)pos, 0))
-        cb_spin(fl + T * 4 + wave, (unsigned)pos, err);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * CB_TILE + wave * CB_SUB + g * 1024, 16);
-    }
-    cb_half(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 1, wave, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dS^T written; tile j + 1 landed at the mid wait
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // dQ^T sub-tile (dhw, qhw) of tile T over the block's 128 keys
-    f32x16 dq = mfma(kt[0], frag_tr_sw(dsT, 0, 32 * qhw, lane), zero16());
-#pragma unroll
-    for (int ks = 1; ks < 8; ++ks) dq = mfma(kt[ks], frag_tr_sw(dsT, 16 * ks, 32 * qhw, lane), dq);
-    if (pos > 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 r = __builtin_bit_cast(f32x4, run[g]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dq[4 * g + i] += r[i];
-      }
-    }
-    pub = false;
-    if (pos < last) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]}), cr, lane * 16,
-            T * CB_TILE + wave * CB_SUB + g * 1024, 16);
-      pub = true;
-      pub_T = T;
-      pub_val = (unsigned)(pos + 1);
-    } else {  // the last contribution: bf16 dQ rows of the sub-tile's 32 queries
-      const int q = T * 64 + 32 * qhw + (lane & 31);
-      if (q < N) {
-        bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D + 32 * dhw;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d0 = 8 * g4 + 4 * (lane >> 5);
-          *reinterpret_cast<bf16x4*>(qrow + d0) =
-              bf16x4{(bf16)(dq[4 * g4] * scale), (bf16)(dq[4 * g4 + 1] * scale), (bf16)(dq[4 * g4 + 2] * scale),
-                     (bf16)(dq[4 * g4 + 3] * scale)};
-        }
-      }
-    }
-  };
-  {
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    int j = 0;
-    for (; j + 1 < nt; j += 2) {
-      step(j, P0{});
-      step(j + 1, P1{});
-    }
-    if (j < nt) step(j, P0{});
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
-  if (key >= N) return;
-  bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
-  bf16* vrow = krow + H * D;
-#pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
-    const int d0 = 8 * g4 + 4 * (lane >> 5);
-    bf16x4 a0, a1, c0, c1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      a0[i] = (bf16)(dk[0][4 * g4 + i] * dk_scale);
-      a1[i] = (bf16)(dk[1][4 * g4 + i] * dk_scale);
-      c0[i] = (bf16)dv[0][4 * g4 + i];
-      c1[i] = (bf16)dv[1][4 * g4 + i];
-    }
-    *reinterpret_cast<bf16x4*>(krow + d0) = a0;
-    *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
-    *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
-    *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
   }
 }
 
@@ -1792,53 +1135,4 @@ extern "C" int mia_attn_fwd_save_q(const void* qkv, void* out, float* lse, void*
 extern "C" int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                                     void* work, int32_t B, int32_t N, int32_t H, float scale, mia_stream_t stream) {
   return attn_bwd_impl(qkv, out, dout, lse, dqkv, work, MIA_BF16, B, N, H, scale, 1, 0, stream);
-}
-
-// ------------------------------------------------------------------------------ one-pass backward: host side
-static int64_t cb_flags_bytes(int32_t B, int32_t N, int32_t H) {
-  return (((int64_t)B * H * cdiv(N, 64) * 4 * 4) + 255) / 256 * 256;  // [B*H][nt][4 sub-tiles] u32
-}
-// the largest rotation lag (<= 3) that leaves >= 2 steps between consecutive contributions to every tile, else 1
-static int cb_lag(int32_t N) {
-  const int nt = (int)cdiv(N, 64), nkb = (int)cdiv(N, CB_K);
-  if (nkb == 1) return 1;
-  for (int L = 3; L >= 2; --L)
-    if (nt - L * (nkb - 1) >= 2) return L;
-  return 1;
-}
-
-extern "C" int64_t mia_attn_bwd_chain_bytes(int32_t B, int32_t N, int32_t H) {
-  return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE;
-}
-
-extern "C" int mia_attn_bwd_onepass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
-                                    void* saved, void* chain, uint32_t* err, int32_t B, int32_t N, int32_t H,
-                                    float scale, int32_t q_ready, mia_stream_t stream) {
-  MIA_CHECK_ARG(qkv && out && dout && lse && dqkv && saved && chain && err, "attn_bwd_onepass: null pointer");
-  MIA_CHECK_ARG(B > 0 && N > 0 && H > 0 && (int64_t)B * H < 65536, "attn_bwd_onepass: bad shape");
-  const int64_t rows = (int64_t)B * N * H;
-  MIA_CHECK_ARG(rows * 8 < (1ll << 31), "attn_bwd_onepass: B*N*H too large");
-  MIA_CHECK_ARG((int64_t)N * 3 * H * D * 2 < (1ll << 31), "attn_bwd_onepass: one sequence must span < 2 GiB");
-  MIA_CHECK_ARG((int64_t)cdiv(N, 64) * CB_TILE < (1ll << 31), "attn_bwd_onepass: sequence too long");
-  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(saved) | reinterpret_cast<uintptr_t>(chain)) & 255) == 0,
-                "attn_bwd_onepass: saved / chain workspaces must be 256-B aligned");
-  hipStream_t s = as_stream(stream);
-  bf16* qs = (bf16*)saved;
-  bf16* frag = qs + rows * D;
-  // Q' (unless the forward wrote it) and the row-constant fragments -L2, -delta
-  attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
-                                                                     (const bf16*)dout, lse, qs, frag, B, N, H,
-                                                                     scale * LOG2E, q_ready ? 0 : 1);
-  MIA_LAUNCH_CHECK("attn_bwd_prep");
-  unsigned* flags = reinterpret_cast<unsigned*>(chain);
-  float* sums = reinterpret_cast<float*>(reinterpret_cast<char*>(chain) + cb_flags_bytes(B, N, H));
-  hipError_t e = hipMemsetAsync(flags, 0, (size_t)cb_flags_bytes(B, N, H), s);
-  if (e != hipSuccess) return mia::fail(-(int)e, "attn_bwd_onepass: memset: %s", hipGetErrorString(e));
-  const int nkb = (int)cdiv(N, CB_K);
-  MIA_CHECK_ARG((int64_t)nkb * B * H < (1ll << 31), "attn_bwd_onepass: grid too large");
-  attn_bwd_chain_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>(
-      (const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, sums, flags, err, N, H, nkb, cb_lag(N), scale,
-      1.f / LOG2E);
-  MIA_LAUNCH_CHECK("attn_bwd_chain");
-  return 0;
 }

@@ -24,14 +24,21 @@ lib, s = L.load(), L.stream_ptr()
 work = torch.empty(int(lib.mia_attn_bwd_workspace_bytes(L.BF16, B, N, H)), dtype=torch.uint8, device=dev)
 L.check(lib.mia_attn_fwd_save_q(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), None, None, work.data_ptr(), B, N, H,
                                 D ** -0.5, s), "fwd")
-dq = {k: torch.empty_like(qkv) for k in ("fused", "two", "one")}
+ALT = {}  # experiment builds of attention.hip (ATTN_LIBS=path,...): timed as "one:<stem>"
+for path in filter(None, os.environ.get("ATTN_LIBS", "").split(",")):
+    import ctypes as C
+    x = C.CDLL(str(REPO / path))
+    x.mia_attn_bwd_onepass.argtypes = L.SIGNATURES["mia_attn_bwd_onepass"][1]
+    ALT["one:" + Path(path).stem] = x
+dq = {k: torch.empty_like(qkv) for k in ("fused", "two", "one", *ALT)}
 chain = torch.empty(int(lib.mia_attn_bwd_chain_bytes(B, N, H)), dtype=torch.uint8, device=dev)
-err = torch.zeros(1, dtype=torch.int32, device=dev)
+errs = {}  # one sticky error word per one-pass variant
 
 
 def run(name):
-    if name == "one":
-        L.check(lib.mia_attn_bwd_onepass(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+    if name.startswith("one"):
+        err = errs.setdefault(name, torch.zeros(1, dtype=torch.int32, device=dev))
+        L.check(ALT.get(name, lib).mia_attn_bwd_onepass(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
                                          dq[name].data_ptr(), work.data_ptr(), chain.data_ptr(), err.data_ptr(), B, N,
                                          H, D ** -0.5, 1, s), name)
     elif name == "fused":
@@ -51,11 +58,12 @@ torch.cuda.synchronize()
 print("fused error word", int(work[off:off + 4].view(torch.int32).item()), flush=True)
 d = (dq["fused"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
 print(f"fused vs two-pass: max |d| / max {float(d):.3g}", flush=True)
-d = (dq["one"].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
-print(f"one-pass vs two-pass: max |d| / max {float(d):.3g}, error word {int(err.item())}", flush=True)
+for name in ["one", *ALT]:
+    d = (dq[name].float() - dq["two"].float()).abs().max() / dq["two"].float().abs().max()
+    print(f"{name} vs two-pass: max |d| / max {float(d):.3g}, error word {int(errs[name].item())}", flush=True)
 flop = 8.0 * B * H * N * N * D  # 2x the forward, recompute not credited
 for r in range(ROUNDS):
-    for name in os.environ.get("VARIANTS", "two,fused,one").split(","):
+    for name in os.environ.get("VARIANTS", "two,fused,one").split(",") + list(ALT):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(ITERS):
