@@ -318,8 +318,9 @@ constexpr int CB2_K = 256;
 constexpr int CB2L_Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
 constexpr int CB2L_G = CB2L_Q + 2 * 8192;        // [2][64][64] bf16 dO tiles (sw_off)
 constexpr int CB2L_F = CB2L_G + 2 * 8192;        // [2][2 parts][64][8] bf16 fifth-k-step rows
-constexpr int CB2L_S = CB2L_F + 2 * 2048;        // [2][256][64] bf16 dS^T (sw_off); slot 1 holds K in the prologue
-constexpr int CB2L_BYTES = CB2L_S + 2 * 32768;   // 102 400 B: one workgroup per CU
+constexpr int CB2L_S = CB2L_F + 2 * 2048;        // [2][256][64] bf16 dS^T (sw_off)
+constexpr int CB2L_K = CB2L_S + 2 * 32768;       // [256][64] bf16 the block's keys (sw_off): K rows and K^T
+constexpr int CB2L_BYTES = CB2L_K + 32768;       // 135 168 B: one workgroup per CU
 
 // MFMA whose accumulator lives in AGPRs the compiler never moves (the dK / dV sums: 128 registers a wave
 // keeps for the whole sweep), and one whose A operand does (K^T); s_nop 1 in front covers the VALU-write ->
@@ -390,8 +391,8 @@ __device__ __forceinline__ void cb2_half(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2],
       *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4 + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
 #pragma unroll
       for (int dh = 0; dh < 2; ++dh) {
-        mfma_acc_a(dv[kk][dh], gt[dh], pf);
-        mfma_acc_a(dk[kk][dh], qt[dh], df);
+        dv[kk][dh] = mfma(gt[dh], pf, dv[kk][dh]);
+        dk[kk][dh] = mfma(qt[dh], df, dk[kk][dh]);
       }
     }
   }
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
   const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
   const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
-  bf16* const Kt = reinterpret_cast<bf16*>(lds + CB2L_S + 32768);
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + CB2L_K);
   {  // the block's 256 keys -> Kt: wave w loads its own 64 keys as 8 pieces of 8 rows; keys past N read zeros
     const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
@@ -452,13 +453,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // K and tile 0 in LDS
   const int dhw = wave & 1, qhw = wave >> 1;  // this wave's dQ^T sub-tile
-  bf16x8 kf[2][4], kt[16];
+  bf16x8 kf[2][4];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) kf[kk][ks] = frag_row_sw(Kt, 64 * wave + 32 * kk + (lane & 31), ks, lane);
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) kt[ks] = to_agpr(frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane));
   const bf16x8 one = ones3(lane);
   f32x16 dk[2][2], dv[2][2];
 #pragma unroll
@@ -481,8 +480,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     const bf16* dsT = Sb(SP);
     f32x16 dq = zero16();
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) mfma_src_a(dq, kt[ks], frag_tr_sw(dsT, 16 * ks, 32 * qhw, lane));
-    mfma_drain(dq);
+    for (int ks = 0; ks < 16; ++ks)
+      dq = mfma(frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane), frag_tr_sw(dsT, 16 * ks, 32 * qhw, lane), dq);
     return dq;
   };
   // mid-step: the running-sum stores of the previous step are done (the tile DMA needs this wait anyway):
@@ -584,10 +583,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) { mfma_drain_a(dk[kk][dh]); mfma_drain_a(dv[kk][dh]); }
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int key = kb * CB2_K + 64 * wave + 32 * kk + (lane & 31);
