@@ -70,9 +70,10 @@ def parse():
     ap.add_argument("--probe", default=None, help="comma list of probe tags to time live (default: auto)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N > 1 ranks on one GPU")
-    ap.add_argument("--fc1-exchange", choices=["gather", "allreduce"], default="gather",
+    ap.add_argument("--fc1-exchange", choices=["gather", "shard", "allreduce"], default="gather",
                     help="N > 1, EnvNet FC1 weight gradient: all-gather the bf16 operands and defer the averaged "
-                         "gradient to the fused Adam GEMM (the N = 1 program), or materialise + chunked all-reduce")
+                         "gradient to the fused Adam GEMM (the N = 1 program), the same with each rank updating "
+                         "its row slice only, or materialise + chunked all-reduce")
     return ap.parse_args()
 
 
@@ -556,6 +557,9 @@ def main():
         log(f"AST fp8-mixed: {results['ast_fp8']['value']} clips/s")
         del step
         free_leg()
+    if "ast" in results or "ast_fp8" in results:
+        from src.miaudio import kernels as K
+        K.check_attention_errors()  # raises if a timed step's one-pass attention backward gave up a dQ hand-off
     for leg in results.values():
         add_box_fraction(leg, calib["gbs"])
     out = results.get("envnet") or results.get("ast") or results["ast_fp8"]

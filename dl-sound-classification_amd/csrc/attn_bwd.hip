@@ -1,22 +1,19 @@
-// One-pass bf16 attention backward for training (the default of mia_attn_bwd_onepass), gfx950: S, dP and dS
-// computed once per tile, dV / dK accumulated in registers, dQ = dS K summed over the key blocks of each
-// (b, h) by an ordered hand-off of running f32 sums (bit-reproducible).  Replaces the backward of
-// F.scaled_dot_product_attention inside timm's Attention (reference src/models/ast.py:60-61).
+// One-pass bf16 attention backward for training (mia_attn_bwd_onepass), gfx950: S, dP and dS computed once
+// per tile, dV / dK accumulated in registers, dQ = dS K summed over the key blocks of each (b, h) by an ordered
+// hand-off of running f32 sums (bit-reproducible).  Replaces the backward of F.scaled_dot_product_attention
+// inside timm's Attention (reference src/models/ast.py:60-61).  The two-pass backward (attention.hip) remains
+// the AST default while it is the faster of the two (attention backward).
 // Compiled without -amdgpu-mfma-vgpr-form (see the Makefile): its dK / dV sums live in the AGPR half of
 // the register file.
-#include "attn_common.h"
-
-namespace {
-
-// ------------------------------------------------------------------------------ one-pass backward (chain)
-// The default bf16 backward.  One 4-wave workgroup per (b, h, 128-key block), two workgroups per CU (LDS
-// 68 KB, <= 256 VGPRs: each SIMD runs one wave of each of two independent workgroups, so one's softmax /
-// hand-off issues beside the other's MFMAs).  Per 64-query tile each wave (32 keys, key on the lane)
-// computes S and dP ONCE (Q' and dO row fragments from LDS against its K / V rows in registers, the row
-// constants as a fifth k-step), P and dS = P (dP - delta), accumulates dV^T += dO^T P and dK^T += Q'^T dS in
-// registers and writes dS^T (bf16) into an LDS image; after the step's one barrier wave w computes the dQ^T
-// sub-tile (d half w & 1, query half w >> 1) of the tile over the block's 128 keys (K^T fragments in
-// registers, dS^T from the image): 5 GEMM units per tile, no recompute.
+//
+// One 4-wave workgroup per (b, h, 256-key block) and CU, one wave per SIMD with up to 512 registers; each wave
+// owns 64 keys (two 32-key halves, key on the lane) and keeps their K / V fragments in registers, the block's
+// 256 keys also as an LDS image (K^T fragments for dQ).  Per 64-query tile each wave computes S' and dP' ONCE
+// (Q' and dO row fragments from LDS against its K / V rows, the row constants -L2 and -delta as a fifth
+// k-step), P = exp2(S') and dS = P dP', accumulates dV^T += dO^T P and dK^T += Q'^T dS and writes dS^T (bf16)
+// into a double-buffered LDS image; the dQ^T sub-tile of wave w (d half w & 1, query half w >> 1) of the
+// PREVIOUS tile is computed over the block's 256 keys during this tile's work: 5 GEMM units per tile, no
+// recompute.  Each query half runs as a software pipeline in four stages (cb2_half_staged).
 //
 // dQ sums over the key blocks of one (b, h) by an ORDERED HAND-OFF of running f32 sums (no float atomics:
 // bit-reproducible).  Block kb walks the query tiles rotated by lag * kb; a tile's contributions are added
@@ -25,7 +22,7 @@ namespace {
 // by an `sc1` flag store in the MIDDLE of the next step, behind a vmcnt wait that the step's own loads need
 // anyway (no wait for the store acknowledgement on the critical path); the successor block polls the flag
 // with an `sc1` load issued with its tile DMA at the start of the step that needs the sum, checks it in the
-// middle of that step and loads the sum (`sc1`, to registers) for the dQ phase after the barrier
+// middle of that step and loads the sum (`sc1`, to registers) for the link after the second half
 // (MI355X_MICROARCH.md, visibility table row 1: one storing wave per flag, every byte stored and loaded
 // `sc1`, the store drained before its flag).  With a lag of >= 2 steps between consecutive contributions
 // the sum is published a step before it is polled; at a lag of 1 (sequence lengths where 2 does not fit) the
@@ -37,20 +34,13 @@ namespace {
 // Rows past the sequence end read as zeros everywhere (K / V / Q' / dO by the descriptors' ranges, the row
 // constants per part): such a key meets K = V = 0, such a query p = 1 and dP' = 0, so dS = 0 there, nothing
 // is masked and nothing past the end is stored.
-// experiment builds only (tools/bench_attn_bwd.py ATTN_LIBS): bit 0 = no hand-off (every block writes its own
-// partial as dQ), bit 1 = no wait for the next tile's DMA before the barrier.  Wrong results; timing only.
-#ifndef CB_EXP
-#define CB_EXP 0
-#endif
-constexpr int CB_K = 128;                      // keys per workgroup: 4 waves x 32
+#include "attn_common.h"
+
+namespace {
+
 constexpr int CB_SUB = 4096;                   // one 32 x 32 f32 dQ^T sub-tile in register order
 constexpr int CB_TILE = 4 * CB_SUB;            // the four sub-tiles of a 64-query tile
 constexpr unsigned long long CB_SPIN_TICKS = 20000000ull;  // 200 ms at 100 MHz
-constexpr int CBL_Q = 0;                       // [2][64][64] bf16 Q' tiles (sw_off)
-constexpr int CBL_G = CBL_Q + 2 * 8192;        // [2][64][64] bf16 dO tiles (sw_off)
-constexpr int CBL_F = CBL_G + 2 * 8192;        // [2][2 parts][64][8] bf16 fifth-k-step rows
-constexpr int CBL_S = CBL_F + 2 * 2048;        // [2][128][64] bf16 dS^T (sw_off); slot 1 holds K in the prologue
-constexpr int CBL_BYTES = CBL_S + 2 * 16384;   // 69 632 B: two workgroups per CU
 
 // the row-constant fragments of 64 queries by LDS-DMA, one descriptor per part (rows past N read zeros in
 // both parts): waves 0 / 1 issue part 0 / 1
@@ -99,221 +89,6 @@ __device__ __forceinline__ void cb_spin(const unsigned* flag, unsigned want, uns
   }
 }
 
-// S', dP' of 32 queries (half sq of the tile) x this wave's 32 keys -> P, dS; dV^T, dK^T MFMAs; dS^T -> LDS
-__device__ __forceinline__ void cb_half(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_,
-                                        const bf16* F_, bf16* dsT, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4],
-                                        bf16x8 one, int sq, int wave, int lane) {
-  const int qr = sq * 32 + (lane & 31);
-  const int krow = 32 * wave + (lane & 31);
-  f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), kf[0], zero16());
-  f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
-#pragma unroll
-  for (int ks = 1; ks < 4; ++ks) {
-    sc = mfma(frag_row_sw(Q_, qr, ks, lane), kf[ks], sc);
-    dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
-  }
-  sc = mfma(row_frag(F_ + qr * 8), one, sc);
-  dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float p = __builtin_amdgcn_exp2f(sc[r]);
-    sc[r] = p;
-    dp[r] *= p;
-  }
-#pragma unroll
-  for (int sk = 0; sk < 2; ++sk) {
-    const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
-    // dS^T[key][q]: elements 0..3 = queries 16 sk + 4h + 0..3, 4..7 = 16 sk + 8 + 4h + 0..3 (of this half)
-    const int qa = sq * 32 + 16 * sk + 4 * (lane >> 5);
-    *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa)) = bf16x4{df[0], df[1], df[2], df[3]};
-    *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      dv[dh] = mfma(frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane), pf, dv[dh]);
-      dk[dh] = mfma(frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane), df, dk[dh]);
-    }
-  }
-}
-
-template <int LAG>
-__global__ __launch_bounds__(256, 2) void attn_bwd_chain_kernel(const bf16* __restrict__ qkv,
-                                                                const bf16* __restrict__ dout,
-                                                                const bf16* __restrict__ qs,
-                                                                const bf16* __restrict__ frag,
-                                                                bf16* __restrict__ dqkv, float* chain,
-                                                                unsigned* flags, unsigned* err, int N, int H,
-                                                                int nkb, float scale, float dk_scale) {
-  __shared__ __attribute__((aligned(1024))) char lds[CBL_BYTES];
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int w = xcd_work_item(blockIdx.x, gridDim.x);  // the key blocks of one (b, h): consecutive, one XCD
-  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
-  const int nt = (N + 63) / 64;
-  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
-  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
-  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
-  bf16* const Kt = reinterpret_cast<bf16*>(lds + CBL_S + 16384);
-  // the block's 128 keys -> Kt (dS^T slot 1, first written at step 1, after every wave has read K): wave w
-  // loads its own 32 keys as 4 pieces of 8 rows; keys past N read as zeros
-  {
-    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = 32 * wave + 8 * i + (lane >> 3);
-      const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
-      lds_dma16(kr, Kt + (4 * wave + i) * 512, vo, (unsigned)((int64_t)(kb * CB_K + 32 * wave + 8 * i) * ldt * 2));
-    }
-  }
-  TileDMA qd, gd;
-  FragDMA2 fd;
-  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
-  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
-  fd.init(frag + (int64_t)bh * 2 * N * 8, N, wave);
-  auto Qb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_Q + P * 8192); };
-  auto Gb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_G + P * 8192); };
-  auto Fb = [&](int P) { return reinterpret_cast<bf16*>(lds + CBL_F + P * 2048); };
-  const CbOrder<LAG> ord{nt, nkb, kb};
-  int T = ord.first();  // the tile of the current step
-  qd.issue(Qb(0), (unsigned)T * tile_bytes, wave);
-  gd.issue(Gb(0), (unsigned)T * tile_bytes, wave);
-  fd.issue(Fb(0), (unsigned)T * 64u, wave, lane);
-  const int key = kb * CB_K + wave * 32 + (lane & 31);
-  bf16x8 vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
-  settle(vf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // K and tile 0 in LDS
-  const int dhw = wave & 1, qhw = wave >> 1;  // this wave's dQ^T sub-tile
-  bf16x8 kf[4], kt[8];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kf[ks] = frag_row_sw(Kt, 32 * wave + (lane & 31), ks, lane);
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) kt[ks] = frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane);
-  const bf16x8 one = ones3(lane);
-  f32x16 dk[2], dv[2];
-  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-  unsigned* const fl = flags + (int64_t)bh * nt * 4;
-  const __amdgpu_buffer_rsrc_t flr = __builtin_amdgcn_make_buffer_rsrc((void*)fl, 0, nt * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(chain + (int64_t)bh * nt * (CB_TILE / 4)), 0, nt * CB_TILE, 0x00020000);
-  const int last = nkb - 1;
-  bool pub = false;  // this wave stored a running sum last step: publish its flag in the middle of this step
-  int pub_T = 0;
-  unsigned pub_val = 0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K fragments in registers before slot 1 is reused
-  // one step; P = buffer parity (compile time: the loop is unrolled by 2)
-  auto step = [&](int j, auto par) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;
-    const int pos = (CB_EXP & 1) ? last : ord.pos(T), T1 = ord.next(T);
-    if (j + 1 < nt) {  // buffer P^1 was last read by step j - 1's body, before its barrier
-      qd.issue(Qb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
-      gd.issue(Gb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
-      fd.issue(Fb(P ^ 1), (unsigned)T1 * 64u, wave, lane);
-    }
-    unsigned fv = 0;
-    if (pos > 0) fv = cb_load_flag(flr, (T * 4 + wave) * 4);  // this tile's predecessor (checked mid-step)
-    bf16* const dsT = reinterpret_cast<bf16*>(lds + CBL_S + P * 16384);
-    cb_half(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 0, wave, lane);
-    // mid-step: last step's running-sum stores are done (the poll needs this wait anyway): publish them;
-    // then this tile's predecessor, and its running sum into registers for the dQ phase
-    if (!(CB_EXP & 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
-    u32x4 run[4];
-    if (pos > 0) {
-      if (__builtin_expect(__builtin_amdgcn_readfirstlane(fv) != (unsigned)pos, 0))
-        cb_spin(fl + T * 4 + wave, (unsigned)pos, err);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, T * CB_TILE + wave * CB_SUB + g * 1024, 16);
-    }
-    cb_half(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 1, wave, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dS^T written; tile j + 1 landed at the mid wait
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // dQ^T sub-tile (dhw, qhw) of tile T over the block's 128 keys
-    f32x16 dq = mfma(kt[0], frag_tr_sw(dsT, 0, 32 * qhw, lane), zero16());
-#pragma unroll
-    for (int ks = 1; ks < 8; ++ks) dq = mfma(kt[ks], frag_tr_sw(dsT, 16 * ks, 32 * qhw, lane), dq);
-    if (pos > 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 r = __builtin_bit_cast(f32x4, run[g]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dq[4 * g + i] += r[i];
-      }
-    }
-    pub = false;
-    if (pos < last) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]}), cr, lane * 16,
-            T * CB_TILE + wave * CB_SUB + g * 1024, 16);
-      pub = true;
-      pub_T = T;
-      pub_val = (unsigned)(pos + 1);
-    } else {  // the last contribution: bf16 dQ rows of the sub-tile's 32 queries
-      const int q = T * 64 + 32 * qhw + (lane & 31);
-      if (q < N) {
-        bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D + 32 * dhw;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d0 = 8 * g4 + 4 * (lane >> 5);
-          *reinterpret_cast<bf16x4*>(qrow + d0) =
-              bf16x4{(bf16)(dq[4 * g4] * scale), (bf16)(dq[4 * g4 + 1] * scale), (bf16)(dq[4 * g4 + 2] * scale),
-                     (bf16)(dq[4 * g4 + 3] * scale)};
-        }
-      }
-    }
-    T = T1;
-  };
-  {
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    int j = 0;
-    for (; j + 1 < nt; j += 2) {
-      step(j, P0{});
-      step(j + 1, P1{});
-    }
-    if (j < nt) step(j, P0{});
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
-  if (key >= N) return;
-  bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
-  bf16* vrow = krow + H * D;
-#pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
-    const int d0 = 8 * g4 + 4 * (lane >> 5);
-    bf16x4 a0, a1, c0, c1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      a0[i] = (bf16)(dk[0][4 * g4 + i] * dk_scale);
-      a1[i] = (bf16)(dk[1][4 * g4 + i] * dk_scale);
-      c0[i] = (bf16)dv[0][4 * g4 + i];
-      c1[i] = (bf16)dv[1][4 * g4 + i];
-    }
-    *reinterpret_cast<bf16x4*>(krow + d0) = a0;
-    *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
-    *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
-    *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
-  }
-}
-
-}  // namespace
-
-// ------------------------------------------------------------------------------ one-pass backward, 256-key form
-// The chain kernel above with 64 keys per wave (two 32-key halves): one 4-wave workgroup per (b, h, 256-key
-// block) and CU, one wave per SIMD with up to 512 registers.  Per query half the Q' / dO row fragments and
-// the dO^T / Q'^T transposed fragments are read once for both key halves (half the LDS reads per MFMA), the
-// dQ^T sub-tile of a wave sums 256 keys (16 MFMAs on K^T fragments in registers), and a (b, h) has half as
-// many key blocks: half the hand-off hops and tile re-reads.  The dQ of tile j is computed at the start of
-// step j + 1 (the dS^T image is double-buffered), in the same basic block as step j + 1's S / dP work, so a
-// single wave has independent MFMA chains to issue while it waits; its running sum is stored right after and
-// published in the middle of the step (behind the vmcnt wait the tile DMA needs anyway).
 constexpr int CB2_K = 256;
 constexpr int CB2L_Q = 0;                        // [2][64][64] bf16 Q' tiles (sw_off)
 constexpr int CB2L_G = CB2L_Q + 2 * 8192;        // [2][64][64] bf16 dO tiles (sw_off)
@@ -322,28 +97,20 @@ constexpr int CB2L_S = CB2L_F + 2 * 2048;        // [2][256][64] bf16 dS^T (sw_o
 constexpr int CB2L_K = CB2L_S + 2 * 32768;       // [256][64] bf16 the block's keys (sw_off): K rows and K^T
 constexpr int CB2L_BYTES = CB2L_K + 32768;       // 135 168 B: one workgroup per CU
 
-// MFMA whose accumulator lives in AGPRs the compiler never moves (the dK / dV sums: 128 registers a wave
-// keeps for the whole sweep), and one whose A operand does (K^T); s_nop 1 in front covers the VALU-write ->
-// MFMA-read hazard of a freshly converted operand.  Not volatile: the compiler schedules them by their data.
-__device__ __forceinline__ void mfma_acc_a(f32x16& acc, bf16x8 a, bf16x8 b) {
-  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_src_a(f32x16& acc, bf16x8 a_agpr, bf16x8 b) {
-  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(a_agpr), "v"(b));
-}
-// the MFMA -> VALU read hazard after a chain of the asm MFMAs above (18 wait states for 32x32x16)
-__device__ __forceinline__ void mfma_drain(f32x16& acc) { asm("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc)); }
-__device__ __forceinline__ void mfma_drain_a(f32x16& acc) { asm("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(acc)); }
-__device__ __forceinline__ bf16x8 to_agpr(bf16x8 v) {
-  bf16x8 r;
-  asm("; kept in AGPRs" : "=a"(r) : "0"(v));
-  return r;
-}
-
-// one query half sq: S', dP' for both key halves, P, dS, dV^T / dK^T MFMAs, dS^T -> LDS
-__device__ __forceinline__ void cb2_half(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2], const bf16* Q_, const bf16* G_,
-                                         const bf16* F_, bf16* dsT, const bf16x8 (&kf)[2][4],
-                                         const bf16x8 (&vf)[2][4], bf16x8 one, int sq, int wave, int lane) {
+// The same half as a software pipeline in four stages separated by sched_barriers (one wave per SIMD has no
+// partner to hide latency behind, so the MFMA chains of one unit issue while the VALU of the previous one
+// runs): A = S / dP of key half 0 (their operand reads issued first) with the dV / dK transposed fragments and
+// the first dQ fragments requested under it; B = S / dP of key half 1 under the softmax of half 0 (exp, dS,
+// the bf16 operands, the dS^T image writes); C = dV / dK of half 0 and four k-steps of the previous tile's dQ
+// under the softmax of half 1; D = dV / dK of half 1 and four more dQ k-steps.  sched_group_barrier lays one
+// MFMA and its share of the stage's other instructions into each MFMA gap.  dq: k-steps kq0 .. kq0 + 7 of the
+// previous tile's dQ^T (A = K^T from the block's image Kt, B = that tile's dS^T image dsP), DQ: any at all.
+template <bool DQ>
+__device__ __forceinline__ void cb2_half_staged(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2], f32x16& dq,
+                                                const bf16* Q_, const bf16* G_, const bf16* F_, bf16* dsT,
+                                                const bf16* Kt, const bf16* dsP, int kq0, int dhw, int qhw,
+                                                const bf16x8 (&kf)[2][4], const bf16x8 (&vf)[2][4], bf16x8 one,
+                                                int sq, int wave, int lane) {
   const int qr = sq * 32 + (lane & 31);
   bf16x8 qa[4], ga[4];
 #pragma unroll
@@ -352,9 +119,10 @@ __device__ __forceinline__ void cb2_half(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2],
     ga[ks] = frag_row_sw(G_, qr, ks, lane);
   }
   const bf16x8 fl = row_frag(F_ + qr * 8), fd = row_frag(F_ + 512 + qr * 8);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- A
   f32x16 sc[2], dp[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
+  auto sdp = [&](int kk) __attribute__((always_inline)) {
     sc[kk] = mfma(qa[0], kf[kk][0], zero16());
     dp[kk] = mfma(ga[0], vf[kk][0], zero16());
 #pragma unroll
@@ -364,38 +132,95 @@ __device__ __forceinline__ void cb2_half(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2],
     }
     sc[kk] = mfma(fl, one, sc[kk]);
     dp[kk] = mfma(fd, one, dp[kk]);
+  };
+  sdp(0);
+  bf16x8 gt[2][2], qt[2][2];
+#pragma unroll
+  for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      gt[sk][dh] = frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane);
+      qt[sk][dh] = frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane);
+    }
+  bf16x8 ka[2][4], sf[2][4];
+  if constexpr (DQ) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      ka[0][ks] = frag_tr_sw(Kt, 16 * (kq0 + ks), 32 * dhw, lane);
+      sf[0][ks] = frag_tr_sw(dsP, 16 * (kq0 + ks), 32 * qhw, lane);
+    }
   }
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
+  for (int g = 0; g < 10; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, DQ ? 3 : 2, 0);  // DS read
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- B
+  bf16x8 pf[2][2], df[2][2];
+  auto softmax = [&](int kk) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = __builtin_amdgcn_exp2f(sc[kk][r]);
       sc[kk][r] = p;
       dp[kk][r] *= p;
     }
+    const int krow = 64 * wave + 32 * kk + (lane & 31);
 #pragma unroll
-  for (int sk = 0; sk < 2; ++sk) {
-    const int q0 = sq * 32 + 16 * sk;
-    bf16x8 gt[2], qt[2];
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      gt[dh] = frag_tr_sw(G_, q0, 32 * dh, lane);
-      qt[dh] = frag_tr_sw(Q_, q0, 32 * dh, lane);
+    for (int sk = 0; sk < 2; ++sk) {
+      pf[kk][sk] = acc_frag(sc[kk], sk);
+      df[kk][sk] = acc_frag(dp[kk], sk);
+      const int qa4 = sq * 32 + 16 * sk + 4 * (lane >> 5);
+      const bf16x8 d = df[kk][sk];
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4)) = bf16x4{d[0], d[1], d[2], d[3]};
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4 + 8)) = bf16x4{d[4], d[5], d[6], d[7]};
     }
+  };
+  sdp(1);
+  softmax(0);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = acc_frag(sc[kk], sk), df = acc_frag(dp[kk], sk);
-      const int krow = 64 * wave + 32 * kk + (lane & 31);
-      const int qa4 = q0 + 4 * (lane >> 5);
-      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4)) = bf16x4{df[0], df[1], df[2], df[3]};
-      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4 + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
+  for (int g = 0; g < 10; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 7, 1);  // VALU
+    if (g & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);  // DS write
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- C
+  auto dvdk = [&](int kk) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk)
 #pragma unroll
       for (int dh = 0; dh < 2; ++dh) {
-        dv[kk][dh] = mfma(gt[dh], pf, dv[kk][dh]);
-        dk[kk][dh] = mfma(qt[dh], df, dk[kk][dh]);
+        dv[kk][dh] = mfma(gt[sk][dh], pf[kk][sk], dv[kk][dh]);
+        dk[kk][dh] = mfma(qt[sk][dh], df[kk][sk], dk[kk][dh]);
       }
+  };
+  dvdk(0);
+  if constexpr (DQ) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) dq = mfma(ka[0][ks], sf[0][ks], dq);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      ka[1][ks] = frag_tr_sw(Kt, 16 * (kq0 + 4 + ks), 32 * dhw, lane);
+      sf[1][ks] = frag_tr_sw(dsP, 16 * (kq0 + 4 + ks), 32 * qhw, lane);
     }
   }
+  softmax(1);
+#pragma unroll
+  for (int g = 0; g < (DQ ? 12 : 8); ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 6, 2);  // VALU
+    if (DQ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);  // DS read
+    if (g & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 2);  // DS write
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- D
+  dvdk(1);
+  if constexpr (DQ) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) dq = mfma(ka[1][ks], sf[1][ks], dq);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int LAG>
@@ -480,8 +305,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     const bf16* dsT = Sb(SP);
     f32x16 dq = zero16();
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks)
-      dq = mfma(frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane), frag_tr_sw(dsT, 16 * ks, 32 * qhw, lane), dq);
+    for (int h = 0; h < 2; ++h) {  // 8 k-steps' fragments requested, then their 8 MFMAs
+      bf16x8 ka[8], sf[8];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        ka[ks] = frag_tr_sw(Kt, 16 * (8 * h + ks), 32 * dhw, lane);
+        sf[ks] = frag_tr_sw(dsT, 16 * (8 * h + ks), 32 * qhw, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) dq = mfma(ka[ks], sf[ks], dq);
+    }
     return dq;
   };
   // mid-step: the running-sum stores of the previous step are done (the tile DMA needs this wait anyway):
@@ -545,14 +379,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     }
     unsigned fv = 0;
     if (HP && pp > 0) fv = cb_load_flag(flr, (Tp * 4 + wave) * 4);  // Tp's predecessor (checked mid-step)
-    f32x16 dq;
-    if constexpr (HP) dq = dq_mfma(P ^ 1);
-    cb2_half(dk, dv, Qb(P), Gb(P), Fb(P), Sb(P), kf, vf, one, 0, wave, lane);
+    f32x16 dq = zero16();  // the previous tile's dQ^T: k-steps 0-7 in this half, 8-15 in the next
+    cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 0, dhw, qhw, kf, vf, one, 0, wave,
+                        lane);
     if constexpr (HP) link_fetch(fv);
     else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile j + 1 landed
     }
-    cb2_half(dk, dv, Qb(P), Gb(P), Fb(P), Sb(P), kf, vf, one, 1, wave, lane);
+    cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 8, dhw, qhw, kf, vf, one, 1, wave,
+                        lane);
     if constexpr (HP) link_store(dq);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dS^T written
     __builtin_amdgcn_sched_barrier(0);
@@ -608,6 +443,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   }
 }
 
+}  // namespace
+
 
 // ------------------------------------------------------------------------------ one-pass backward: host side
 static int64_t cb_flags_bytes(int32_t B, int32_t N, int32_t H) {
@@ -649,22 +486,15 @@ extern "C" int mia_attn_bwd_onepass(const void* qkv, const void* out, const void
   float* sums = reinterpret_cast<float*>(reinterpret_cast<char*>(chain) + cb_flags_bytes(B, N, H));
   hipError_t e = hipMemsetAsync(flags, 0, (size_t)cb_flags_bytes(B, N, H), s);
   if (e != hipSuccess) return mia::fail(-(int)e, "attn_bwd_onepass: memset: %s", hipGetErrorString(e));
-  const int keys = (CB_EXP & 4) ? CB2_K : CB_K;  // experiment builds: the 256-key form
-  const int nkb = (int)cdiv(N, keys), lag = cb_lag(N, keys);
+  const int nkb = (int)cdiv(N, CB2_K), lag = cb_lag(N, CB2_K);
   MIA_CHECK_ARG((int64_t)nkb * B * H < (1ll << 31), "attn_bwd_onepass: grid too large");
   const dim3 grid((unsigned)(nkb * B * H));
   const float dks = 1.f / LOG2E;
 #define CB_LAUNCH(KER, L) KER<L><<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, \
                                                     sums, flags, err, N, H, nkb, scale, dks)
-  if (CB_EXP & 4) {
-    if (lag == 3) CB_LAUNCH(attn_bwd_chain2_kernel, 3);
-    else if (lag == 2) CB_LAUNCH(attn_bwd_chain2_kernel, 2);
-    else CB_LAUNCH(attn_bwd_chain2_kernel, 1);
-  } else {
-    if (lag == 3) CB_LAUNCH(attn_bwd_chain_kernel, 3);
-    else if (lag == 2) CB_LAUNCH(attn_bwd_chain_kernel, 2);
-    else CB_LAUNCH(attn_bwd_chain_kernel, 1);
-  }
+  if (lag == 3) CB_LAUNCH(attn_bwd_chain2_kernel, 3);
+  else if (lag == 2) CB_LAUNCH(attn_bwd_chain2_kernel, 2);
+  else CB_LAUNCH(attn_bwd_chain2_kernel, 1);
 #undef CB_LAUNCH
   MIA_LAUNCH_CHECK("attn_bwd_chain");
   return 0;

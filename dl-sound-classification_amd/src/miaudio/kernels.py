@@ -166,6 +166,9 @@ def materialise_deferred_grad(param: torch.Tensor) -> None:
     d = getattr(param, "_mia_deferred", None)
     if d is None:
         return
+    if "row0" in d:
+        raise RuntimeError("a row-sharded deferred gradient (GradAllReducer fc1_exchange='shard') is applied "
+                           "by FusedAdam only; use fc1_exchange='gather' with another optimizer")
     dW = torch.empty(d["M"], d["N"], dtype=torch.float32, device=param.device)
     gemm(d["A"], d["B"], epilogue(dW, d["N"]), d["M"], d["N"], d["K"], L.BF16)
     param._mia_deferred = None
@@ -634,10 +637,20 @@ def soft_ce(logits: torch.Tensor, y: torch.Tensor, input_sigmoid: bool):
     return loss[0], dlogits, correct[0]
 
 
+def wait_param(p: torch.Tensor) -> None:
+    """Order the current stream after a pending update of ``p``'s operand rows by another stream (the
+    comm-stream all-gather of GradAllReducer fc1_exchange="shard"); no-op otherwise."""
+    ev = getattr(p, "_mia_ready", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+        p._mia_ready = None
+
+
 def bf16_shadow(p: torch.Tensor) -> torch.Tensor:
     """bf16 GEMM-operand copy of an f32 parameter, kept on the parameter and refreshed by FusedAdam in
     its update pass (no per-step cast).  Recast when anything else changed the parameter in place
     (``_version`` moved: load_state_dict, DDP broadcast, a non-fused optimizer)."""
+    wait_param(p)
     sh = getattr(p, "_mia_bf16", None)
     if sh is not None and getattr(p, "_mia_bf16_ver", None) == p._version and sh.shape == p.shape:
         return sh

@@ -70,9 +70,11 @@ def _linear(x, W, bias, out, M, cd, act=L.ACT_NONE, aux=None, pre=L.PRE_NONE, ta
 
 
 ATTN_SAVE_Q = True  # bf16 training: the attention forward writes Q' for the backward (mia_attn_fwd_save_q)
-# bf16 training backward: the one-pass kernel (mia_attn_bwd_onepass, no S / dP recompute) or the two-kernel
-# form (mia_attn_bwd_saved_q); tools flip this for A/B runs
-ATTN_ONEPASS = True
+# bf16 training backward: the two-kernel form (mia_attn_bwd_saved_q: dK/dV pass + dQ pass, S / dP recomputed
+# in the second) or the one-pass kernel (mia_attn_bwd_onepass, no recompute).  Measured at the benched grid
+# (B 256, N 1645, H 12; tools/bench_attn_bwd.py, gpurun_out r5i): two-pass 7.3 ms, one-pass 8.1-8.2 ms per
+# layer, so the two-pass form is the default; tools and tests flip this for A/B runs
+ATTN_ONEPASS = False
 
 
 def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None,

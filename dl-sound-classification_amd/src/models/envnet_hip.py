@@ -256,6 +256,7 @@ class EnvNetFunction(torch.autograd.Function):
             Wt, bias = p[40 + 2 * li], p[41 + 2 * li]
             fout, fin = Wt.shape
             last = li == 2
+            K.wait_param(Wt)  # data-parallel fc1_exchange="shard": the rows the other ranks updated
             if cd == L.BF16 and not last:
                 Wt = K.bf16_shadow(Wt)
             wfc.append(Wt)

@@ -29,6 +29,17 @@ never written on one GPU; src/miaudio/kernels.py::defer_weight_grad) crosses the
   ``materialise_k`` gathered rows (world >= 8 at B = 256) the averaged gradient is instead written once by
   the same GEMM with its per-tile sums of squares (the deferred pair recomputes the product; at K = 2048
   that is 5.06 against 4.27 ms per step) -- the same sums, so the same parameters;
+* ``"shard"``: the same all-gather of the two bf16 operands, but rank r owns only rows
+  [r M / world, (r + 1) M / world) of FC1 (whole 128-row GEMM tiles): its sums-only GEMM covers that row slice
+  of the averaged gradient, the per-tile sums of squares of all slices are all-gathered (the slot array of
+  the gather form, so the clip norm is the same bit for bit), and FusedAdam's Adam GEMM updates only the
+  slice -- 1/world of the product and of the 9 GB of f32 parameter + moment traffic.  The updated bf16 operand
+  copy of the slice (K.bf16_shadow) is then all-gathered on the comm stream, overlapping the next forward's
+  convolutions; FC1's forward waits for it (K.wait_param).  The f32 master rows and Adam moments of the other
+  ranks' slices go stale on purpose; ``sync_sharded()`` all-gathers them (lite.Trainer calls it at every
+  epoch end, before validation and checkpointing, and FusedAdam before any step that does not shard).
+  Every rank's slice is computed exactly as the gather form computes those rows, so parameters, moments
+  and norm equal the gather form's bit for bit;
 * ``"allreduce"``: FC1's gradient is materialised as 16 row chunks, each all-reduced as its GEMM is enqueued
   (above).
 
@@ -63,12 +74,14 @@ class GradAllReducer:
     def __init__(self, model: torch.nn.Module, world: int | None = None, bucket_bytes: int = BUCKET_BYTES,
                  broadcast_buffers: bool = True, fc1_exchange: str = "gather",
                  materialise_k: int = MATERIALISE_K):
-        if fc1_exchange not in ("gather", "allreduce"):
-            raise ValueError(f"fc1_exchange must be 'gather' or 'allreduce', not {fc1_exchange!r}")
+        if fc1_exchange not in ("gather", "shard", "allreduce"):
+            raise ValueError(f"fc1_exchange must be 'gather', 'shard' or 'allreduce', not {fc1_exchange!r}")
         self.fc1_exchange = fc1_exchange
         self.materialise_k = materialise_k
         self.model = model
         self.world = world or dist.get_world_size()
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.sharded = {}  # id -> parameter whose f32 rows / moments outside this rank's slice are stale
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.bucket_bytes = bucket_bytes
@@ -86,7 +99,7 @@ class GradAllReducer:
         for m in model.modules():
             m._grad_ready = self.grad_ready
             m._grad_chunk_ready = self.grad_chunk_ready
-            m._grad_gather = self.grad_gather if fc1_exchange == "gather" else None
+            m._grad_gather = self.grad_gather if fc1_exchange in ("gather", "shard") else None
         self.gathers = []  # (param, dY_all, X_all, M, N, K) launched this step, deferred in finish()
         self.gathered = self.last_gathered = 0
         self.gathered_bytes = self.last_gathered_bytes = 0            # operand bytes each rank sends
@@ -254,7 +267,9 @@ class GradAllReducer:
             from ..miaudio import lib as L
             for param, dy_all, x_all, M, N, Kk in self.gathers:
                 A, B = K.dense(dy_all, L.RC, Kk, M), K.dense(x_all, L.RC, Kk, N)
-                if Kk > self.materialise_k:
+                if self.fc1_exchange == "shard" and M % (128 * self.world) == 0:
+                    self._defer_shard(param, dy_all, x_all, M, N, Kk)
+                elif Kk > self.materialise_k:
                     # one GEMM (same main loop and sum order as the deferred pair) writes the gradient and
                     # its per-tile sums of squares; FusedAdam then streams it like any other gradient
                     dW = torch.empty(M, N, dtype=torch.float32, device=dy_all.device)
@@ -281,6 +296,75 @@ class GradAllReducer:
         self.last_gathered_param_bytes, self.gathered_param_bytes = self.gathered_param_bytes, 0
         if self.broadcast_buffers:
             self._broadcast_buffers()
+
+    # ------------------------------------------------------------------ fc1_exchange="shard"
+    def _defer_shard(self, param, dy_all, x_all, M, N, Kk):
+        """Defer this rank's row slice of the averaged gradient (dY_all[:, slice])^T X_all to FusedAdam, with
+        the per-tile sums of squares of ALL slices (one all-gather of f64 slots) for the clip norm."""
+        from ..miaudio import kernels as K
+        from ..miaudio import lib as L
+        if getattr(param, "_mia_deferred", None) is not None:
+            raise RuntimeError("a deferred weight gradient is still pending: call FusedAdam.step() between "
+                               "backward passes")
+        w, r = self.world, self.rank
+        Ms = M // w
+        r0 = r * Ms
+        sq = torch.empty(int(L.load().mia_gemm_sqsum_slots(M, N)), dtype=torch.float64, device=dy_all.device)
+        per = sq.numel() // w  # slots are row-block-major (128 x 128 tiles): a slice's slots are contiguous
+        A = K.dense(dy_all[:, r0:], L.RC, Kk, Ms, ld=M)
+        B = K.dense(x_all, L.RC, Kk, N)
+        mine = sq[r * per:(r + 1) * per]
+        K.gemm_sqsum_only(A, B, Ms, N, Kk, mine, tag="fc1.wgrad")
+        self._all_gather(sq, mine.clone())
+        param._mia_deferred = dict(A=A, B=B, M=Ms, N=N, K=Kk, sq=sq, keep=(dy_all, x_all), row0=r0, rows_total=M,
+                                   shard=self)
+
+    def after_shard_update(self, param, shadow, d):
+        """FusedAdam has updated rows [row0, row0 + M) of ``param`` (and of its bf16 copy ``shadow``): all-gather
+        the updated operand rows on the comm stream; FC1's next forward waits for them (K.wait_param)."""
+        r0, Ms, M = d["row0"], d["M"], d["rows_total"]
+        full = (shadow if shadow is not None else param.data).view(M, -1)
+
+        def run():
+            self._all_gather(full, full[r0:r0 + Ms].clone())
+
+        if self.cuda:
+            ev = torch.cuda.current_stream().record_event()
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                run()
+                param._mia_ready = torch.cuda.current_stream().record_event()
+            full.record_stream(self.stream)
+        else:
+            run()
+        param._mia_shard = (self, r0, Ms, M)
+        self.sharded[id(param)] = param
+
+    @torch.no_grad()
+    def sync_param(self, param):
+        """All-gather the f32 master rows and Adam moments of a sharded parameter, so every rank holds all of
+        them (a collective: every rank calls it at the same point)."""
+        from ..miaudio import kernels as K
+        info = getattr(param, "_mia_shard", None)
+        if info is None:
+            return
+        _, r0, Ms, M = info
+        K.wait_param(param)
+        ref = getattr(param, "_mia_fused_adam", None)
+        opt = ref() if callable(ref) else None
+        ts = [param.data]
+        if opt is not None and param in opt.state:
+            ts += [opt.state[param]["exp_avg"], opt.state[param]["exp_avg_sq"]]
+        for t in ts:
+            t2 = t.view(M, -1)
+            self._all_gather(t2, t2[r0:r0 + Ms].clone())
+        param._mia_shard = None
+        self.sharded.pop(id(param), None)
+
+    def sync_sharded(self):
+        """sync_param for every parameter this reducer sharded (epoch end: before validation / checkpoint)."""
+        for p in list(self.sharded.values()):
+            self.sync_param(p)
 
     @torch.no_grad()
     def _broadcast_buffers(self):

@@ -335,11 +335,16 @@ class Trainer:
                 self.optimizer.zero_grad(set_to_none=True)
                 module.global_step += 1
             train_logs = module._flush_logs()
+            if self.ddp is not None:
+                self.ddp.sync_sharded()  # fc1_exchange="shard": every rank's FC1 rows before eval / checkpoint
             val_logs = {}
             if hasattr(datamodule, "val_dataloader"):
                 val_logs = self._run_eval(module, datamodule.val_dataloader(), "val")
                 module.train()
             module.on_train_epoch_end()
+            if self.device.type == "cuda":  # a timed-out dQ hand-off in this epoch's attention backwards
+                from src.miaudio import kernels as K
+                K.check_attention_errors()
             train_logs.update(module._flush_logs())
             if self.scheduler is not None:
                 self.scheduler.step()

@@ -86,6 +86,11 @@ class FusedAdam(torch.optim.Optimizer):
         L.require_device(ps[0], "FusedAdam")
         deferred = [getattr(p, "_mia_deferred", None) for p in ps]
         for p, d in zip(ps, deferred):
+            shard = getattr(p, "_mia_shard", None)
+            if shard is not None and (d is None or "row0" not in d):
+                # the last steps updated only this rank's row slice (GradAllReducer fc1_exchange="shard"):
+                # bring every rank's rows of the parameter and moments back before a whole-tensor update
+                shard[0].sync_param(p)
             if d is not None and p.grad is not None:
                 raise RuntimeError("a parameter has both a gradient and a deferred weight gradient")
             if p.dtype != torch.float32 or (d is None and p.grad.dtype != torch.float32):
@@ -137,12 +142,13 @@ class FusedAdam(torch.optim.Optimizer):
         b1, b2 = grp["betas"]
         # algorithmic HBM bytes: grad read by the norm pass (4 B/param) + Adam's p, g, m, v read and
         # p, m, v written (28 B/param) + the bf16 operand copies rewritten (2 B/param where shadowed)
-        nel = sum(p.numel() for p in ps)
-        nbytes = 32 * nel + 2 * sum(p.numel() for p, sh in zip(ps, shadows) if sh is not None)
-        nbytes -= 4 * sum(p.numel() for p, q in zip(ps, pre) if q is not None)  # no norm read of those
-        for p, d in zip(ps, deferred):  # no gradient read either; the GEMM reads its two bf16 operands
+        # (a sharded deferred gradient: only this rank's rows are updated and read)
+        upd = [d["M"] * d["N"] if d is not None else p.numel() for p, d in zip(ps, deferred)]
+        nbytes = 32 * sum(upd) + 2 * sum(u for u, sh in zip(upd, shadows) if sh is not None)
+        nbytes -= 4 * sum(u for u, q in zip(upd, pre) if q is not None)  # no norm read of those
+        for u, d in zip(upd, deferred):  # no gradient read either; the GEMM reads its two bf16 operands
             if d is not None:
-                nbytes += -4 * p.numel() + 2 * d["K"] * (d["M"] + d["N"])
+                nbytes += -4 * u + 2 * d["K"] * (d["M"] + d["N"])
         with K.probe("optim.step", 0.0, nbytes):
             L.check(lib.mia_clip_adam(table[0].data_ptr(), table[1].data_ptr(), table[2].data_ptr(),
                                       table[3].data_ptr(), table[4].data_ptr(), table[5].data_ptr(), n,
@@ -162,11 +168,16 @@ class FusedAdam(torch.optim.Optimizer):
                 lr32, b1_32, b2_32 = (float(np.float32(v)) for v in (grp["lr"], b1, b2))
                 lr_bc1 = lr32 / (1.0 - math.pow(b1_32, st))
                 bc2_sqrt = math.sqrt(1.0 - math.pow(b2_32, st))
-                L.check(lib.mia_gemm_adam(d["A"], d["B"], d["M"], d["N"], d["K"], p.data_ptr(),
-                                          self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr(),
-                                          L.ptr(sh), d["N"], coef, lr_bc1, bc2_sqrt, float(b1), float(b2),
-                                          float(grp["eps"]), float(grp["weight_decay"]), L.stream_ptr()),
+                off = d.get("row0", 0) * d["N"]  # a sharded gradient covers rows [row0, row0 + M) only
+                L.check(lib.mia_gemm_adam(d["A"], d["B"], d["M"], d["N"], d["K"], p.data_ptr() + 4 * off,
+                                          self.state[p]["exp_avg"].data_ptr() + 4 * off,
+                                          self.state[p]["exp_avg_sq"].data_ptr() + 4 * off,
+                                          0 if sh is None else sh.data_ptr() + 2 * off, d["N"], coef, lr_bc1,
+                                          bc2_sqrt, float(b1), float(b2), float(grp["eps"]),
+                                          float(grp["weight_decay"]), L.stream_ptr()),
                         "mia_gemm_adam")
+                if "row0" in d:
+                    d["shard"].after_shard_update(p, sh, d)
         self.last_total_norm = tot
         for p, sh in zip(ps, shadows):
             if sh is not None:

@@ -336,12 +336,12 @@ def test_attention_bwd_fused_vs_two_pass(cuda, B, N, H):
 @pytest.mark.parametrize("B,N,H", [(2, 1645, 3), (1, 300, 2), (3, 1000, 2), (1, 2050, 1), (2, 777, 2), (4, 64, 3),
                                    (1, 128, 2), (1, 129, 1), (1, 385, 2), (2, 37, 1)])
 def test_attention_bwd_onepass_vs_two_pass(cuda, B, N, H):
-    """The default training backward (mia_attn_bwd_onepass: S, dP, dS once per tile; dQ summed over the 128-key
+    """The one-pass training backward (mia_attn_bwd_onepass: S, dP, dS once per tile; dQ summed over the 256-key
     blocks by the ordered hand-off of running sums) against float64 and the two-kernel form: within the bf16
     bounds of test_attention_fwd_bwd, bit-identical from call to call (fixed summation order), the sticky
     error word still 0 (every bounded hand-off wait matched), nothing written outside dqkv.  The shapes cover
-    the rotation lags 3 (N 385), 2 (N 1645, the benched length), 1 (N 300, 2050: 2 does not fit) and a single
-    key block (N <= 128)."""
+    two to nine key blocks at rotation lag 3 (with 64-query tiles and 256-key blocks lag 3 always leaves two
+    steps between contributions), a single key block (N <= 256, lag 1), ragged tails of both tile sizes."""
     g = torch.Generator().manual_seed(N * 5 + H)
     qkv = (torch.randn(B, N, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16)
     dout = torch.randn(B, N, H * 64, generator=g).to(torch.bfloat16)

@@ -205,3 +205,90 @@ def test_grad_allreducer_fc1_gather_envnet_hip_two_ranks():
         assert fc1_err < 1e-5, fc1_err  # f32 summation order only (dY / 2 is exact in bf16)
         assert not mism, (r, mism[:5])
         assert same, "ranks diverged after FusedAdam.step, or the materialised run differs from the deferred one"
+
+
+def _shard_worker(rank, world, port, q):
+    """fc1_exchange="shard" against "gather" from the same initial state: three data-parallel steps each
+    (FusedAdam with clip + weight decay), so the second and third forwards run on the bf16 FC1 rows the other
+    rank updated and all-gathered.  Clip norms, logits of every step, and -- after sync_sharded() -- every
+    parameter and Adam moment must equal the gather form's bit for bit, on both ranks."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle.synth import synth_waveform
+        from src.miaudio import kernels as K
+        from src.training.ddp import GradAllReducer
+        from src.training.optim import FusedAdam
+        from tests._util import envnet_with_hash_params
+        dev = torch.device("cuda", 0)
+        B = 64
+        x = torch.from_numpy(synth_waveform(81 + rank, B, 220_500)[:, None, :]).to(dev)
+        y = torch.zeros(B, 50, device=dev)
+        y[torch.arange(B), (torch.arange(B) * (5 + rank)) % 50] = 1.0
+
+        def run(mode):
+            m = envnet_with_hash_params(dev, compute_dtype="bf16").train()
+            opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4, clip=1.0)
+            red = GradAllReducer(m, world, fc1_exchange=mode)
+            norms, logits, deferred = [], [], []
+            for _ in range(3):
+                m.zero_grad(set_to_none=True)
+                z = m(x)
+                logits.append(z.detach().cpu())
+                _, dz, _ = K.soft_ce(z.detach().float().contiguous(), y, input_sigmoid=False)
+                z.backward(dz)
+                red.finish()
+                fc1 = dict(m.named_parameters())["classifier.1.weight"]
+                d = fc1._mia_deferred
+                deferred.append(None if d is None else (d["M"], d.get("row0")))
+                opt.step()
+                norms.append(float(opt.last_total_norm))
+            stale = len(red.sharded)
+            red.sync_sharded()
+            torch.cuda.synchronize()
+            state = {n: torch.cat([p.detach().flatten(), opt.state[p]["exp_avg"].flatten(),
+                                   opt.state[p]["exp_avg_sq"].flatten()]).cpu() for n, p in m.named_parameters()}
+            return norms, logits, state, deferred, stale
+
+        ng, lg, sg, dg, _ = run("gather")
+        ns, ls, ss, ds, stale = run("shard")
+        diff = [n for n in sg if not torch.equal(sg[n], ss[n])]
+        same_logits = all(torch.equal(a, b) for a, b in zip(lg, ls))
+        ranks_same = []
+        for n, v in ss.items():
+            parts = [torch.empty_like(v) for _ in range(world)]
+            dist.all_gather(parts, v)
+            ranks_same.append(torch.equal(parts[0], parts[1]))
+        q.put((rank, (ng, ns), same_logits, diff, (dg, ds, stale), all(ranks_same), None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, False, [], None, False, traceback.format_exc()))
+
+
+@pytest.mark.timeout(600)
+def test_grad_allreducer_fc1_shard_matches_gather_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, *rest = q.get(timeout=500)
+        res[r] = rest
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, (norms, same_logits, diff, dinfo, ranks_same, err) in res.items():
+        assert err is None, (r, err)
+        dg, ds, stale = dinfo
+        assert dg == [(4096, None)] * 3, dg  # gather: the whole averaged gradient deferred
+        assert ds == [(2048, 2048 * r)] * 3, ds  # shard: this rank's half of the rows
+        assert stale == 1  # FC1 carried stale rows until sync_sharded()
+        assert norms[0] == norms[1], norms
+        assert same_logits, "forward after a sharded update differs from the gather form"
+        assert not diff, (r, diff[:5])
+        assert ranks_same, "ranks differ after sync_sharded()"

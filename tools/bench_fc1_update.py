@@ -1,8 +1,10 @@
 """EnvNet FC1 (4096 x 84 480) weight update at K = world * 256 gathered rows: the deferred form (sums-only
 GEMM + the Adam GEMM that recomputes the product, what one GPU runs) against the materialised form (one
 GEMM writing the f32 gradient with per-tile sums of squares, then FusedAdam's streaming update), as the
-data-parallel gather form would run them at world = K / 256 (src/training/ddp.py).  HIP events on the
-launch stream, interleaved rounds.
+data-parallel gather form would run them at world = K / 256 (src/training/ddp.py), and the per-rank work of
+the shard form (fc1_exchange="shard": the sums-only and Adam GEMMs over this rank's M / world rows only; the
+comm-stream all-gather of the updated bf16 rows is not in this single-GPU figure).  The bf16 operand copy is
+live (as in training: FusedAdam rewrites it).  HIP events on the launch stream, interleaved rounds.
     python tools/bench_fc1_update.py [K ...]"""
 import sys
 from pathlib import Path
@@ -21,12 +23,27 @@ Ks = [int(k) for k in sys.argv[1:]] or [256, 512, 1024, 2048]
 g = torch.Generator(device=dev).manual_seed(0)
 p = torch.nn.Parameter(torch.randn(M, N, generator=g, device=dev) * 0.01)
 opt = FusedAdam([p], lr=1e-4, weight_decay=1e-4, clip=1.0)
+K.bf16_shadow(p)
+
+
+class _NoComm:  # the shard form's comm-stream all-gather is not part of this figure
+    @staticmethod
+    def after_shard_update(param, shadow, d):
+        pass
 
 
 def step(kind, dy, x, Kk):
     A, B = K.dense(dy, L.RC, Kk, M), K.dense(x, L.RC, Kk, N)
     if kind == "deferred":
         K.defer_weight_grad(p, A, B, M, N, Kk, keep=(dy, x))
+    elif kind == "shard":
+        w = max(1, Kk // 256)
+        Ms = M // w
+        sq = torch.zeros(int(L.load().mia_gemm_sqsum_slots(M, N)), dtype=torch.float64, device=dev)
+        As = K.dense(dy, L.RC, Kk, Ms, ld=M)  # rank 0's rows
+        K.gemm_sqsum_only(As, B, Ms, N, Kk, sq[:sq.numel() // w])
+        p._mia_deferred = dict(A=As, B=B, M=Ms, N=N, K=Kk, sq=sq, keep=(dy, x), row0=0, rows_total=M,
+                               shard=_NoComm)
     else:
         dW = torch.empty(M, N, dtype=torch.float32, device=dev)
         sq = K.sqsum_slots(dW, M, N)
@@ -40,7 +57,7 @@ def step(kind, dy, x, Kk):
 for Kk in Ks:
     dy = (torch.randn(Kk, M, generator=g, device=dev) * 0.01).to(torch.bfloat16)
     x = torch.randn(Kk, N, generator=g, device=dev).to(torch.bfloat16)
-    res = {"deferred": [], "materialised": []}
+    res = {"deferred": [], "materialised": [], "shard": []}
     for r in range(3):
         for kind in res:
             for _ in range(2):
@@ -54,6 +71,6 @@ for Kk in Ks:
             torch.cuda.synchronize()
             res[kind].append(e0.elapsed_time(e1) / 5)
     print(f"K={Kk:5d} (world {Kk // 256}): deferred {min(res['deferred']):.3f} ms  "
-          f"materialised {min(res['materialised']):.3f} ms", flush=True)
+          f"materialised {min(res['materialised']):.3f} ms  shard per rank {min(res['shard']):.3f} ms", flush=True)
     del dy, x
     torch.cuda.empty_cache()
