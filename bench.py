@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--probe", default=None, help="comma list of probe tags to time live (default: auto)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N > 1 ranks on one GPU")
-    ap.add_argument("--fc1-exchange", choices=["gather", "shard", "allreduce"], default="gather",
+    ap.add_argument("--fc1-exchange", choices=["gather", "shard", "allreduce"], default="shard",
                     help="N > 1, EnvNet FC1 weight gradient: all-gather the bf16 operands and defer the averaged "
                          "gradient to the fused Adam GEMM (the N = 1 program), the same with each rank updating "
                          "its row slice only, or materialise + chunked all-reduce")

@@ -368,9 +368,18 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   // step j on tile T (image slot P); HP: finish the previous tile's dQ (from slot P ^ 1) in the same step --
   // its MFMAs in the basic block of the first query half, its running sum fetched mid-step, its link after
   // the second half
+#ifdef CB_STAMP  // timing builds only (tools/bench_attn_bwd.py ATTN_LIBS): s_memtime per step segment
+  unsigned long long* const stamps =
+      reinterpret_cast<unsigned long long*>(chain + (int64_t)(gridDim.x / nkb) * nt * (CB_TILE / 4));
+  unsigned long long ts[7];
+#define CB_TS(k) ts[k] = __builtin_amdgcn_s_memtime()
+#else
+#define CB_TS(k)
+#endif
   auto step = [&](int j, auto par, auto has_prev) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
     constexpr bool HP = decltype(has_prev)::value;
+    CB_TS(0);
     const int pos = ord.pos(T), T1 = ord.next(T);
     if (j + 1 < nt) {  // buffer P^1 was last read by step j - 1's body, before its barrier
       qd.issue(Qb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
@@ -382,17 +391,29 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     f32x16 dq = zero16();  // the previous tile's dQ^T: k-steps 0-7 in this half, 8-15 in the next
     cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 0, dhw, qhw, kf, vf, one, 0, wave,
                         lane);
+    CB_TS(1);
     if constexpr (HP) link_fetch(fv);
     else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile j + 1 landed
     }
+    CB_TS(2);
     cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 8, dhw, qhw, kf, vf, one, 1, wave,
                         lane);
+    CB_TS(3);
     if constexpr (HP) link_store(dq);
+    CB_TS(4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dS^T written
+    CB_TS(5);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+#ifdef CB_STAMP
+    CB_TS(6);
+    if (w < 256 && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) stamps[((int64_t)(w * 4 + wave) * 64 + j) * 8 + k] = ts[k];
+    }
+#endif
     Tp = T;
     pp = pos;
     T = T1;
@@ -460,6 +481,9 @@ static int cb_lag(int32_t N, int keys) {
 }
 
 extern "C" int64_t mia_attn_bwd_chain_bytes(int32_t B, int32_t N, int32_t H) {
+#ifdef CB_STAMP
+  return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE + 256 * 4 * 64 * 8 * 8;
+#endif
   return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE;
 }
 

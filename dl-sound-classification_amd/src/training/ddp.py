@@ -20,7 +20,7 @@ GEMM instead of after all of it (64-128 MB chunks, FC head fir
 ``fc1_exchange`` chooses how a gradient that FusedAdam could take deferred (EnvNet's FC1: dW = dY^T X,
 never written on one GPU; src/miaudio/kernels.py::defer_weight_grad) crosses the ranks:
 
-* ``"gather"`` (default): the backward hands the reducer its two bf16 operands instead of the product;
+* ``"gather"``: the backward hands the reducer its two bf16 operands instead of the product;
   the reducer all-gathers dY (B x 4096, pre-scaled by 1/world) and X (B x 84 480) on the comm stream --
   45 MB per rank instead of a 1.38 GB f32 ring all-reduce -- and ``finish()`` defers the AVERAGED gradient
   (dY_all / world)^T X_all, K = world * B, to FusedAdam exactly as one GPU does.  Every rank runs the same
@@ -29,7 +29,7 @@ never written on one GPU; src/miaudio/kernels.py::defer_weight_grad) crosses the
   ``materialise_k`` gathered rows (world >= 8 at B = 256) the averaged gradient is instead written once by
   the same GEMM with its per-tile sums of squares (the deferred pair recomputes the product; at K = 2048
   that is 5.06 against 4.27 ms per step) -- the same sums, so the same parameters;
-* ``"shard"``: the same all-gather of the two bf16 operands, but rank r owns only rows
+* ``"shard"`` (default): the same all-gather of the two bf16 operands, but rank r owns only rows
   [r M / world, (r + 1) M / world) of FC1 (whole 128-row GEMM tiles): its sums-only GEMM covers that row slice
   of the averaged gradient, the per-tile sums of squares of all slices are all-gathered (the slot array of
   the gather form, so the clip norm is the same bit for bit), and FusedAdam's Adam GEMM updates only the
@@ -72,7 +72,7 @@ MATERIALISE_K = 1536
 
 class GradAllReducer:
     def __init__(self, model: torch.nn.Module, world: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 broadcast_buffers: bool = True, fc1_exchange: str = "gather",
+                 broadcast_buffers: bool = True, fc1_exchange: str = "shard",
                  materialise_k: int = MATERIALISE_K):
         if fc1_exchange not in ("gather", "shard", "allreduce"):
             raise ValueError(f"fc1_exchange must be 'gather', 'shard' or 'allreduce', not {fc1_exchange!r}")
@@ -351,10 +351,10 @@ class GradAllReducer:
         _, r0, Ms, M = info
         K.wait_param(param)
         ref = getattr(param, "_mia_fused_adam", None)
-        opt = ref() if callable(ref) else None
+        st = getattr(ref() if callable(ref) else None, "state", {}).get(param)  # FusedAdam's moments
         ts = [param.data]
-        if opt is not None and param in opt.state:
-            ts += [opt.state[param]["exp_avg"], opt.state[param]["exp_avg_sq"]]
+        if st:
+            ts += [st["exp_avg"], st["exp_avg_sq"]]
         for t in ts:
             t2 = t.view(M, -1)
             self._all_gather(t2, t2[r0:r0 + Ms].clone())

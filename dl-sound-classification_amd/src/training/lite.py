@@ -155,7 +155,7 @@ def _to(batch, dev):
 class Trainer:
     def __init__(self, max_epochs=1, accelerator="auto", precision=32, devices=1, log_every_n_steps=50,
                  gradient_clip_val=0.0, logger=None, callbacks=None, limit_train_batches=None,
-                 limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, fc1_exchange="gather",
+                 limit_val_batches=None, limit_test_batches=None, enable_progress_bar=True, fc1_exchange="shard",
                  dist_backend="nccl", **unused):
         self.fc1_exchange = str(fc1_exchange)  # DDP: how FC1's deferred weight gradient crosses ranks (ddp.py)
         # DDP process-group backend: "nccl" (= RCCL over xGMI, the product path, one GPU per rank) or "gloo"

@@ -124,7 +124,7 @@ def _gather_worker(rank, world, port, q):
         plain = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         m.zero_grad(set_to_none=True)
         opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4, clip=1.0)
-        red = GradAllReducer(m, world)  # default: gather
+        red = GradAllReducer(m, world, fc1_exchange="gather")
         # the plain step above ran without the reducer: redo it under the reducer from the same state
         step()
         red.finish()
@@ -165,7 +165,7 @@ def _gather_worker(rank, world, port, q):
         step()
         m.zero_grad(set_to_none=True)
         opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4, clip=1.0)
-        red = GradAllReducer(m, world, materialise_k=0)
+        red = GradAllReducer(m, world, fc1_exchange="gather", materialise_k=0)
         step()
         red.finish()
         fc1 = dict(m.named_parameters())["classifier.1.weight"]

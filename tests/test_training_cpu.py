@@ -517,7 +517,7 @@ def _gather_worker(rank, world, port, q):
     lin = torch.nn.Linear(6, 4)
     owner = _Owner()
     lin.weight._mia_fused_adam = weakref.ref(owner)
-    red = GradAllReducer(lin, world)
+    red = GradAllReducer(lin, world, fc1_exchange="gather")
     assert lin._grad_gather == red.grad_gather
     g = torch.Generator().manual_seed(50 + rank)
     dy, x = torch.randn(8, 4, generator=g), torch.randn(8, 6, generator=g)
@@ -553,3 +553,71 @@ def test_grad_allreducer_fc1_gather_gloo():
         avg = dy_all.T.astype(np.float64) @ x_all
         want = sum(res[k][3].T.astype(np.float64) @ res[k][4] for k in range(world)) / world
         np.testing.assert_allclose(avg, want, rtol=1e-6, atol=1e-7)
+
+
+def _shard_worker(rank, world, port, q):
+    """GradAllReducer(fc1_exchange="shard") plumbing on CPU/gloo: ``finish()`` defers only this rank's row slice
+    of the averaged gradient (A = the slice's columns of the gathered dY, ld = M) and all-gathers every rank's
+    per-tile sums of squares into the full slot array; after the update the operand rows are all-gathered and
+    ``sync_sharded()`` brings back the parameter rows and moments.  The HIP GEMMs are replaced by recorders."""
+    import weakref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src.miaudio import kernels as K
+    from src.training.ddp import GradAllReducer
+    rec = []
+
+    def sums_only(A, B, M, N, Kk, sq, tag=None):
+        sq.fill_(10.0 * rank + 1.0)  # this rank's tiles
+        rec.append((A.ptr, A.rows, A.cols, A.ld, M, N, Kk))
+
+    K.gemm_sqsum_only = sums_only
+    M, N, B = 256, 6, 8
+    lin = torch.nn.Linear(N, M)
+    owner = _Owner()
+    lin.weight._mia_fused_adam = weakref.ref(owner)
+    red = GradAllReducer(lin, world)  # default: shard
+    g = torch.Generator().manual_seed(70 + rank)
+    dy, x = torch.randn(B, M, generator=g), torch.randn(B, N, generator=g)
+    assert red.grad_gather(lin.weight, dy, x)
+    red.finish()
+    d = lin.weight._mia_deferred
+    dy_all = d["keep"][0]
+    aptr, arows, acols, ald, Ms, Nn, Kk = rec[0]
+    sl = (aptr - dy_all.data_ptr()) // dy_all.element_size()
+    # what FusedAdam's Adam GEMM would write: this rank's rows of the parameter (here: a marker)
+    with torch.no_grad():
+        lin.weight[d["row0"]:d["row0"] + d["M"]] = float(rank + 1)
+    red.after_shard_update(lin.weight, None, d)
+    after = lin.weight.detach().clone()
+    stale = len(red.sharded)
+    red.sync_sharded()
+    q.put((rank, (d["M"], d["row0"], d["rows_total"], Kk), (arows, acols, ald, sl), d["sq"].tolist(), stale,
+           after.numpy(), len(red.sharded)))
+    dist.destroy_process_group()
+
+
+def test_grad_allreducer_fc1_shard_gloo():
+    import numpy as np
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, *rest = q.get(timeout=60)
+        res[r] = rest
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        dinfo, ainfo, sq, stale, after, left = res[r]
+        assert dinfo == (128, 128 * r, 256, 8 * world)  # rows [128 r, 128 r + 128) of M = 256, K = world * B
+        assert ainfo == (8 * world, 128, 256, 128 * r)  # A: K x 128 columns of dY_all starting at column 128 r
+        assert sq == [1.0, 11.0]  # the full slot array: rank 0's tiles, then rank 1's
+        assert stale == 1 and left == 0
+        # the operand rows of both ranks after the all-gather
+        np.testing.assert_array_equal(after[:128], 1.0)
+        np.testing.assert_array_equal(after[128:], 2.0)

@@ -28,6 +28,12 @@ for s in $STAGES; do
     attnbwd)
       BATCH=${BATCH:-256} timeout -k 10 300 python -u tools/bench_attn_bwd.py > $OUT/attn_bwd.log 2>&1
       rc=$? ;;
+    fc1upd)
+      timeout -k 10 300 python -u tools/bench_fc1_update.py 256 512 1024 2048 > $OUT/fc1upd.log 2>&1
+      rc=$? ;;
+    stamps)
+      BATCH=${BATCH:-256} timeout -k 10 200 python -u tools/attn_bwd_stamps.py > $OUT/stamps.log 2>&1
+      rc=$? ;;
     attnpmc)
       bash tools/attn_bwd_pmc.sh $TAG/attnpmc > $OUT/attnpmc.log 2>&1
       rc=$? ;;
