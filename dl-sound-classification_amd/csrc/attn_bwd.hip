@@ -105,20 +105,40 @@ constexpr int CB2L_BYTES = CB2L_K + 32768;       // 135 168 B: one workgroup per
 // under the softmax of half 1; D = dV / dK of half 1 and four more dQ k-steps.  sched_group_barrier lays one
 // MFMA and its share of the stage's other instructions into each MFMA gap.  dq: k-steps kq0 .. kq0 + 7 of the
 // previous tile's dQ^T (A = K^T from the block's image Kt, B = that tile's dS^T image dsP), DQ: any at all.
-template <bool DQ>
-__device__ __forceinline__ void cb2_half_staged(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2], f32x16& dq,
+#ifndef CB_LEAD
+#define CB_LEAD 3  // MFMAs issued at the head of stages B and C before any VALU
+#endif
+#ifndef CB_PREF
+#define CB_PREF true  // read query half 1's S / dP operands during half 0's last stage
+#endif
+// The S / dP row operands of a query half (Q' and dO row fragments, the two row-constant fragments)
+struct HalfOps {
+  bf16x8 qa[4], ga[4], fl, fd;
+  __device__ __forceinline__ void load(const bf16* Q_, const bf16* G_, const bf16* F_, int sq, int lane) {
+    const int qr = sq * 32 + (lane & 31);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qa[ks] = frag_row_sw(Q_, qr, ks, lane);
+      ga[ks] = frag_row_sw(G_, qr, ks, lane);
+    }
+    fl = row_frag(F_ + qr * 8);
+    fd = row_frag(F_ + 512 + qr * 8);
+  }
+};
+
+// PRE: op already holds this half's operands (read during the previous half); NEXT: read query half 1's
+// operands into op during stage D (the S / dP MFMAs that used op are done by then), so half 1 starts on
+// operands that are already in registers instead of waiting out the LDS latency
+template <bool DQ, bool PRE, bool NEXT>
+__device__ __forceinline__ void cb2_half_staged(f32x16 (&dk)[2][2], f32x16 (&dv)[2][2], f32x16& dq, HalfOps& op,
                                                 const bf16* Q_, const bf16* G_, const bf16* F_, bf16* dsT,
                                                 const bf16* Kt, const bf16* dsP, int kq0, int dhw, int qhw,
                                                 const bf16x8 (&kf)[2][4], const bf16x8 (&vf)[2][4], bf16x8 one,
                                                 int sq, int wave, int lane) {
-  const int qr = sq * 32 + (lane & 31);
-  bf16x8 qa[4], ga[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qa[ks] = frag_row_sw(Q_, qr, ks, lane);
-    ga[ks] = frag_row_sw(G_, qr, ks, lane);
-  }
-  const bf16x8 fl = row_frag(F_ + qr * 8), fd = row_frag(F_ + 512 + qr * 8);
+  if constexpr (!PRE) op.load(Q_, G_, F_, sq, lane);
+  const bf16x8 (&qa)[4] = op.qa;
+  const bf16x8 (&ga)[4] = op.ga;
+  const bf16x8 fl = op.fl, fd = op.fd;
   __builtin_amdgcn_sched_barrier(0);
   // ---- A
   f32x16 sc[2], dp[2];
@@ -178,12 +198,17 @@ __device__ __forceinline__ void cb2_half_staged(f32x16 (&dk)[2][2], f32x16 (&dv)
   };
   sdp(1);
   softmax(0);
+  // the first MFMAs go out alone: half 0's S / dP chains (stage A's last MFMAs) complete under them before
+  // the first exp needs them (in-order issue: a stalled VALU would hold every MFMA behind it)
+  __builtin_amdgcn_sched_group_barrier(0x008, CB_LEAD, 1);
 #pragma unroll
-  for (int g = 0; g < 10; ++g) {
+  for (int g = 0; g < 10 - CB_LEAD; ++g) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
     __builtin_amdgcn_sched_group_barrier(0x002, 7, 1);  // VALU
     if (g & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);  // DS write
   }
+  __builtin_amdgcn_sched_group_barrier(0x002, 64, 1);  // the rest of the VALU
+  __builtin_amdgcn_sched_group_barrier(0x200, 8, 1);
   __builtin_amdgcn_sched_barrier(0);
   // ---- C
   auto dvdk = [&](int kk) __attribute__((always_inline)) {
@@ -206,19 +231,31 @@ __device__ __forceinline__ void cb2_half_staged(f32x16 (&dk)[2][2], f32x16 (&dv)
     }
   }
   softmax(1);
+  __builtin_amdgcn_sched_group_barrier(0x008, CB_LEAD, 2);  // as in B: half 1's S / dP complete first
 #pragma unroll
-  for (int g = 0; g < (DQ ? 12 : 8); ++g) {
+  for (int g = 0; g < (DQ ? 12 : 8) - CB_LEAD; ++g) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);  // MFMA
     __builtin_amdgcn_sched_group_barrier(0x002, 6, 2);  // VALU
     if (DQ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);  // DS read
     if (g & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 2);  // DS write
   }
+  __builtin_amdgcn_sched_group_barrier(0x002, 64, 2);
+  __builtin_amdgcn_sched_group_barrier(0x100, 8, 2);
+  __builtin_amdgcn_sched_group_barrier(0x200, 8, 2);
   __builtin_amdgcn_sched_barrier(0);
-  // ---- D
-  dvdk(1);
+  // ---- D: the dQ k-steps (independent of softmax(1)) first, while its last bf16 operands settle
   if constexpr (DQ) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) dq = mfma(ka[1][ks], sf[1][ks], dq);
+  }
+  dvdk(1);
+  if constexpr (NEXT) {
+    op.load(Q_, G_, F_, 1, lane);
+#pragma unroll
+    for (int g = 0; g < 10; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 3);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 3);  // DS read
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
 }
@@ -298,6 +335,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   int pub_T = 0;
   unsigned pub_val = 0;
   u32x4 run[4];      // the running sum of the previous step's tile (loaded in the middle of that step)
+#ifdef CB_STAMP  // timing builds only (tools/attn_bwd_stamps.py): s_memtime per step segment
+  unsigned long long* const stamps =
+      reinterpret_cast<unsigned long long*>(chain + (int64_t)(gridDim.x / nkb) * nt * (CB_TILE / 4));
+  unsigned long long ts[16] = {};
+#define CB_TS(k) ts[k] = __builtin_amdgcn_s_memtime()
+#else
+#define CB_TS(k)
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K fragments in registers before slot 1 is reused
   // dQ of the tile of step jp (image slot SP), its running sum added, handed on or written as bf16
   // dQ^T of the previous step's tile from dS^T image SP (16 MFMAs over the block's 256 keys)
@@ -322,11 +367,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   // publish them; then the predecessor's running sum of tile Tp into registers
   auto link_fetch = [&](unsigned fv) __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    CB_TS(7);
+    // the flag value into an SGPR BEFORE the publish store: vmcnt counts stores too, and a wait for the
+    // flag load placed after the store would wait for the store's acknowledgement (~500 cycles a step)
+    const unsigned fs = __builtin_amdgcn_readfirstlane(fv);
+    asm volatile("; flag read" ::"s"(fs));
     if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
     pub = false;
+    CB_TS(8);
     if (pp > 0) {
-      if (__builtin_expect(__builtin_amdgcn_readfirstlane(fv) != (unsigned)pp, 0))
+      if (__builtin_expect(fs != (unsigned)pp, 0)) {
+        CB_TS(10);
         cb_spin(fl + Tp * 4 + wave, (unsigned)pp, err);
+      }
+      CB_TS(9);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, Tp * CB_TILE + wave * CB_SUB + g * 1024, 16);
@@ -368,14 +422,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
   // step j on tile T (image slot P); HP: finish the previous tile's dQ (from slot P ^ 1) in the same step --
   // its MFMAs in the basic block of the first query half, its running sum fetched mid-step, its link after
   // the second half
-#ifdef CB_STAMP  // timing builds only (tools/bench_attn_bwd.py ATTN_LIBS): s_memtime per step segment
-  unsigned long long* const stamps =
-      reinterpret_cast<unsigned long long*>(chain + (int64_t)(gridDim.x / nkb) * nt * (CB_TILE / 4));
-  unsigned long long ts[7];
-#define CB_TS(k) ts[k] = __builtin_amdgcn_s_memtime()
-#else
-#define CB_TS(k)
-#endif
   auto step = [&](int j, auto par, auto has_prev) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
     constexpr bool HP = decltype(has_prev)::value;
@@ -389,16 +435,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     unsigned fv = 0;
     if (HP && pp > 0) fv = cb_load_flag(flr, (Tp * 4 + wave) * 4);  // Tp's predecessor (checked mid-step)
     f32x16 dq = zero16();  // the previous tile's dQ^T: k-steps 0-7 in this half, 8-15 in the next
-    cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 0, dhw, qhw, kf, vf, one, 0, wave,
-                        lane);
+    HalfOps op;
+    cb2_half_staged<HP, false, CB_PREF>(dk, dv, dq, op, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 0, dhw, qhw, kf, vf,
+                                     one, 0, wave, lane);
     CB_TS(1);
     if constexpr (HP) link_fetch(fv);
     else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile j + 1 landed
     }
     CB_TS(2);
-    cb2_half_staged<HP>(dk, dv, dq, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 8, dhw, qhw, kf, vf, one, 1, wave,
-                        lane);
+    cb2_half_staged<HP, CB_PREF, false>(dk, dv, dq, op, Qb(P), Gb(P), Fb(P), Sb(P), Kt, Sb(P ^ 1), 8, dhw, qhw, kf, vf,
+                                     one, 1, wave, lane);
     CB_TS(3);
     if constexpr (HP) link_store(dq);
     CB_TS(4);
@@ -411,7 +458,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_chain2_kernel(const bf16* __r
     CB_TS(6);
     if (w < 256 && lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 7; ++k) stamps[((int64_t)(w * 4 + wave) * 64 + j) * 8 + k] = ts[k];
+      for (int k = 0; k < 16; ++k) stamps[((int64_t)(w * 4 + wave) * 64 + j) * 16 + k] = ts[k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) ts[k] = 0;
     }
 #endif
     Tp = T;
@@ -482,7 +531,7 @@ static int cb_lag(int32_t N, int keys) {
 
 extern "C" int64_t mia_attn_bwd_chain_bytes(int32_t B, int32_t N, int32_t H) {
 #ifdef CB_STAMP
-  return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE + 256 * 4 * 64 * 8 * 8;
+  return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE + 256 * 4 * 64 * 16 * 8;
 #endif
   return cb_flags_bytes(B, N, H) + (int64_t)B * H * cdiv(N, 64) * CB_TILE;
 }

@@ -30,7 +30,7 @@ x.mia_attn_bwd_chain_bytes.restype = C.c_int64
 x.mia_attn_bwd_chain_bytes.argtypes = [C.c_int32] * 3
 plain = int(lib.mia_attn_bwd_chain_bytes(B, N, H))
 chain = torch.zeros(int(x.mia_attn_bwd_chain_bytes(B, N, H)), dtype=torch.uint8, device=dev)
-assert chain.numel() > plain, "not a CB_STAMP build"
+assert chain.numel() > plain + 256 * 4 * 64 * 16 * 8 - 1, "not a CB_STAMP build"
 err = torch.zeros(1, dtype=torch.int32, device=dev)
 dq = torch.empty_like(qkv)
 ms = []
@@ -45,10 +45,11 @@ for _ in range(4):
 print(f"stamp build: {min(ms):.3f} ms per call, error word {int(err.item())}")
 nt = (N + 63) // 64
 flags_bytes = plain - B * H * nt * 16384
-st = chain[plain:plain + 256 * 4 * 64 * 8 * 8].view(torch.int64).cpu().numpy().reshape(256, 4, 64, 8)[:, :, :nt, :7]
+st = chain[plain:plain + 256 * 4 * 64 * 16 * 8].view(torch.int64).cpu().numpy().reshape(256, 4, 64, 16)[:, :, :nt, :]
 st = st.astype(np.float64)
-names = ["issue+half0", "link_fetch", "half1", "link_store", "lgkm wait", "barrier"]
-seg = np.diff(st, axis=3)  # [w][wave][j][6]
+order = [0, 1, 7, 8, 9, 2, 3, 4, 5, 6]  # 7 after the mid-step vmcnt(0), 8 after the flag publish, 9 after the spin
+names = ["issue+half0", "vmcnt(0)", "publish", "flag/spin", "run loads", "half1", "link_store", "lgkm wait", "barrier"]
+seg = np.diff(st[..., order], axis=3)
 mid = seg[:, :, 2:nt - 1, :]
 print(f"steps 2..{nt - 2}, 256 work items x 4 waves: median / mean cycles per segment")
 for k, n in enumerate(names):
@@ -56,8 +57,8 @@ for k, n in enumerate(names):
     print(f"  {n:12s} median {np.median(v):8.0f}  mean {v.mean():8.0f}  p90 {np.percentile(v, 90):8.0f}")
 step = st[:, :, 3:nt, 0] - st[:, :, 2:nt - 1, 0]
 print(f"  step total   median {np.median(step):8.0f}  mean {step.mean():8.0f}")
+spun = st[:, :, 2:nt - 1, 10] != 0
+print(f"steps whose start-of-step flag was not ready (spun): {spun.mean():.3f}")
 for wv in range(4):
-    print(f"  wave {wv}: " + " ".join(f"{np.median(mid[:, wv, :, k]):6.0f}" for k in range(6)))
-first = st[:, :, 0, 0]
-print(f"step-0 start spread over the 256 items: {np.ptp(first) :.0f} cycles; kernel span of item 0 wave 0: "
-      f"{st[0, 0, nt - 1, 6] - st[0, 0, 0, 0]:.0f}")
+    print(f"  wave {wv}: " + " ".join(f"{np.median(mid[:, wv, :, k]):6.0f}" for k in range(len(names))))
+print(f"kernel span of item 0 wave 0: {st[0, 0, nt - 1, 6] - st[0, 0, 0, 0]:.0f} cycles")
