@@ -289,8 +289,28 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
   const bool bf_out = EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_GELU_SAVE_D || DG ||
                       (EPI == EPI_PLAIN && !g.out_f32);
   if (!bf_out) {
+    // ADD_AUX: the residual rows of fragment row i + 2 are requested while row i is added and stored (a
+    // rolling three-row window of loads in flight instead of a wait at every fragment)
+    f32x4 ax[8][4];
+    auto ld_row = [&](int i) __attribute__((always_inline)) {
+      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+        ax[i][j] = (m < g.M && n < g.N)
+                       ? *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g.aux) + m * g.ldaux + n)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    if constexpr (EPI == EPI_ADD_AUX) {
+      ld_row(0);
+      ld_row(1);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if constexpr (EPI == EPI_ADD_AUX) {
+        if (i + 2 < 8) ld_row(i + 2);
+      }
       const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
       if (m >= g.M) continue;
 #pragma unroll
@@ -298,8 +318,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
         const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
         if (n >= g.N) continue;
         f32x4 v = acc[i][j] + bias4[j];
-        if constexpr (EPI == EPI_ADD_AUX)
-          v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g.aux) + m * g.ldaux + n);
+        if constexpr (EPI == EPI_ADD_AUX) v += ax[i][j];
         float* dst = EPI == EPI_SLAB ? g.ws + ((int64_t)z * g.M + m) * g.N + n
                                      : reinterpret_cast<float*>(g.out) + m * g.ldc + n;
         *reinterpret_cast<f32x4*>(dst) = v;
@@ -313,6 +332,20 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
     // conflict-free 8-B writes (16 rows of one column group) and 16-B row reads.
     __syncthreads();
     char* img = smem + wave * 16384;
+    // the backward epilogues' aux rows (saved gelu'(u) / u) requested before the image pass, so their
+    // latency runs under it instead of under the store loop (fc2.dgrad 1.99 -> 1.73 ms at B = 256,
+    // tools/gemm_epi_ab.sh, gpurun_out r5o / r5p)
+    uint4 ua[16];
+    if constexpr (DG) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = 8 * it + (lane >> 3);
+        const int64_t m = m0 + wr * 128 + r, n = n0 + wc * 64 + 8 * (lane & 7);
+        ua[it] = (m < g.M && n < g.N)
+                     ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)
+                     : make_uint4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -328,7 +361,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
 #pragma unroll
     for (int c = 0; c < 8; ++c) cs[c] = 0.f;
     const int cc = lane & 7;
-#pragma unroll 4
+#pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int r = 8 * it + (lane >> 3);
       const uint4 q = *reinterpret_cast<const uint4*>(img + r * 128 + ((cc ^ (r & 7) ^ ((r >> 3) & 1)) << 4));
@@ -341,8 +374,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
       if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_GELU_SAVE_D || DG) {
         f32x4 v0 = unpack4(make_uint2(q.x, q.y)), v1 = unpack4(make_uint2(q.z, q.w));
         if constexpr (DG) {
-          const uint4 u = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)
-                             : make_uint4(0, 0, 0, 0);
+          const uint4 u = ua[it];
           const f32x4 u0 = unpack4(make_uint2(u.x, u.y)), u1 = unpack4(make_uint2(u.z, u.w));
           if constexpr (EPI == EPI_DGELU) {
             dgelu4(v0, u0);

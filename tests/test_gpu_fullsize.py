@@ -77,7 +77,7 @@ def test_envnet_bf16_step_b256_deferred_fc1_vs_autocast_oracle(cuda):
 
     r16, r32 = ref(True), ref(False)
     _check("envnet-b256", zz, loss, total, deltas, {}, r16, r32,
-           tol={"logits": 0.2, "loss": 0.03, "gradnorm": 0.03, "sign": 0.95})
+           tol={"logits": 0.17, "logits_f32": 0.12, "loss": 0.03, "gradnorm": 0.03, "sign": 0.95})
 
 
 def _ast(cuda, cd, depth, st, hw, hb):
@@ -131,9 +131,9 @@ def test_ast_depth12_bf16_step_b32_vs_autocast_oracle(cuda):
 
 
 def test_attention_benched_grid_b256_h12(cuda):
-    """mia_attn_fwd_save_q / mia_attn_bwd_saved_q (the training form) over the whole benched grid
-    (B*H = 3 072 blocks of 13 query / key blocks each); sampled (clip, head) pairs against float64, with the
-    bounds of test_gpu_ast.test_attention_fwd_bwd (bf16)."""
+    """mia_attn_fwd_save_q / mia_attn_bwd_saved_q (the training form) and the one-pass / fused backwards over
+    the whole benched grid (B*H = 3 072 (clip, head) pairs of 1 645 tokens); every pair against float64, with
+    the bounds of test_gpu_ast.test_attention_fwd_bwd (bf16)."""
     from src.miaudio import lib as L
     B, N, H = 256, 1645, 12
     g = torch.Generator(device=cuda).manual_seed(5)
@@ -160,8 +160,8 @@ def test_attention_benched_grid_b256_h12(cuda):
     assert int(work[off:off + 4].view(torch.int32).item()) == 0
     e = float((dq2.float() - dq.float()).abs().max() / dq.float().abs().max())
     assert e < 5e-3, e
-    # the default training backward (one pass, 13 key blocks of 128 per (b, h) handing dQ on at lag 2): the
-    # sticky error word still 0, bit-identical from call to call, the two-kernel result up to summation order
+    # the one-pass backward (7 key blocks of 256 per (b, h) handing dQ on at lag 3): the sticky error word
+    # still 0, bit-identical from call to call, the two-kernel result up to summation order
     err = torch.zeros(1, dtype=torch.int32, device=cuda)
     chain = torch.empty(int(lib.mia_attn_bwd_chain_bytes(B, N, H)), dtype=torch.uint8, device=cuda)
     ones = []
@@ -176,20 +176,32 @@ def test_attention_benched_grid_b256_h12(cuda):
     assert torch.equal(ones[0], ones[1])
     e = float((ones[0].float() - dq.float()).abs().max() / dq.float().abs().max())
     assert e < 5e-3, e
+    one = ones[0]
     del chain, ones
+    # EVERY (clip, head) pair of the grid against float64 (computed on the GPU, one clip's 12 heads at a
+    # time): forward output and lse, and the three gradients of both the two-kernel and the one-pass form,
+    # each within the bounds of test_gpu_ast.test_attention_fwd_bwd (max |error| / max |reference| per pair)
     qkv4 = qkv.view(B, N, 3, H, 64)
-    for b, h in [(0, 0), (1, 11), (97, 5), (128, 0), (200, 7), (255, 11)]:
-        q, k, v = (qkv4[b, :, i, h].double().requires_grad_(True) for i in range(3))
-        o = torch.softmax(q @ k.t() / 8.0, -1) @ v
-        o.backward(dout.view(B, N, H, 64)[b, :, h].double())
-        got = out.view(B, N, H, 64)[b, :, h].double()
-        assert float((got - o).abs().max() / o.abs().max()) < 2e-2, (b, h)
-        lref = torch.logsumexp(q.detach() @ k.detach().t() / 8.0, -1)
-        assert float((lse[b, h].double() - lref).abs().max()) < 2e-2, (b, h)
-        d4 = dq.view(B, N, 3, H, 64)
-        for i, ref in enumerate((q.grad, k.grad, v.grad)):
-            e = float((d4[b, :, i, h].double() - ref).abs().max() / ref.abs().max())
-            assert e < 6e-2, (b, h, "qkv"[i], e)
+    worst = {"out": 0.0, "lse": 0.0, "two": 0.0, "one": 0.0}
+    for b in range(B):
+        q, k, v = (qkv4[b, :, i].permute(1, 0, 2).double().requires_grad_(True) for i in range(3))
+        s_ = (q @ k.transpose(1, 2)) / 8.0
+        o = torch.softmax(s_, -1) @ v
+        o.backward(dout.view(B, N, H, 64)[b].permute(1, 0, 2).double())
+        with torch.no_grad():
+            got = out.view(B, N, H, 64)[b].permute(1, 0, 2).double()
+            worst["out"] = max(worst["out"], float(((got - o).abs().amax((1, 2)) / o.abs().amax((1, 2))).max()))
+            lref = torch.logsumexp(s_, -1)
+            worst["lse"] = max(worst["lse"], float((lse[b].double() - lref).abs().max()))
+            for name, d in (("two", dq), ("one", one)):
+                d4 = d.view(B, N, 3, H, 64)[b]
+                for i, ref in enumerate((q.grad, k.grad, v.grad)):
+                    e = (d4[:, i].permute(1, 0, 2).double() - ref).abs().amax((1, 2)) / ref.abs().amax((1, 2))
+                    worst[name] = max(worst[name], float(e.max()))
+        del q, k, v, s_, o
+    print("benched grid, all 3 072 (clip, head) pairs vs float64, worst per-pair max-relative:", worst)
+    assert worst["out"] < 2e-2 and worst["lse"] < 2e-2, worst
+    assert worst["two"] < 6e-2 and worst["one"] < 6e-2, worst
 
 
 def test_envnet_eval_batch_independence_b256(cuda):

@@ -1,5 +1,7 @@
 """Time mia_gemm on the AST linear shapes with the epilogues the AST step uses (one process).
-    TOKENS=421120 python tools/bench_gemm.py [name ...]
+    TOKENS=310784 python tools/bench_gemm.py [name[:epilogue] ...]
+(an explicit epilogue overrides the shape's own: plain, bias, gelu, gelu_save, gelu_save_d, dgelu, dmul, dmul_nocs,
+residual, f32 -- the epilogue ablations of one shape)
 Prints ms and TFLOP/s per shape (random bf16 operands; HIP events on the launch stream)."""
 import os
 import sys
@@ -12,7 +14,7 @@ import torch  # noqa: E402
 from src.miaudio import kernels as K  # noqa: E402
 from src.miaudio import lib as L  # noqa: E402
 
-T = int(os.environ.get("TOKENS", 421120))
+T = int(os.environ.get("TOKENS", 310784))
 REPS = int(os.environ.get("REPS", 10))
 # (name, M, N, K, la, lb, epilogue kind)
 SHAPES = [
@@ -25,13 +27,15 @@ SHAPES = [
 ]
 
 def main():
-    want = set(sys.argv[1:])
+    want = sys.argv[1:] or [s[0] for s in SHAPES]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     total = 0.0
-    for name, M, N, Kd, la, lb, epi in SHAPES:
-        if want and name not in want:
-            continue
+    table = {s[0]: s for s in SHAPES}
+    for w in want:
+        name, _, over = w.partition(":")
+        _, M, N, Kd, la, lb, epi = table[name]
+        epi = over or epi
         a = (torch.randn(M, Kd, generator=g, device=dev) if la == L.KC else torch.randn(Kd, M, generator=g, device=dev))
         a = a.to(torch.bfloat16)
         b = (torch.randn(N, Kd, generator=g, device=dev) if lb == L.KC else torch.randn(Kd, N, generator=g, device=dev))
@@ -50,11 +54,18 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             u = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             E = K.epilogue(out, N, act=L.ACT_GELU_SAVE, bias=bias, aux=u, ldaux=N)
-        elif epi == "dgelu":
+        elif epi == "gelu_save_d":
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            u = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            E = K.epilogue(out, N, act=L.ACT_GELU_SAVE_D, bias=bias, aux=u, ldaux=N)
+        elif epi == "gelu":
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            E = K.epilogue(out, N, act=L.ACT_GELU, bias=bias)
+        elif epi in ("dgelu", "dmul", "dmul_nocs"):
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             u = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
-            cs = torch.empty(N, device=dev)
-            E = K.epilogue(out, N, act=L.DACT_GELU, aux=u, ldaux=N, colsum=cs)
+            cs = torch.empty(N, device=dev) if epi != "dmul_nocs" else None
+            E = K.epilogue(out, N, act=L.DACT_GELU if epi == "dgelu" else L.DACT_MUL, aux=u, ldaux=N, colsum=cs)
         else:
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             E = K.epilogue(out, N, bias=bias if epi == "bias" else None)
@@ -70,7 +81,7 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / REPS
         total += ms
-        print(f"path {path} {name:11s} {epi:9s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
+        print(f"path {path} {name:11s} {epi:11s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
               f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
         del a, b, A, Bo, E, out
         torch.cuda.empty_cache()
