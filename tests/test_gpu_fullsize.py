@@ -191,16 +191,19 @@ def test_attention_benched_grid_b256_h12(cuda):
         with torch.no_grad():
             got = out.view(B, N, H, 64)[b].permute(1, 0, 2).double()
             worst["out"] = max(worst["out"], float(((got - o).abs().amax((1, 2)) / o.abs().amax((1, 2))).max()))
+            # lse relative to the clip's score range: Q' = bf16(q scale log2 e) rounds every score by up to
+            # 2^-9 of its size (here |S| reaches ~12; test_attention_fwd_bwd's 2e-2 absolute is for |S| ~ 4)
             lref = torch.logsumexp(s_, -1)
-            worst["lse"] = max(worst["lse"], float((lse[b].double() - lref).abs().max()))
+            worst["lse"] = max(worst["lse"], float((lse[b].double() - lref).abs().max() / s_.abs().max()))
             for name, d in (("two", dq), ("one", one)):
                 d4 = d.view(B, N, 3, H, 64)[b]
                 for i, ref in enumerate((q.grad, k.grad, v.grad)):
                     e = (d4[:, i].permute(1, 0, 2).double() - ref).abs().amax((1, 2)) / ref.abs().amax((1, 2))
                     worst[name] = max(worst[name], float(e.max()))
         del q, k, v, s_, o
-    print("benched grid, all 3 072 (clip, head) pairs vs float64, worst per-pair max-relative:", worst)
-    assert worst["out"] < 2e-2 and worst["lse"] < 2e-2, worst
+    print("benched grid, all 3 072 (clip, head) pairs vs float64, worst per-pair max-relative (lse: absolute "
+          "error / max |S| of the clip):", worst)
+    assert worst["out"] < 2e-2 and worst["lse"] < 4e-3, worst
     assert worst["two"] < 6e-2 and worst["one"] < 6e-2, worst
 
 

@@ -1,0 +1,219 @@
+// Experiment (not product code): where the one-pass attention backward's cost comes from.  The two-pass
+// dK/dV kernel's structure (4 waves x 32 keys = 128 keys per block, two blocks per CU) with the one-pass
+// additions switched on one at a time (XQ): 0 = dK / dV only, 1 = + the dS^T image writes, 2 = + the
+// per-tile barrier and the dQ^T MFMAs over the block's keys (summed, one store at the end), 3 = + the
+// per-tile bf16 dQ stores (every key block writes its partial: wrong dQ, timing only), 4 = 3 with the dQ of
+// tile j computed between the two query halves of step j + 1 (from the other dS^T image) instead of after
+// the barrier.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DXQ=<n> -I dl-sound-classification_amd/csrc \
+//         tools/probe/exp_dkdvq.hip dl-sound-classification_amd/csrc/runtime.hip -o tools/probe/libxq<n>.so
+#include "attn_common.h"
+
+#ifndef XQ
+#define XQ 0
+#endif
+
+namespace {
+constexpr int XK = 128;
+constexpr int XL_Q = 0, XL_G = 16384, XL_F = 32768, XL_S = 36864, XL_BYTES = XL_S + 2 * 16384;
+
+struct FragDMA2 {
+  __amdgpu_buffer_rsrc_t rsrc;
+  __device__ __forceinline__ void init(const bf16* g, int N, int wave) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(g + (int64_t)(wave & 1) * N * 8), 0, N * 16, 0x00020000);
+  }
+  __device__ __forceinline__ void issue(bf16* tile, unsigned row0, int wave, int lane) const {
+    if (wave < 2) lds_dma16(rsrc, tile + wave * 512, lane * 16, row0 * 16);
+  }
+};
+
+__device__ __forceinline__ void xhalf(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_, const bf16* F_,
+                                      bf16* dsT, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one, int sq,
+                                      int wave, int lane) {
+  const int qr = sq * 32 + (lane & 31);
+  const int krow = 32 * wave + (lane & 31);
+  f32x16 sc = mfma(frag_row_sw(Q_, qr, 0, lane), kf[0], zero16());
+  f32x16 dp = mfma(frag_row_sw(G_, qr, 0, lane), vf[0], zero16());
+#pragma unroll
+  for (int ks = 1; ks < 4; ++ks) {
+    sc = mfma(frag_row_sw(Q_, qr, ks, lane), kf[ks], sc);
+    dp = mfma(frag_row_sw(G_, qr, ks, lane), vf[ks], dp);
+  }
+  sc = mfma(row_frag(F_ + qr * 8), one, sc);
+  dp = mfma(row_frag(F_ + 512 + qr * 8), one, dp);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(sc[r]);
+    sc[r] = p;
+    dp[r] *= p;
+  }
+#pragma unroll
+  for (int sk = 0; sk < 2; ++sk) {
+    const bf16x8 pf = acc_frag(sc, sk), df = acc_frag(dp, sk);
+    if constexpr (XQ >= 1) {
+      const int qa4 = sq * 32 + 16 * sk + 4 * (lane >> 5);
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4)) = bf16x4{df[0], df[1], df[2], df[3]};
+      *reinterpret_cast<bf16x4*>(dsT + sw_off(krow, qa4 + 8)) = bf16x4{df[4], df[5], df[6], df[7]};
+    }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      dv[dh] = mfma(frag_tr_sw(G_, sq * 32 + 16 * sk, 32 * dh, lane), pf, dv[dh]);
+      dk[dh] = mfma(frag_tr_sw(Q_, sq * 32 + 16 * sk, 32 * dh, lane), df, dk[dh]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void xq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                     const bf16* __restrict__ qs, const bf16* __restrict__ frag,
+                                                     bf16* __restrict__ dqkv, int N, int H, int nkb, float scale,
+                                                     float dk_scale) {
+  __shared__ __attribute__((aligned(1024))) char lds[XL_BYTES];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);
+  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
+  const int nt = (N + 63) / 64;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + XL_S + 16384);
+  {
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = 32 * wave + 8 * i + (lane >> 3);
+      const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
+      lds_dma16(kr, Kt + (4 * wave + i) * 512, vo, (unsigned)((int64_t)(kb * XK + 32 * wave + 8 * i) * ldt * 2));
+    }
+  }
+  TileDMA qd, gd;
+  FragDMA2 fd;
+  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  fd.init(frag + (int64_t)bh * 2 * N * 8, N, wave);
+  auto Qb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_Q + P * 8192); };
+  auto Gb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_G + P * 8192); };
+  auto Fb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_F + P * 2048); };
+  qd.issue(Qb(0), 0u, wave);
+  gd.issue(Gb(0), 0u, wave);
+  fd.issue(Fb(0), 0u, wave, lane);
+  const int key = kb * XK + wave * 32 + (lane & 31);
+  bf16x8 vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
+  settle(vf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int dhw = wave & 1, qhw = wave >> 1;
+  bf16x8 kf[4], kt[8];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kf[ks] = frag_row_sw(Kt, 32 * wave + (lane & 31), ks, lane);
+  if constexpr (XQ >= 2) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kt[ks] = frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane);
+  }
+  const bf16x8 one = ones3(lane);
+  f32x16 dk[2], dv[2], dqs = zero16();
+  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // dQ^T sub-tile (dhw, qhw) of tile T over the block's 128 keys from a dS^T image
+  auto dq_of = [&](int T, const bf16* dsT) __attribute__((always_inline)) {
+    f32x16 dq = zero16();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 sf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) sf[ks] = frag_tr_sw(dsT, 16 * (4 * h + ks), 32 * qhw, lane);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) dq = mfma(kt[4 * h + ks], sf[ks], dq);
+    }
+    if constexpr (XQ >= 3) {
+      const int q = T * 64 + 32 * qhw + (lane & 31);
+      if (q < N) {
+        bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D + 32 * dhw;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 8 * g4 + 4 * (lane >> 5);
+          *reinterpret_cast<bf16x4*>(qrow + d0) =
+              bf16x4{(bf16)(dq[4 * g4] * scale), (bf16)(dq[4 * g4 + 1] * scale), (bf16)(dq[4 * g4 + 2] * scale),
+                     (bf16)(dq[4 * g4 + 3] * scale)};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqs[r] += dq[r];
+    }
+  };
+  auto step = [&](int T, auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    if (T + 1 < nt) {
+      qd.issue(Qb(P ^ 1), (unsigned)(T + 1) * tile_bytes, wave);
+      gd.issue(Gb(P ^ 1), (unsigned)(T + 1) * tile_bytes, wave);
+      fd.issue(Fb(P ^ 1), (unsigned)(T + 1) * 64u, wave, lane);
+    }
+    bf16* const dsT = reinterpret_cast<bf16*>(lds + XL_S + P * 16384);
+    xhalf(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 0, wave, lane);
+    if constexpr (XQ >= 4) {
+      if (T > 0) dq_of(T - 1, reinterpret_cast<const bf16*>(lds + XL_S + (P ^ 1) * 16384));
+    }
+    xhalf(dk, dv, Qb(P), Gb(P), Fb(P), dsT, kf, vf, one, 1, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (XQ >= 2 && XQ < 4) dq_of(T, dsT);
+  };
+  {
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    int T = 0;
+    for (; T + 1 < nt; T += 2) {
+      step(T, P0{});
+      step(T + 1, P1{});
+    }
+    if (T < nt) step(T, P0{});
+  }
+  if constexpr (XQ >= 4) dq_of(nt - 1, reinterpret_cast<const bf16*>(lds + XL_S + ((nt - 1) & 1) * 16384));
+  if (key >= N) return;
+  bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
+  bf16* vrow = krow + H * D;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d0 = 8 * g4 + 4 * (lane >> 5);
+    bf16x4 a0, a1, c0, c1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a0[i] = (bf16)(dk[0][4 * g4 + i] * dk_scale);
+      a1[i] = (bf16)(dk[1][4 * g4 + i] * dk_scale);
+      c0[i] = (bf16)dv[0][4 * g4 + i];
+      c1[i] = (bf16)dv[1][4 * g4 + i];
+    }
+    *reinterpret_cast<bf16x4*>(krow + d0) = a0;
+    *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
+    *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
+    *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
+  }
+  if constexpr (XQ == 2) {  // keep the dQ work alive
+    if (dqs[0] == 1.2345e-30f) dqkv[0] = (bf16)dqs[1];
+  }
+}
+}  // namespace
+
+// same arguments as mia_attn_bwd_onepass (chain / err unused); q_ready must be 1 (Q' saved by the forward)
+extern "C" int mia_attn_bwd_onepass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                                    void* saved, void* chain, uint32_t* err, int32_t B, int32_t N, int32_t H,
+                                    float scale, int32_t q_ready, mia_stream_t stream) {
+  hipStream_t s = as_stream(stream);
+  const int64_t rows = (int64_t)B * N * H;
+  bf16* qs = (bf16*)saved;
+  bf16* frag = qs + rows * D;
+  attn_bwd_prep_kernel<<<(unsigned)cdiv(rows * 8, 256), 256, 0, s>>>((const bf16*)qkv, (const bf16*)out,
+                                                                     (const bf16*)dout, lse, qs, frag, B, N, H,
+                                                                     scale * LOG2E, q_ready ? 0 : 1);
+  const int nkb = (int)cdiv(N, XK);
+  xq_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, N, H,
+                                                    nkb, scale, 1.f / LOG2E);
+  return 0;
+}
