@@ -4,7 +4,8 @@
 // per-tile barrier and the dQ^T MFMAs over the block's keys (summed, one store at the end), 3 = + the
 // per-tile bf16 dQ stores (every key block writes its partial: wrong dQ, timing only), 4 = 3 with the dQ of
 // tile j computed between the two query halves of step j + 1 (from the other dS^T image) instead of after
-// the barrier.
+// the barrier, 5 = the one-pass backward on this structure (dQ of tile j between the halves of step j + 1,
+// the ordered running-sum hand-off; correct dQ).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DXQ=<n> -I dl-sound-classification_amd/csrc \
 //         tools/probe/exp_dkdvq.hip dl-sound-classification_amd/csrc/runtime.hip -o tools/probe/libxq<n>.so
 #include "attn_common.h"
@@ -26,6 +27,36 @@ struct FragDMA2 {
     if (wave < 2) lds_dma16(rsrc, tile + wave * 512, lane * 16, row0 * 16);
   }
 };
+
+
+// ---- ordered dQ hand-off (as in csrc/attn_bwd.hip)
+constexpr int CB_SUB = 4096, CB_TILE = 4 * CB_SUB;
+constexpr unsigned long long CB_SPIN_TICKS = 20000000ull;
+template <int LAG>
+struct CbOrder {
+  int nt, nkb, kb;
+  __device__ __forceinline__ int first() const { return (nt - (LAG * kb) % nt) % nt; }
+  __device__ __forceinline__ int next(int T) const { return T + 1 == nt ? 0 : T + 1; }
+  __device__ __forceinline__ int pos(int T) const {
+    const int z = min(nkb, (nt - T + LAG - 1) / LAG);
+    return kb >= z ? kb - z : nkb - z + kb;
+  }
+};
+__device__ __forceinline__ unsigned cb_load_flag(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, 0, off, 16);
+}
+__device__ __forceinline__ void cb_spin(const unsigned* flag, unsigned want, unsigned* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (fb_ld_flag(flag) == want) return;
+    if (fb_ld_flag(err) != 0u) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > CB_SPIN_TICKS) {
+      fb_st_flag(err, 1u);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 
 __device__ __forceinline__ void xhalf(f32x16 (&dk)[2], f32x16 (&dv)[2], const bf16* Q_, const bf16* G_, const bf16* F_,
                                       bf16* dsT, const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], bf16x8 one, int sq,
@@ -199,6 +230,198 @@ __global__ __launch_bounds__(256, 2) void xq_kernel(const bf16* __restrict__ qkv
     if (dqs[0] == 1.2345e-30f) dqkv[0] = (bf16)dqs[1];
   }
 }
+
+// XQ 5: the one-pass backward on this structure: dQ of tile j between the halves of step j + 1, handed on
+// through the ordered running-sum chain (flag read before the publish store)
+template <int LAG>
+__global__ __launch_bounds__(256, 2) void xc_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                     const bf16* __restrict__ qs, const bf16* __restrict__ frag,
+                                                     bf16* __restrict__ dqkv, float* chain, unsigned* flags,
+                                                     unsigned* err, int N, int H, int nkb, float scale,
+                                                     float dk_scale) {
+  __shared__ __attribute__((aligned(1024))) char lds[XL_BYTES];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int w = xcd_work_item(blockIdx.x, gridDim.x);
+  const int bh = w / nkb, kb = w - bh * nkb, b = bh / H, hd = bh % H;
+  const int nt = (N + 63) / 64;
+  const int64_t ldt = (int64_t)3 * H * D, ldo = (int64_t)H * D;
+  const bf16* base = qkv + (int64_t)b * N * ldt + hd * D;
+  const unsigned tile_bytes = (unsigned)(64 * ldo * 2);
+  bf16* const Kt = reinterpret_cast<bf16*>(lds + XL_S + 16384);
+  {
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(base + H * D), 0, (int)(((int64_t)(N - 1) * ldt + 64) * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = 32 * wave + 8 * i + (lane >> 3);
+      const unsigned vo = (unsigned)(((lane >> 3) * (int)ldt + ((lane & 7) ^ swz(rl)) * 8) * 2);
+      lds_dma16(kr, Kt + (4 * wave + i) * 512, vo, (unsigned)((int64_t)(kb * XK + 32 * wave + 8 * i) * ldt * 2));
+    }
+  }
+  TileDMA qd, gd;
+  FragDMA2 fd;
+  qd.init(qs + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  gd.init(dout + (int64_t)b * N * ldo + hd * D, ldo, N, wave, lane);
+  fd.init(frag + (int64_t)bh * 2 * N * 8, N, wave);
+  auto Qb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_Q + P * 8192); };
+  auto Gb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_G + P * 8192); };
+  auto Fb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_F + P * 2048); };
+  auto Sb = [&](int P) { return reinterpret_cast<bf16*>(lds + XL_S + P * 16384); };
+  const CbOrder<LAG> ord{nt, nkb, kb};
+  int T = ord.first(), Tp = 0, pp = 0;
+  qd.issue(Qb(0), (unsigned)T * tile_bytes, wave);
+  gd.issue(Gb(0), (unsigned)T * tile_bytes, wave);
+  fd.issue(Fb(0), (unsigned)T * 64u, wave, lane);
+  const int key = kb * XK + wave * 32 + (lane & 31);
+  bf16x8 vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) vf[ks] = load_frag_global(base + (int64_t)key * ldt + 2 * H * D, ks, lane, key < N);
+  settle(vf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int dhw = wave & 1, qhw = wave >> 1;
+  bf16x8 kf[4], kt[8];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kf[ks] = frag_row_sw(Kt, 32 * wave + (lane & 31), ks, lane);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kt[ks] = frag_tr_sw(Kt, 16 * ks, 32 * dhw, lane);
+  const bf16x8 one = ones3(lane);
+  f32x16 dk[2], dv[2];
+  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+  unsigned* const fl = flags + (int64_t)bh * nt * 4;
+  const __amdgpu_buffer_rsrc_t flr = __builtin_amdgcn_make_buffer_rsrc((void*)fl, 0, nt * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(chain + (int64_t)bh * nt * (CB_TILE / 4)), 0, nt * CB_TILE, 0x00020000);
+  const int last = nkb - 1;
+  bool pub = false;
+  int pub_T = 0;
+  unsigned pub_val = 0;
+  u32x4 run[4];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave has its K fragments before dS^T image 1 (Kt) is overwritten
+  auto dq_mfma = [&](const bf16* dsT) __attribute__((always_inline)) {
+    f32x16 dq = zero16();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 sf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) sf[ks] = frag_tr_sw(dsT, 16 * (4 * h + ks), 32 * qhw, lane);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) dq = mfma(kt[4 * h + ks], sf[ks], dq);
+    }
+    return dq;
+  };
+  auto link_fetch = [&](unsigned fv) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned fs = __builtin_amdgcn_readfirstlane(fv);
+    asm volatile("; flag read" ::"s"(fs));
+    if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
+    pub = false;
+    if (pp > 0) {
+      if (__builtin_expect(fs != (unsigned)pp, 0)) cb_spin(fl + Tp * 4 + wave, (unsigned)pp, err);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        run[g] = __builtin_amdgcn_raw_buffer_load_b128(cr, lane * 16, Tp * CB_TILE + wave * CB_SUB + g * 1024, 16);
+    }
+  };
+  auto link_store = [&](f32x16 dq) __attribute__((always_inline)) {
+    if (pp > 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 r = __builtin_bit_cast(f32x4, run[g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dq[4 * g + i] += r[i];
+      }
+    }
+    if (pp < last) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]}), cr, lane * 16,
+            Tp * CB_TILE + wave * CB_SUB + g * 1024, 16);
+      pub = true;
+      pub_T = Tp;
+      pub_val = (unsigned)(pp + 1);
+    } else {
+      const int q = Tp * 64 + 32 * qhw + (lane & 31);
+      if (q < N) {
+        bf16* qrow = dqkv + ((int64_t)b * N + q) * ldt + hd * D + 32 * dhw;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 8 * g4 + 4 * (lane >> 5);
+          *reinterpret_cast<bf16x4*>(qrow + d0) =
+              bf16x4{(bf16)(dq[4 * g4] * scale), (bf16)(dq[4 * g4 + 1] * scale), (bf16)(dq[4 * g4 + 2] * scale),
+                     (bf16)(dq[4 * g4 + 3] * scale)};
+        }
+      }
+    }
+  };
+  auto step = [&](int j, auto par, auto has_prev) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    constexpr bool HP = decltype(has_prev)::value;
+    const int pos = ord.pos(T), T1 = ord.next(T);
+    if (j + 1 < nt) {
+      qd.issue(Qb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
+      gd.issue(Gb(P ^ 1), (unsigned)T1 * tile_bytes, wave);
+      fd.issue(Fb(P ^ 1), (unsigned)T1 * 64u, wave, lane);
+    }
+    unsigned fv = 0;
+    if (HP && pp > 0) fv = cb_load_flag(flr, (Tp * 4 + wave) * 4);
+    xhalf(dk, dv, Qb(P), Gb(P), Fb(P), Sb(P), kf, vf, one, 0, wave, lane);
+    if constexpr (HP) link_fetch(fv);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xhalf(dk, dv, Qb(P), Gb(P), Fb(P), Sb(P), kf, vf, one, 1, wave, lane);
+    if constexpr (HP) link_store(dq_mfma(Sb(P ^ 1)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Tp = T;
+    pp = pos;
+    T = T1;
+  };
+  {
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using F = std::false_type;
+    using Tr = std::true_type;
+    step(0, P0{}, F{});
+    int j = 1;
+    for (; j + 1 < nt; j += 2) {
+      step(j, P1{}, Tr{});
+      step(j + 1, P0{}, Tr{});
+    }
+    if (j < nt) step(j, P1{}, Tr{});
+  }
+  {
+    const unsigned fv = pp > 0 ? cb_load_flag(flr, (Tp * 4 + wave) * 4) : 0u;
+    const f32x16 dq = dq_mfma(Sb((nt - 1) & 1));
+    link_fetch(fv);
+    link_store(dq);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (pub && lane == 0) fb_st_flag(fl + pub_T * 4 + wave, pub_val);
+  if (key >= N) return;
+  bf16* krow = dqkv + ((int64_t)b * N + key) * ldt + H * D + hd * D;
+  bf16* vrow = krow + H * D;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d0 = 8 * g4 + 4 * (lane >> 5);
+    bf16x4 a0, a1, c0, c1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a0[i] = (bf16)(dk[0][4 * g4 + i] * dk_scale);
+      a1[i] = (bf16)(dk[1][4 * g4 + i] * dk_scale);
+      c0[i] = (bf16)dv[0][4 * g4 + i];
+      c1[i] = (bf16)dv[1][4 * g4 + i];
+    }
+    *reinterpret_cast<bf16x4*>(krow + d0) = a0;
+    *reinterpret_cast<bf16x4*>(krow + 32 + d0) = a1;
+    *reinterpret_cast<bf16x4*>(vrow + d0) = c0;
+    *reinterpret_cast<bf16x4*>(vrow + 32 + d0) = c1;
+  }
+}
 }  // namespace
 
 // same arguments as mia_attn_bwd_onepass (chain / err unused); q_ready must be 1 (Q' saved by the forward)
@@ -213,7 +436,27 @@ extern "C" int mia_attn_bwd_onepass(const void* qkv, const void* out, const void
                                                                      (const bf16*)dout, lse, qs, frag, B, N, H,
                                                                      scale * LOG2E, q_ready ? 0 : 1);
   const int nkb = (int)cdiv(N, XK);
-  xq_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, N, H,
-                                                    nkb, scale, 1.f / LOG2E);
+  if constexpr (XQ >= 5) {
+    const int nt = (int)cdiv(N, 64);
+    const int64_t fbytes = (((int64_t)B * H * nt * 4 * 4) + 255) / 256 * 256;
+    unsigned* flags = reinterpret_cast<unsigned*>(chain);
+    float* sums = reinterpret_cast<float*>(reinterpret_cast<char*>(chain) + fbytes);
+    hipMemsetAsync(flags, 0, (size_t)fbytes, s);
+    int lag = 1;
+    if (nkb > 1) {
+      for (int L = 3; L >= 2; --L)
+        if (nt - L * (nkb - 1) >= 2) { lag = L; break; }
+    }
+#define XC(L) xc_kernel<L><<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag, \
+                                                                  (bf16*)dqkv, sums, flags, err, N, H, nkb, scale, \
+                                                                  1.f / LOG2E)
+    if (lag == 3) XC(3);
+    else if (lag == 2) XC(2);
+    else XC(1);
+#undef XC
+  } else {
+    xq_kernel<<<(unsigned)(nkb * B * H), 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, qs, frag, (bf16*)dqkv, N,
+                                                      H, nkb, scale, 1.f / LOG2E);
+  }
   return 0;
 }
