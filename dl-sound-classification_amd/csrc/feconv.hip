@@ -84,6 +84,9 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   return (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
 }
 
+#ifdef FE_STAMP
+__device__ unsigned long long g_fe_st[64 * 4 * 256 * 8];
+#endif
 template <int CIN, int KW, int S, bool PRE>
 __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void feconv_kernel(FeArgs g) {
   using Cfg = FeCfg<CIN, KW, S>;
@@ -228,15 +231,36 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   // one item: issue item+2G's loads into `ld`, compute from LDS half `buf`, store the outputs, move
   // item+G's raw window (`st`, loaded one item earlier) into the other half, barrier (LDS only: the
   // global stores stay in flight across it)
+#ifdef FE_STAMP  // timing builds only (tools/fe_stamps.py): s_memtime per item segment
+  unsigned long long ts[8] = {};
+  int kst = 0;
+#define FT(k) ts[k] = __builtin_amdgcn_s_memtime()
+#else
+#define FT(k)
+#endif
   auto step = [&](int item, int buf, u32x4 (&ld)[Cfg::LCH], uint32_t& ldok, const u32x4 (&st)[Cfg::LCH],
                   uint32_t stok) __attribute__((always_inline)) {
+    FT(0);
     load(item + 2 * (int)gridDim.x, ld, ldok);
+    FT(1);
     f32x16 acc[2];
     compute(buf, acc);
+    FT(2);
     epilogue(item, acc);      // global stores issue behind the in-flight loads; nothing waits for them
+    FT(3);
     store(buf ^ 1, st, stok);  // waits only for `st`'s loads (issued an item ago)
+    FT(4);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    FT(5);
     __builtin_amdgcn_s_barrier();
+#ifdef FE_STAMP
+    FT(6);
+    if (blockIdx.x < 64 && kst < 256 && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g_fe_st[(((int)blockIdx.x * 4 + wave) * 256 + kst) * 8 + k] = ts[k];
+    }
+    ++kst;
+#endif
   };
 
   int item = blockIdx.x;
@@ -926,3 +950,9 @@ extern "C" int mia_fe_conv3_fwd(const void* x, const void* w, const float* bias,
   MIA_LAUNCH_CHECK("fe_conv3_fwd");
   return 0;
 }
+
+#ifdef FE_STAMP
+extern "C" int mia_fe_stamps_copy(void* dst, int64_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fe_st), (size_t)bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -488,17 +488,21 @@ int mia_attn_bwd_saved_q(const void* qkv, const void* out, const void* dout, con
 /* The bf16 backward in its two-kernel form (what mia_attn_bwd / mia_attn_bwd_saved_q run), and in a
  * fused one-pass form: per (b, h, 256-key block) S, dP, dS are computed once, dV / dK accumulate in
  * registers and dQ is summed over the key blocks by an ordered hand-off of running f32 sums in `work`
- * (fixed order: bit-reproducible).  q_ready: `work` already holds Q' (mia_attn_fwd_save_q). */
+ * (fixed order: bit-reproducible).  q_ready: `work` already holds Q' (mia_attn_fwd_save_q).
+ * mia_attn_bwd_fused returns 0 even when one of its bounded hand-off waits gave up: the caller MUST read the
+ * u32 error word at byte offset mia_attn_bwd_error_offset(B, N, H) of `work` after the call (nonzero: that
+ * call's dQ is invalid).  No model path calls it; mia_attn_bwd_onepass takes a caller-owned error word. */
 int mia_attn_bwd_two_pass(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                           void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
                           mia_stream_t stream);
 int mia_attn_bwd_fused(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                        void* work, int32_t B, int32_t N, int32_t H, float scale, int32_t q_ready,
                        mia_stream_t stream);
-/* The default bf16 training backward: one pass, no recompute (S, dP, dS once per tile; dV, dK in registers;
- * dQ = dS K summed over the 128-key blocks of each (b, h) by an ordered hand-off of running f32 sums:
+/* The one-pass bf16 training backward: no recompute (S, dP, dS once per tile; dV, dK in registers;
+ * dQ = dS K summed over the 256-key blocks of each (b, h) by an ordered hand-off of running f32 sums:
  * bit-reproducible).  Replaces F.scaled_dot_product_attention's backward inside timm's Attention
- * (reference src/models/ast.py:60-61).
+ * (reference src/models/ast.py:60-61); an alternative to mia_attn_bwd_saved_q, which is faster on MI355X
+ * at the AST shape and is what the model calls.
  * saved: mia_attn_saved_q_bytes (Q' -- already there when q_ready, from mia_attn_fwd_save_q -- and the
  *   row-constant fragments, written here); chain: mia_attn_bwd_chain_bytes of scratch for this call only
  *   (hand-off flags + running sums; both 256-B aligned).

@@ -1,6 +1,6 @@
 #!/bin/bash
 # frontend kernel A/B: tools/bench_fe.py on the product library and tools/probe/libmia_<name>.so builds
-OUT=gpurun_out/feab; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-feab}; mkdir -p $OUT
 for i in 1 2; do
   for v in base "$@"; do
     if [ $v = base ]; then LIBV=; else LIBV=$(realpath tools/probe/libmia_$v.so); fi
