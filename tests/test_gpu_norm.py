@@ -327,7 +327,7 @@ def test_conv3_wgrad(cuda, n, h, wd):
 
 
 @pytest.mark.parametrize("n,h,w,kw,C", [(3, 1, 55102, 64, 64), (2, 1, 300, 64, 64), (2, 1, 70, 7, 64),
-                                        (2, 10, 279, 2, 64), (2, 10, 139, 2, 128)])
+                                        (2, 1, 64 * 130, 64, 64), (2, 10, 279, 2, 64), (2, 10, 139, 2, 128)])
 def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     """One-pass maxpool-on-raw-winners + BN statistics (then relu(bn(winner))) == BN statistics pass +
     maxpool of relu(bn(x)); argmax equal wherever the pooled value is positive (elsewhere the routed
@@ -347,6 +347,11 @@ def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     st1 = K.bn_finalize_shifted(part, nb, n * h * w, C, kshift, gamma, beta, rm1, rv1, 0.1, 1e-5)
     out1 = torch.empty(n, h, ow, C, dtype=torch.bfloat16, device=cuda)
     K.pool_apply(win, n, h, ow, C, st1, out1, 0)
+    if h == 1 and C == 64:  # the transposed trunk image (layout 1, the tiled kernel): the same values, bit for bit
+        out1t = torch.full((n, C, ow), float("nan"), dtype=torch.bfloat16, device=cuda)
+        K.pool_apply(win, n, h, ow, C, st1, out1t, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(out1t, out1[:, 0].permute(0, 2, 1))
     st2 = K.bn_fwd_stats(x, n * h * w, C, gamma, beta, rm2, rv2, 0.1, 1e-5, True)
     out2 = torch.empty(n, h, ow, C, dtype=torch.bfloat16, device=cuda)
     am2 = torch.empty(n, h, ow, C, dtype=torch.uint8, device=cuda)
