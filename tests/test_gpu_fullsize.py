@@ -130,6 +130,47 @@ def test_ast_depth12_bf16_step_b32_vs_autocast_oracle(cuda):
            tol={"logits": 0.045, "loss": 0.006, "gradnorm": 0.018, "sign": 0.97})
 
 
+def test_ast_depth2_bf16_step_b256_vs_autocast_oracle(cuda):
+    """The AST bf16 training step at the benched batch (B = 256: the full attention grid, the GEMM shapes of the
+    bench) with two transformer blocks, against the oracle's autocast-bf16 and f32 steps (torch on the same
+    GPU): logits, loss, clip norm and the Adam update directions, with the depth-2 bounds widened 2x for the
+    larger batch and the self-calibrated bounds of _check."""
+    os.environ["MIA_QUIET"] = "1"
+    from src.miaudio import kernels as K
+    from src.training.optim import FusedAdam
+    B = 256
+    st = oast.deit_hash_state(300, depth=2)
+    hw, hb = oast.head_hash(901, 50)
+    m = _ast(cuda, "bf16", 2, st, hw, hb).train()
+    x = torch.from_numpy(hash_uniform(35, (B, 128, 1379))).to(cuda)
+    y = _labels(cuda, B, 35)
+    pmap = dict(m.named_parameters())
+    before = {n: p.detach().clone() for n, p in pmap.items()}
+    probs = m(x)
+    loss, dp, _ = K.soft_ce(probs.detach().float().contiguous(), y, input_sigmoid=False)
+    probs.backward(dp)
+    opt = FusedAdam(m.parameters(), lr=1e-4, weight_decay=1e-4, clip=1.0)
+    opt.step()
+    total = float(opt.last_total_norm)
+    deltas = {n: p.detach() - before[n] for n, p in pmap.items()}
+    pp, loss = probs.detach().float(), float(loss)
+    _t("ast d2 b256: HIP step done")
+    del probs, dp, m, opt, before, pmap
+    torch.cuda.empty_cache()
+    ref_names = list(oast.model_params(st, hw, hb, depth=2))
+
+    def ref(autocast):
+        p = {k: v.to(cuda).requires_grad_(True) for k, v in oast.model_params(st, hw, hb, depth=2).items()}
+        r = _oracle_step(p, ref_names, lambda q: oast.forward(q, x, depth=2), y, autocast)
+        torch.cuda.empty_cache()
+        _t(f"ast d2 b256: oracle step done (autocast={autocast})")
+        return r
+
+    r16, r32 = ref(True), ref(False)
+    _check("ast-d2-b256", pp, loss, total, deltas, {}, r16, r32,
+           tol={"logits": 0.03, "loss": 0.004, "gradnorm": 0.012, "sign": 0.98})
+
+
 def test_attention_benched_grid_b256_h12(cuda):
     """mia_attn_fwd_save_q / mia_attn_bwd_saved_q (the training form) and the one-pass / fused backwards over
     the whole benched grid (B*H = 3 072 (clip, head) pairs of 1 645 tokens); every pair against float64, with
