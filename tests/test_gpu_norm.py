@@ -193,11 +193,14 @@ def test_fe_conv1_fwd_with_bn_stats(cuda, n, t):
         assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a - b).abs().max()
 
 
-@pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64), (3, 1, 1001, 64, 1, 64), (2, 6, 67, 32, 2, 8)])
+@pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64), (3, 1, 1001, 64, 1, 64), (2, 6, 67, 32, 2, 8),
+                                  (2, 50, 846, 32, 5, 3), (3, 11, 68, 32, 5, 3), (2, 10, 67, 64, 1, 2),
+                                  (2, 5, 33, 256, 2, 4)])
 def test_pool_bn_bwd_apply_octets_bf16(cuda, geom):
-    """bf16 pooled BN backward with kw % 8 == 0 (row-octet kernel: one cell lookup per 8 pixels;
-    ragged rows, pixels past the last whole cell) vs a float64 restatement: dx = BN backward of the
-    max-pool's routed, ReLU-masked gradient."""
+    """bf16 pooled BN backward with kw % 8 == 0 (row-octet kernel: one cell lookup per 8 pixels) and
+    kw = 2..4 (run kernel: one cell lookup per kw-pixel run of a row; the trunk's (5, 3) and (1, 2)
+    pools), with ragged rows and columns (pixels past the last whole cell) vs a float64 restatement:
+    dx = BN backward of the max-pool's routed, ReLU-masked gradient."""
     n, h, w, c, kh, kw = geom
     g = torch.Generator().manual_seed(h * w + c)
     y = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16)
