@@ -61,6 +61,9 @@ __device__ __forceinline__ u32x4 cook(u32x4 u, bool ok, const float* sc, const f
   return u32x4{w4[0], w4[1], w4[2], w4[3]};
 }
 
+#ifndef C8_EDGE
+#define C8_EDGE 1
+#endif
 template <bool PRE, bool STATS, int JU>
 __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv8_kernel(C8Args g) {
   __shared__ __attribute__((aligned(16))) char smem[C8_WB + 4 * C8_STRIP];
@@ -184,8 +187,10 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
 
     // one padded input row r (r % 8 == P): stage it, start the next row's loads, 8 x 32 MFMAs,
     // then retire output row r - 7 (slot (P + 1) % 8)
-    auto step = [&](auto PC, int r) __attribute__((always_inline)) {
+    auto step = [&](auto PC, auto EC, int r) __attribute__((always_inline)) {
       constexpr int P = decltype(PC)::value;
+      constexpr bool EDGE = decltype(EC)::value;  // a row whose kernel rows partly map outside [oy_lo, oy_hi)
+      const int kylo = r - oy_hi + 1, kyhi = r - oy_lo;  // kernel rows with a live output row
       const int iy = r - g.ph;
       const bool live = iy >= 0 && iy < g.h;  // wave-uniform: padding rows contribute nothing
       if (live) {
@@ -215,11 +220,15 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
           const int cur = j & 1;
           fetch((j + 1) & 15, cur ^ 1);  // (the last block re-reads block 0: harmless, keeps the body uniform)
 #pragma unroll
-          for (int ky = 0; ky < 8; ++ky)
+          for (int ky = 0; ky < 8; ++ky) {
+            if constexpr (EDGE) {
+              if (ky < kylo || ky > kyhi) continue;  // wave-uniform: that output row is outside the item
+            }
 #pragma unroll
             for (int tt = 0; tt < 2; ++tt)
               acc[(P - ky + 8) & 7][tt] =
                   __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[cur][ky], fb[cur][tt], acc[(P - ky + 8) & 7][tt], 0, 0, 0);
+          }
 #pragma unroll
           for (int i = 0; i < 10; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -239,7 +248,18 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
 
     load_row(r_lo);
     for (int r0 = r_lo & ~7; r0 < r_hi; r0 += 8) {
-#define C8_STEP(k) if (r0 + k >= r_lo && r0 + k < r_hi) step(std::integral_constant<int, k>{}, r0 + k);
+#if C8_EDGE
+      // rows within 7 of either end of the item run only the kernel rows that land on its output rows
+#define C8_STEP(k)                                                                                   \
+  if (r0 + k >= r_lo && r0 + k < r_hi) {                                                             \
+    if (r0 + k < oy_lo + 7 || r0 + k >= oy_hi)                                                       \
+      step(std::integral_constant<int, k>{}, std::true_type{}, r0 + k);                              \
+    else                                                                                             \
+      step(std::integral_constant<int, k>{}, std::false_type{}, r0 + k);                             \
+  }
+#else
+#define C8_STEP(k) if (r0 + k >= r_lo && r0 + k < r_hi) step(std::integral_constant<int, k>{}, std::false_type{}, r0 + k);
+#endif
       C8_STEP(0) C8_STEP(1) C8_STEP(2) C8_STEP(3) C8_STEP(4) C8_STEP(5) C8_STEP(6) C8_STEP(7)
 #undef C8_STEP
     }
