@@ -485,12 +485,43 @@ def hbm_calibration(dev, gib: int = 2, iters: int = 5):
             "frac_of_spec": round(2 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def add_box_fraction(leg: dict, box_gbs: float):
-    """frac_vs_box beside frac for every HBM-bound figure of a leg."""
+def mfma_calibration(dev, iters: int = 16384, reps: int = 5):
+    """This box's bf16 MFMA rate, measured in this process: every SIMD issuing back-to-back
+    ``v_mfma_f32_16x16x32_bf16`` on pseudo-random operands (``mia_mfma_rate``: 2 waves per SIMD, 4 independent
+    accumulators each), FLOPs over the HIP-event time on the launch stream.  The clock a box holds under an MFMA
+    load differs box to box (whole AST legs moved 3-5 % between boxes with every MFMA kernel moving together),
+    so MFMA-bound figures report ``frac_vs_box`` = achieved / this rate beside ``frac`` = achieved / the
+    2.5 PF spec."""
+    from src.miaudio import lib as L
+    lib, s = L.load(), L.stream_ptr()
+    wps = 2
+    sink = torch.empty(int(lib.mia_mfma_rate_sink_floats(wps)), dtype=torch.float32, device=dev)
+    L.check(lib.mia_mfma_rate(sink.data_ptr(), iters // 8, wps, s), "mfma_rate")  # warm-up (clock ramp)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+        L.check(lib.mia_mfma_rate(sink.data_ptr(), iters, wps, s), "mfma_rate")
+        e1.record(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    flop = sink.numel() / 64 * iters * 16 * 16384  # waves x iters x 16 MFMAs x 2*16*16*32
+    del sink
+    tf = flop / (best * 1e-3) / 1e12
+    return {"kernel": "mfma_rate_kernel (mia_mfma_rate)", "instruction": "v_mfma_f32_16x16x32_bf16",
+            "flop": flop, "ms": round(best, 4), "tflops": round(tf, 1),
+            "frac_of_spec": round(tf / BF16_MFMA_PEAK_TF, 4)}
+
+
+def add_box_fraction(leg: dict, box_gbs: float, box_tf: float = None):
+    """frac_vs_box beside frac for every HBM-bound (copy rate) and MFMA-bound (MFMA rate) figure of a leg."""
     for key in ("roofline", "dominant_kernel"):
         r = leg.get(key)
         if r and r.get("unit") == "GB/s":
             r["frac_vs_box"] = round(r["achieved"] / box_gbs, 4)
+        elif r and r.get("unit") == "TFLOP/s" and box_tf and leg.get("dtype", "bf16").startswith(("bf16", "mxfp8")):
+            r["frac_vs_box"] = round(r["achieved"] / box_tf, 4)
     fp = leg.get("frontend_path")
     if fp:
         fp["frac_vs_box"] = round(fp["achieved_gbs"] / box_gbs, 4)
@@ -514,6 +545,8 @@ def main():
     torch.cuda.set_device(dev)
     calib = hbm_calibration(dev)
     log(f"HBM calibration: {calib['gbs']} GB/s streaming copy on this box")
+    mcal = mfma_calibration(dev)
+    log(f"MFMA calibration: {mcal['tflops']} TFLOP/s bf16 on this box")
     results = {}
     if args.model in ("both", "envnet"):
         log("EnvNet-v2 leg: building")
@@ -561,7 +594,7 @@ def main():
         from src.miaudio import kernels as K
         K.check_attention_errors()  # raises if a timed step's one-pass attention backward gave up a dQ hand-off
     for leg in results.values():
-        add_box_fraction(leg, calib["gbs"])
+        add_box_fraction(leg, calib["gbs"], mcal["tflops"])
     out = results.get("envnet") or results.get("ast") or results["ast_fp8"]
     if "envnet" in results and "ast" in results:
         out = dict(results["envnet"])
@@ -569,6 +602,7 @@ def main():
     if "ast_fp8" in results and out is not results["ast_fp8"]:
         out["ast_fp8"] = results["ast_fp8"]
     out["hbm_calibration"] = calib
+    out["mfma_calibration"] = mcal
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads, why = cpu_threads()
         log(f"CPU baseline threads: {threads} ({why})")

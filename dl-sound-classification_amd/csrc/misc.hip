@@ -772,3 +772,43 @@ extern "C" int mia_stream_copy(const void* src, void* dst, int64_t bytes, mia_st
   MIA_LAUNCH_CHECK("stream_copy");
   return 0;
 }
+
+// Back-to-back bf16 MFMAs (bench.py's same-process MFMA calibration: the v_mfma_f32_16x16x32_bf16 rate this box
+// holds with every SIMD busy on random operands -- the DVFS clock under an MFMA load differs box to box, so an
+// MFMA-bound kernel's TFLOP/s is also read against this rate).  Each wave keeps 4 independent accumulators
+// (the dependent-issue latency hidden), operands are per-lane pseudo-random bf16 (the clock held on zeros is
+// higher), and the accumulators are written out at the end so nothing is dead.
+__global__ __launch_bounds__(256) void mfma_rate_kernel(int iters, uint32_t seed, float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63;
+  uint32_t h = seed ^ (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
+  bf16x8 a, b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h = h * 1664525u + 1013904223u;
+    a[i] = (bf16)((float)(int)(h >> 16 & 0xff) * (1.f / 128.f) - 1.f);
+    b[i] = (bf16)((float)(int)(h >> 24) * (1.f / 128.f) - 1.f);
+  }
+  f32x4 acc[4] = {};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[q], 0, 0, 0);
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+  sink[blockIdx.x * 256 + threadIdx.x] = v + (float)lane * 0.f;
+}
+
+extern "C" int64_t mia_mfma_rate_sink_floats(int32_t waves_per_simd) {
+  return (int64_t)mia::cu_count() * (waves_per_simd > 0 ? waves_per_simd : 1) * 256;
+}
+
+extern "C" int mia_mfma_rate(float* sink, int32_t iters, int32_t waves_per_simd, mia_stream_t stream) {
+  MIA_CHECK_ARG(sink && iters > 0 && waves_per_simd > 0 && waves_per_simd <= 8, "mfma_rate: bad arguments");
+  const unsigned grid = (unsigned)(mia::cu_count() * waves_per_simd);  // 4 waves per block: one per SIMD
+  mfma_rate_kernel<<<grid, 256, 0, as_stream(stream)>>>(iters, 0x9e3779b9u, sink);
+  MIA_LAUNCH_CHECK("mfma_rate");
+  return 0;
+}

@@ -126,6 +126,8 @@ SIGNATURES = {
     "mia_attn_bwd_fused": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),
     "mia_attn_bwd_error_offset": (C.c_int64, [i32, i32, i32]),
     "mia_stream_copy": (C.c_int, [vp, vp, i64, vp]),
+    "mia_mfma_rate_sink_floats": (i64, [i32]),
+    "mia_mfma_rate": (C.c_int, [vp, i32, i32, vp]),
     "mia_tokens_fwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_tokens_bwd": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_ast_patches": (C.c_int, [vp, i32, i32, i32, i32, i32, vp, vp]),

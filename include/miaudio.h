@@ -577,6 +577,14 @@ int mia_spec_augment_mixup(const float* spec, const float* pool, float* out, int
  * this box's HBM actually streams at (`frac_vs_box`). */
 int mia_stream_copy(const void* src, void* dst, int64_t bytes, mia_stream_t stream);
 
+/* Back-to-back bf16 MFMAs on every SIMD (`waves_per_simd` 4-wave blocks per CU, each wave `iters` x 16
+ * v_mfma_f32_16x16x32_bf16 on pseudo-random operands, 4 independent accumulators): bench.py's MFMA
+ * calibration, the rate this box's matrix cores hold under load (FLOPs = cu_count * waves_per_simd * 4 *
+ * iters * 16 * 16384).  `sink` (mia_mfma_rate_sink_floats floats) receives the accumulators.  Not on the
+ * training path. */
+int64_t mia_mfma_rate_sink_floats(int32_t waves_per_simd);
+int mia_mfma_rate(float* sink, int32_t iters, int32_t waves_per_simd, mia_stream_t stream);
+
 const char* mia_last_error_string(void);
 int mia_device_arch(char* buf, int32_t len); /* gcnArchName of the current device */
 
