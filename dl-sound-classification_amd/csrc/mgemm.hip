@@ -403,7 +403,7 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
           }
         }
       }
-      if constexpr (!DG) {
+      {
         if (g.mxq) {  // MX-fp8 copy of the stored bf16 values (the next MX GEMM's A operand)
           const f32x4 w0 = unpack4(make_uint2(o.x, o.y)), w1 = unpack4(make_uint2(o.z, o.w));
           const float v8[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
@@ -776,6 +776,7 @@ template __global__ void mxgemm_kernel<0>(MArgs, MxArgs);
 template __global__ void mxgemm_kernel<1>(MArgs, MxArgs);
 template __global__ void mxgemm_kernel<2>(MArgs, MxArgs);
 template __global__ void mxgemm_kernel<3>(MArgs, MxArgs);
+template __global__ void mxgemm_kernel<7>(MArgs, MxArgs);  // EPI_DMUL: the fp8 backward-data of fc2
 
 // MX quantiser: 8 values per thread, 4 threads per 32-element block (a block never straddles a row:
 // cols % 32 == 0).  OCP MX rule: shared exponent e = floor(log2(amax)) - 8 (e4m3 emax), clamped to
@@ -802,6 +803,32 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const T* __restrict__ x, 
     const int e = mx_exponent_4lanes(v);
     *reinterpret_cast<uint2*>(q + r * ldq + c) = mx_pack8(v, e);
     if ((c & 31) == 0) sc[r * (cols >> 5) + (c >> 5)] = (uint8_t)(e + 127);
+  }
+}
+
+// MX quantiser of a transpose: q[c][r] = x[r][c] with one shared exponent per 32 consecutive r (the
+// backward-data operand W^T of a weight stored W[out][in]: the contraction runs over `out`).  One thread per
+// 32-element block, lanes over c (coalesced 4-B / 2-B column reads), the same OCP rule as mx_quant_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void mx_quant_t_kernel(const T* __restrict__ x, int64_t rows, int64_t cols,
+                                                         int64_t ldx, uint8_t* __restrict__ q, int64_t ldq,
+                                                         uint8_t* __restrict__ sc) {
+  const int64_t nb = rows >> 5;  // blocks per output row
+  const int64_t total = nb * cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t blk = i / cols, c = i - blk * cols;
+    float v[32];
+    float am = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      v[k] = (float)x[(blk * 32 + k) * ldx + c];
+      am = fmaxf(am, fabsf(v[k]));
+    }
+    const int e = mx_exponent(am);
+    uint2* dst = reinterpret_cast<uint2*>(q + c * ldq + blk * 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = mx_pack8(v + 8 * k, e);
+    sc[c * nb + blk] = (uint8_t)(e + 127);
   }
 }
 
@@ -871,9 +898,10 @@ namespace mgemm {
 // Which epilogue kind the kernel would run for E (-1: not this kernel)
 int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
   if (E.accumulate || E.rm_inner || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
-  if (E.mx_q && (!E.mx_scales || E.dtype != MIA_BF16 || E.ldc != N || N % 32 || E.colsum ||
+  if (E.mx_q && (!E.mx_scales || E.dtype != MIA_BF16 || E.ldc != N || N % 32 ||
+                 (E.colsum && E.act != MIA_DACT_MUL) ||
                  !(E.act == MIA_ACT_NONE || E.act == MIA_ACT_GELU || E.act == MIA_ACT_GELU_SAVE ||
-                   E.act == MIA_ACT_GELU_SAVE_D)))
+                   E.act == MIA_ACT_GELU_SAVE_D || E.act == MIA_DACT_MUL)))
     return -1;
   const bool bf = E.dtype == MIA_BF16, f32 = E.dtype == MIA_F32;
   if ((E.ldc & 3) || E.ldc < N || (reinterpret_cast<uintptr_t>(E.ptr) & (bf ? 7 : 15)) != 0) return -1;
@@ -1021,8 +1049,38 @@ extern "C" int mia_mx_quantize(const void* x, int32_t x_dtype, int64_t rows, int
   return 0;
 }
 
+extern "C" int mia_mx_quantize_t(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ldx, void* q,
+                                 int64_t ldq, void* scales, mia_stream_t stream) {
+  MIA_CHECK_ARG(x_dtype == MIA_BF16 || x_dtype == MIA_F32, "mx_quantize_t: input must be bf16 or f32");
+  MIA_CHECK_ARG(rows >= 0 && cols >= 0 && rows % 32 == 0, "mx_quantize_t: rows must be a multiple of 32");
+  MIA_CHECK_ARG(ldx >= cols && ldq >= rows && ldq % 8 == 0, "mx_quantize_t: bad leading dimension");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(q) & 7) == 0, "mx_quantize_t: q must be 8-B aligned");
+  if (rows == 0 || cols == 0) return 0;
+  const int64_t total = (rows / 32) * cols;
+  const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 16384);
+  hipStream_t s = as_stream(stream);
+  if (x_dtype == MIA_BF16)
+    mx_quant_t_kernel<bf16><<<blocks, 256, 0, s>>>(reinterpret_cast<const bf16*>(x), rows, cols, ldx,
+                                                   reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(scales));
+  else
+    mx_quant_t_kernel<float><<<blocks, 256, 0, s>>>(reinterpret_cast<const float*>(x), rows, cols, ldx,
+                                                    reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(scales));
+  MIA_LAUNCH_CHECK("mx_quantize_t");
+  return 0;
+}
+
+extern "C" int64_t mia_gemm_mxfp8_workspace_bytes(int64_t M, int64_t N, int32_t colsum) {
+  return colsum ? cdiv(cdiv(M, MG_BM) * N * 4, 256) * 256 + colsum_part2_bytes((int)N) : 0;
+}
+
 extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales,
                               int64_t ldb, const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, mia_stream_t stream) {
+  return mia_gemm_mxfp8_ex(a, a_scales, lda, b, b_scales, ldb, E, M, N, K, nullptr, stream);
+}
+
+extern "C" int mia_gemm_mxfp8_ex(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales,
+                                 int64_t ldb, const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, void* workspace,
+                                 mia_stream_t stream) {
   MIA_CHECK_ARG(a && b && a_scales && b_scales && E && E->ptr, "gemm_mxfp8: null operand");
   MIA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mxfp8: K must be a positive multiple of 128");
   MIA_CHECK_ARG(lda >= K && ldb >= K && lda % 16 == 0 && ldb % 16 == 0, "gemm_mxfp8: lda / ldb (bytes) must be >= K and 16-B multiples");
@@ -1032,8 +1090,12 @@ extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, 
   MIA_CHECK_ARG(N % 4 == 0 && (E->dtype != MIA_BF16 || N % 8 == 0) && cdiv(M, MG_BM) * cdiv(N, MG_BN) < (1ll << 24),
                 "gemm_mxfp8: N must be a multiple of 4 (of 8 for a bf16 output)");
   const int epi = mgemm::mg_epi_kind(*E, N);
-  MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_GELU_SAVE_D || epi == EPI_ADD_AUX,
-                "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE(_D) / f32 residual (row-major, aligned)");
+  MIA_CHECK_ARG(epi == EPI_PLAIN || epi == EPI_GELU || epi == EPI_GELU_SAVE || epi == EPI_GELU_SAVE_D || epi == EPI_ADD_AUX ||
+                    epi == EPI_DMUL,
+                "gemm_mxfp8: epilogue must be plain / bias / GELU / GELU_SAVE(_D) / f32 residual / x saved gelu' "
+                "(row-major, aligned)");
+  MIA_CHECK_ARG(!E->colsum || (epi == EPI_DMUL && workspace),
+                "gemm_mxfp8: column sums ride the x-gelu' epilogue and need mia_gemm_mxfp8_workspace_bytes");
   MArgs g;
   memset(&g, 0, sizeof(g));
   g.a = reinterpret_cast<const bf16*>(a);
@@ -1047,13 +1109,21 @@ extern "C" int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, 
   MxArgs x{reinterpret_cast<const uint8_t*>(a_scales), reinterpret_cast<const uint8_t*>(b_scales)};
   const unsigned grid = (unsigned)((int64_t)g.nbm * g.nbn);
   hipStream_t s = as_stream(stream);
+  if (E->colsum) g.colsum_part = reinterpret_cast<float*>(workspace);
   switch (epi) {
     case EPI_PLAIN: mxgemm_kernel<EPI_PLAIN><<<grid, MG_NT, 0, s>>>(g, x); break;
     case EPI_GELU: mxgemm_kernel<EPI_GELU><<<grid, MG_NT, 0, s>>>(g, x); break;
     case EPI_GELU_SAVE: mxgemm_kernel<EPI_GELU_SAVE><<<grid, MG_NT, 0, s>>>(g, x); break;
     case EPI_GELU_SAVE_D: mxgemm_kernel<EPI_GELU_SAVE_D><<<grid, MG_NT, 0, s>>>(g, x); break;
+    case EPI_DMUL: mxgemm_kernel<EPI_DMUL><<<grid, MG_NT, 0, s>>>(g, x); break;
     default: mxgemm_kernel<EPI_ADD_AUX><<<grid, MG_NT, 0, s>>>(g, x); break;
   }
   MIA_LAUNCH_CHECK("gemm_mxfp8");
+  if (E->colsum) {
+    double* part2 = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + cdiv((int64_t)g.nbm * N * 4, 256) * 256);
+    colsum_pass1(g.colsum_part, g.nbm, (int)N, N, part2, s);
+    mg_colsum_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, s>>>(part2, (int)N, E->colsum);
+    MIA_LAUNCH_CHECK("gemm_mxfp8 colsum");
+  }
   return 0;
 }

@@ -461,12 +461,16 @@ __device__ __forceinline__ void stv4(void* p, int dt, int64_t rowoff, int lane, 
   }
 }
 
-template <int PER, bool CS>
+// MX (fp8-mixed backward): the bf16 dx2 row is also written as OCP MX-fp8 (q [rows][D], scales [rows][D / 32],
+// of the stored bf16 values, as ln_fwd_vec_kernel<MX>) -- the A operand of the next MX backward-data GEMM.
+template <int PER, bool CS, bool MX = false>
 __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__ dy, int dydt, const void* __restrict__ x,
                                                         int xdt, const float* __restrict__ g,
                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
                                                         void* dx, int dxdt, int accumulate, void* dx2, int dx2dt,
-                                                        float* __restrict__ partial, int64_t rows) {
+                                                        float* __restrict__ partial, int64_t rows,
+                                                        uint8_t* __restrict__ mq = nullptr,
+                                                        uint8_t* __restrict__ ms = nullptr) {
   // CS: also the column sums of the stored dx2 values (the next linear's bias gradient); partial
   // rows are then [blk][3][D] instead of [blk][2][D] (and the LDS plane for them exists only then)
   constexpr int D = 64 * PER;
@@ -508,6 +512,25 @@ __global__ __launch_bounds__(NT) void ln_bwd_vec_kernel(const void* __restrict__
     }
     stv4<PER>(dx, dxdt, row * D, lane, o);
     if (dx2) stv4<PER>(dx2, dx2dt, row * D, lane, o);
+    if constexpr (MX) {  // dx2 is bf16 here: quantise the stored values, a 32-block = 8 lanes
+#pragma unroll
+      for (int q4 = 0; q4 < PER / 4; ++q4) {
+        float w[4], am = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { w[k] = (float)(bf16)o[4 * q4 + k]; am = fmaxf(am, fabsf(w[k])); }
+#pragma unroll
+        for (int m = 1; m < 8; m <<= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+        const int ex = mx_exponent(am);
+        float tq[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tq[k] = __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(w[k], -ex), -448.f, 448.f);
+        const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(tq[0], tq[1], 0, false);
+        const int wd = __builtin_amdgcn_cvt_pk_fp8_f32(tq[2], tq[3], lo, true);
+        const int d0 = 4 * lane + 256 * q4;
+        *reinterpret_cast<uint32_t*>(mq + row * D + d0) = (uint32_t)wd;
+        if ((lane & 7) == 0) ms[row * (D >> 5) + (d0 >> 5)] = (uint8_t)(ex + 127);
+      }
+    }
     if constexpr (CS) {
 #pragma unroll
       for (int i = 0; i < PER; ++i) ac[i] += dx2dt == MIA_BF16 ? (float)(bf16)o[i] : o[i];
@@ -709,7 +732,8 @@ extern "C" int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D) {
 static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, int32_t xdtype, const float* gamma,
                               const float* mean, const float* rstd, void* dx, int32_t dxdtype, int32_t accumulate,
                               void* dx2, int32_t dx2dtype, float* dgamma, float* dbeta, float* dx2_colsum,
-                              void* partial, int64_t rows, int32_t D, mia_stream_t stream) {
+                              void* partial, int64_t rows, int32_t D, mia_stream_t stream, void* mq = nullptr,
+                              void* ms = nullptr) {
   MIA_CHECK_ARG(dy && x && gamma && mean && rstd && dx && partial, "layernorm_bwd: null pointer");
   MIA_CHECK_ARG(!dx2_colsum || dx2, "layernorm_bwd: the column sums are of dx2");
   MIA_CHECK_ARG(D > 0 && D <= 1024, "layernorm_bwd: D must be <= 1024");
@@ -719,7 +743,11 @@ static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, in
                     reinterpret_cast<uintptr_t>(dx2) | reinterpret_cast<uintptr_t>(gamma)) & 15) == 0;
   if (D == 768 && al) {
     nb = (unsigned)cdiv(rows, LN_VEC_ROWS);
-    if (dx2_colsum)
+    if (mq)
+      ln_bwd_vec_kernel<12, true, true><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype,
+                                                          accumulate, dx2, dx2dtype, (float*)partial, rows,
+                                                          (uint8_t*)mq, (uint8_t*)ms);
+    else if (dx2_colsum)
       ln_bwd_vec_kernel<12, true><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
                                                     dx2, dx2dtype, (float*)partial, rows);
     else
@@ -727,6 +755,7 @@ static int layernorm_bwd_impl(const void* dy, int32_t dydtype, const void* x, in
                                                      accumulate, dx2, dx2dtype, (float*)partial, rows);
   } else {
     MIA_CHECK_ARG(dx2 == nullptr, "layernorm_bwd: the bf16 copy needs D == 768 and aligned rows");
+    MIA_CHECK_ARG(mq == nullptr, "layernorm_bwd: the MX copy needs D == 768 and aligned rows");
     nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
     if (D <= 768)
       ln_bwd_kernel<12><<<nb, NT, 0, s>>>(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate,
@@ -750,6 +779,18 @@ extern "C" int mia_layernorm_bwd(const void* dy, int32_t dydtype, const void* x,
                                  int32_t D, mia_stream_t stream) {
   return layernorm_bwd_impl(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate, dx2, dx2dtype, dgamma,
                             dbeta, nullptr, partial, rows, D, stream);
+}
+
+extern "C" int mia_layernorm_bwd_colsum_mx(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
+                                           const float* gamma, const float* mean, const float* rstd, void* dx,
+                                           int32_t dxdtype, int32_t accumulate, void* dx2, float* dgamma,
+                                           float* dbeta, float* dx2_colsum, void* q, void* scales, void* partial,
+                                           int64_t rows, int32_t D, mia_stream_t stream) {
+  MIA_CHECK_ARG(dx2_colsum && dx2 && q && scales && D == 768, "layernorm_bwd_colsum_mx: needs dx2 (bf16), its column "
+                "sums, the MX q / scales and D == 768");
+  MIA_CHECK_ARG((reinterpret_cast<uintptr_t>(q) & 3) == 0, "layernorm_bwd_colsum_mx: q must be 4-B aligned");
+  return layernorm_bwd_impl(dy, dydtype, x, xdtype, gamma, mean, rstd, dx, dxdtype, accumulate, dx2, MIA_BF16, dgamma,
+                            dbeta, dx2_colsum, partial, rows, D, stream, q, scales);
 }
 
 extern "C" int mia_layernorm_bwd_colsum(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,

@@ -699,16 +699,36 @@ def mx_quantize(x: torch.Tensor) -> MXTensor:
     return MXTensor(q, sc)
 
 
+def mx_quantize_t(x: torch.Tensor) -> MXTensor:
+    """OCP MX-fp8 quantisation of the transpose of a row-major [rows][cols] bf16/f32 tensor: q [cols][rows]
+    with one scale per 32 consecutive rows (mia_mx_quantize_t; the backward-data operand W^T of W[out][in])."""
+    if not x.is_cuda:
+        raise RuntimeError("mx_quantize_t runs on the MI355X HIP kernels only (input is on CPU)")
+    x = x.contiguous()
+    rows, cols = x.shape
+    q = torch.empty(cols, rows, dtype=torch.uint8, device=x.device)
+    sc = torch.empty(cols, rows // 32, dtype=torch.uint8, device=x.device)
+    L.check(L.load().mia_mx_quantize_t(x.data_ptr(), L.dtype_code(x), rows, cols, cols, q.data_ptr(), rows,
+                                       sc.data_ptr(), _s()), "mia_mx_quantize_t")
+    return MXTensor(q, sc)
+
+
 def gemm_mxfp8(a: MXTensor, b: MXTensor, E: L.MiaEpilogue, tag: str | None = None):
-    """C = epilogue(A B^T) on MX-fp8 operands A [M][K], B [N][K] (mia_gemm_mxfp8)."""
+    """C = epilogue(A B^T) on MX-fp8 operands A [M][K], B [N][K] (mia_gemm_mxfp8_ex; an epilogue with column
+    sums -- the x-gelu' backward-data one -- gets its partials' workspace here)."""
     M, K = a.q.shape
     N = b.q.shape[0]
+    lib = L.load()
+    ws = None
+    if E.colsum:
+        ws = workspace(lib.mia_gemm_mxfp8_workspace_bytes(M, N, 1), a.q.device, "mxgemm")
     rec = PROBE is not None and tag in PROBE
     if rec:
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    L.check(L.load().mia_gemm_mxfp8(a.q.data_ptr(), a.scales.data_ptr(), a.q.stride(0), b.q.data_ptr(),
-                                    b.scales.data_ptr(), b.q.stride(0), E, M, N, K, _s()), "mia_gemm_mxfp8")
+    L.check(lib.mia_gemm_mxfp8_ex(a.q.data_ptr(), a.scales.data_ptr(), a.q.stride(0), b.q.data_ptr(),
+                                  b.scales.data_ptr(), b.q.stride(0), E, M, N, K, L.ptr(ws), _s()),
+            "mia_gemm_mxfp8")
     if rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()

@@ -67,6 +67,9 @@ SIGNATURES = {
     "mia_gemm_path": (C.c_int, [P(MiaOperand), P(MiaOperand), i64, i64, i64, i32, i32]),
     "mia_mx_quantize": (C.c_int, [vp, i32, i64, i64, i64, vp, i64, vp, vp]),
     "mia_gemm_mxfp8": (C.c_int, [vp, vp, i64, vp, vp, i64, P(MiaEpilogue), i64, i64, i64, vp]),
+    "mia_mx_quantize_t": (C.c_int, [vp, i32, i64, i64, i64, vp, i64, vp, vp]),
+    "mia_gemm_mxfp8_workspace_bytes": (i64, [i64, i64, i32]),
+    "mia_gemm_mxfp8_ex": (C.c_int, [vp, vp, i64, vp, vp, i64, P(MiaEpilogue), i64, i64, i64, vp, vp]),
     "mia_layernorm_fwd_mx": (C.c_int, [vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mia_attn_fwd_mx": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_splitk_reduce": (C.c_int, [vp, i32, i64, i64, P(MiaEpilogue), vp]),
@@ -114,6 +117,7 @@ SIGNATURES = {
     "mia_layernorm_partial_bytes": (i64, [i64, i32]),
     "mia_layernorm_bwd_colsum": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp, vp, vp, i64,
                                            i32, vp]),
+    "mia_layernorm_bwd_colsum_mx": (C.c_int, [vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "mia_attn_fwd": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
     "mia_attn_bwd_workspace_bytes": (C.c_int64, [i32, i32, i32, i32]),

@@ -12,6 +12,8 @@ on the LDS-DMA dense kernel (mia_gemm path 5).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..miaudio import kernels as K
@@ -37,15 +39,25 @@ def _ln(x, g, b, out_dtype, rows, D, mx: bool = False):
     return y, mean, rstd, None
 
 
-def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool, dx2=None):
+def _ln_bwd(dy, x, g, mean, rstd, dx, rows, D, accumulate: bool, dx2=None, dx2_mx=None):
     """LayerNorm backward into dx (optionally accumulating); dx2 receives a second copy of the result
     (the bf16 operand of the next linear backward).  Returns (dgamma, dbeta, colsum(dx2) or None): with
     dx2 the column sums of its stored values -- the next linear's bias gradient -- come from the same
-    pass (mia_layernorm_bwd_colsum)."""
+    pass (mia_layernorm_bwd_colsum).  dx2_mx (fp8-mixed): an MXTensor receiving the MX-fp8 copy of the
+    stored bf16 dx2 (mia_layernorm_bwd_colsum_mx), the next MX backward-data GEMM's A operand."""
     dg = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty(D, dtype=torch.float32, device=x.device)
     lib = L.load()
     ws = K.workspace(lib.mia_layernorm_partial_bytes(rows, D), x.device, "ln")
+    if dx2_mx is not None:
+        cs = torch.empty(D, dtype=torch.float32, device=x.device)
+        L.check(lib.mia_layernorm_bwd_colsum_mx(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x),
+                                                g.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                                L.dtype_code(dx), int(accumulate), dx2.data_ptr(), dg.data_ptr(),
+                                                db.data_ptr(), cs.data_ptr(), dx2_mx.q.data_ptr(),
+                                                dx2_mx.scales.data_ptr(), ws.data_ptr(), rows, D, L.stream_ptr()),
+                "mia_layernorm_bwd_colsum_mx")
+        return dg, db, cs
     if dx2 is not None and D == 768:
         cs = torch.empty(D, dtype=torch.float32, device=x.device)
         L.check(lib.mia_layernorm_bwd_colsum(dy.data_ptr(), L.dtype_code(dy), x.data_ptr(), L.dtype_code(x),
@@ -75,13 +87,18 @@ ATTN_SAVE_Q = True  # bf16 training: the attention forward writes Q' for the bac
 # (B 256, N 1645, H 12; tools/bench_attn_bwd.py, gpurun_out r5i): two-pass 7.3 ms, one-pass 8.1-8.2 ms per
 # layer, so the two-pass form is the default; tools and tests flip this for A/B runs
 ATTN_ONEPASS = False
+# fp8-mixed: the backward-data GEMMs that run on MX-fp8 operands (dy quantised per call, W^T from the f32 master);
+# the weight gradients stay bf16.  MIA_MX_DGRAD="" keeps every backward GEMM in bf16 (A/B switch).
+MX_DGRAD = frozenset(t for t in os.environ.get("MIA_MX_DGRAD", "fc2,fc1,proj").split(",") if t)
 
 
 def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.PRE_NONE, tag="", db=None,
-                dx_colsum=None):
+                dx_colsum=None, wt_mx=None, dy_mx=None, dx_mx=None):
     """dW = dy^T x (f32), db = colsum(dy) (unless the producer of dy already summed it), dx = dy @ W
     (optionally with an activation backward; dx_colsum receives dx's column sums, the next linear's
-    bias gradient)."""
+    bias gradient).  wt_mx (fp8-mixed): the MX copy of W^T -- the backward-data GEMM then runs on MX-fp8
+    operands: dy_mx, the MX copy of dy its producer wrote (quantised here when None); dx_mx receives the MX
+    copy of the stored dx (the next MX backward-data GEMM's A operand).  The weight gradient stays bf16."""
     Nf, Kf = W.shape
     if cd == L.BF16 and dy.dtype == torch.float32:
         dy = K.cast(dy, torch.bfloat16)  # bf16 GEMM operands (f32 accumulation inside)
@@ -91,7 +108,11 @@ def _linear_bwd(dy, x, W, M, cd, dx_out=None, dact=None, dact_aux=None, x_pre=L.
         db = a_cs = torch.empty(Nf, dtype=torch.float32, device=dy.device)
     K.gemm(K.dense(dy, L.RC, M, Nf), K.dense(x, L.RC, M, Kf, pre=x_pre), K.epilogue(dW, Kf, a_colsum=a_cs),
            Nf, Kf, M, cd, tag=tag + ".wgrad")
-    if dx_out is not None:
+    if dx_out is not None and wt_mx is not None:
+        K.gemm_mxfp8(dy_mx if dy_mx is not None else K.mx_quantize(dy), wt_mx,
+                     K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf,
+                                colsum=dx_colsum, mx=dx_mx), tag=tag + ".dgrad")
+    elif dx_out is not None:
         K.gemm(K.dense(dy, L.KC, M, Nf), K.dense(W, L.RC, Nf, Kf),
                K.epilogue(dx_out, Kf, act=dact if dact is not None else L.ACT_NONE, aux=dact_aux, ldaux=Kf,
                           colsum=dx_colsum),
@@ -206,7 +227,7 @@ class ASTFunction(torch.autograd.Function):
         z = torch.empty(B, wh.shape[0], dtype=torch.float32, device=dev)
         _linear(hc, wh, bh, z, B, cd, tag="head.fwd")
         probs = torch.sigmoid(z)
-        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, spec=spec if pmat is None else None, pmat=pmat, gh=gh, gw=gw, blocks=saved_blocks, xc=xc, wcast=wcast,
+        ctx.s = dict(B=B, N=N, Np=Np, D=D, H=Hh, cd=cd, mx=mx, spec=spec if pmat is None else None, pmat=pmat, gh=gh, gw=gw, blocks=saved_blocks, xc=xc, wcast=wcast,
                      mc=mc, rc=rc, hc=hc, probs=probs, scale=scale)
         ctx.model = model
         ctx.params = params
@@ -249,24 +270,39 @@ class ASTFunction(torch.autograd.Function):
             dxb = dx
         dxb2 = torch.empty_like(dxb) if cd == L.BF16 else None
         db_next = None  # column sums of dxb from the LayerNorm backward that wrote it (bf16 mode)
+        # fp8-mixed: MX copies of dxb written by the LayerNorm backwards (the first one quantised here)
+        use_mx = s["mx"] and ("fc2" in MX_DGRAD or "proj" in MX_DGRAD)
+        dxb_mx = K.mx_quantize(dxb) if use_mx and "fc2" in MX_DGRAD else None
+        dxb2_mx = K.mx_empty(Tt, D, dev) if use_mx else None
         for i in reversed(range(nb)):
             sb = s["blocks"][i]
             g1, b1, wqkv, bqkv, wproj, bproj, g2, b2, w1, bb1, w2, bb2 = p[4 + 12 * i: 16 + 12 * i]
+            wt = {}
+            if s["mx"]:  # MX copies of W^T for the fp8 backward-data GEMMs, from the f32 masters
+                wt = {t: K.mx_quantize_t(w) for t, w in (("qkv", wqkv), ("proj", wproj), ("fc1", w1), ("fc2", w2))
+                      if t in MX_DGRAD}
             wqkv, wproj, w1, w2 = s["wcast"][i]
             # fc2 (input gelu(u)) and fc1 with gelu' fused into the dgrad epilogue
             du = torch.empty(Tt, w1.shape[0], dtype=tdt, device=dev)
+            du_mx = K.mx_empty(Tt, w1.shape[0], dev) if "fc2" in wt and "fc1" in wt else None
             db1_ = torch.empty(w1.shape[0], dtype=torch.float32, device=dev)  # fc1 bias grad = colsum(du)
             dW2, db2_ = _linear_bwd(dxb, sb["gu"], w2, Tt, cd, dx_out=du, dact=L.DACT_MUL, dact_aux=sb["gd"],
-                                    tag="fc2", db=db_next, dx_colsum=db1_)
+                                    tag="fc2", db=db_next, dx_colsum=db1_, wt_mx=wt.get("fc2"), dy_mx=dxb_mx,
+                                    dx_mx=du_mx)
             dh2 = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1", db=db1_)
-            dg2, dbt2, db_proj = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2)  # d(xm)
+            dW1, db1_ = _linear_bwd(du, sb["h2"], w1, Tt, cd, dx_out=dh2, tag="fc1", db=db1_, wt_mx=wt.get("fc1"),
+                                    dy_mx=du_mx)
+            del du_mx
+            dg2, dbt2, db_proj = _ln_bwd(dh2, sb["xm"], g2, sb["m2"], sb["r2"], dx, Tt, D, True, dx2=dxb2,
+                                         dx2_mx=dxb2_mx)  # d(xm)
             if dxb2 is not None:
                 dxb, dxb2 = dxb2, dxb
+                dxb_mx, dxb2_mx = dxb2_mx, dxb_mx
             else:
                 dxb = dx
             da = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj", db=db_proj)
+            dWp, dbp = _linear_bwd(dxb, sb["a"], wproj, Tt, cd, dx_out=da, tag="proj", db=db_proj, wt_mx=wt.get("proj"),
+                                   dy_mx=dxb_mx)
             dqkv = torch.empty(Tt, 3 * D, dtype=tdt, device=dev)
             work = sb["attn_work"]
             with K.probe("attn.bwd", 8.0 * B * Hh * N * N * (D // Hh),  # 2x fwd, recompute not credited
@@ -289,10 +325,14 @@ class ASTFunction(torch.autograd.Function):
                                                   sb["lse"].data_ptr(), dqkv.data_ptr(), work.data_ptr(), cd, B, N, Hh,
                                                   s["scale"], L.stream_ptr()), "mia_attn_bwd")
             dh = torch.empty(Tt, D, dtype=tdt, device=dev)
-            dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv")
-            dg1, dbt1, db_next = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2)  # d(block in)
+            dWq, dbq = _linear_bwd(dqkv, sb["h"], wqkv, Tt, cd, dx_out=dh, tag="qkv", wt_mx=wt.get("qkv"))
+            if use_mx and dxb2_mx is None:
+                dxb2_mx = K.mx_empty(Tt, D, dev)
+            dg1, dbt1, db_next = _ln_bwd(dh, sb["x"], g1, sb["m1"], sb["r1"], dx, Tt, D, True, dx2=dxb2,
+                                         dx2_mx=dxb2_mx)  # d(block in)
             if dxb2 is not None:
                 dxb, dxb2 = dxb2, dxb
+                dxb_mx, dxb2_mx = dxb2_mx, dxb_mx
             else:
                 dxb = dx
             grads[4 + 12 * i: 16 + 12 * i] = [dg1, dbt1, dWq, dbq, dWp, dbp, dg2, dbt2, dW1, db1_, dW2, db2_]

@@ -122,6 +122,19 @@ int mia_mx_quantize(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, 
                     void* scales, mia_stream_t stream);
 int mia_gemm_mxfp8(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales, int64_t ldb,
                    const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, mia_stream_t stream);
+/* The fp8-mixed backward-data GEMMs (dX = dY W on MX operands; round 5):
+ * mia_mx_quantize_t: the MX copy of a transpose, q [cols][rows] = x [rows][cols]^T with one scale per 32
+ * consecutive rows (rows % 32 == 0; q row stride ldq bytes, scales [cols][rows / 32]) -- the B operand W^T
+ * of a weight stored W[out][in], quantised from the f32 master each step like the forward's W.
+ * mia_gemm_mxfp8_ex: mia_gemm_mxfp8 that also takes the fc2 backward-data epilogue (MIA_DACT_MUL: x the
+ * saved gelu'(u), with the column sums of the stored values into E->colsum -- fc1's bias gradient), whose
+ * partials need `workspace` of mia_gemm_mxfp8_workspace_bytes(M, N, colsum != 0) bytes (0 without). */
+int mia_mx_quantize_t(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ldx, void* q, int64_t ldq,
+                      void* scales, mia_stream_t stream);
+int64_t mia_gemm_mxfp8_workspace_bytes(int64_t M, int64_t N, int32_t colsum);
+int mia_gemm_mxfp8_ex(const void* a, const void* a_scales, int64_t lda, const void* b, const void* b_scales,
+                      int64_t ldb, const MiaEpilogue* E, int64_t M, int64_t N, int64_t K, void* workspace,
+                      mia_stream_t stream);
 /* Quantise-on-store producers of the fp8-mixed AST forward (the MX GEMMs' A operands without a
  * separate pass; both also write their usual bf16 output, which the backward keeps using):
  * mia_layernorm_fwd_mx: mia_layernorm_fwd with a bf16 y plus q [rows][D] e4m3 and scales [rows][D/32]
@@ -456,6 +469,14 @@ int mia_layernorm_bwd_colsum(const void* dy, int32_t dydtype, const void* x, int
                              int32_t dxdtype, int32_t accumulate, void* dx2, int32_t dx2dtype, float* dgamma,
                              float* dbeta, float* dx2_colsum, void* partial, int64_t rows, int32_t D,
                              mia_stream_t stream);
+/* As mia_layernorm_bwd_colsum with a bf16 dx2, also writing the OCP MX-fp8 copy of the stored dx2 values
+ * (q [rows][D] e4m3 bytes, 4-B aligned; scales [rows][D / 32], mia_mx_quantize's format): the A operand of
+ * the fp8-mixed backward-data GEMMs of proj / fc2 (mia_gemm_mxfp8_ex) without a quantisation pass. */
+int mia_layernorm_bwd_colsum_mx(const void* dy, int32_t dydtype, const void* x, int32_t xdtype,
+                                const float* gamma, const float* mean, const float* rstd, void* dx,
+                                int32_t dxdtype, int32_t accumulate, void* dx2, float* dgamma, float* dbeta,
+                                float* dx2_colsum, void* q, void* scales, void* partial, int64_t rows, int32_t D,
+                                mia_stream_t stream);
 int64_t mia_layernorm_partial_bytes(int64_t rows, int32_t D);
 
 /* Fused multi-head attention (timm Attention with F.scaled_dot_product_attention,

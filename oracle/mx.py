@@ -48,11 +48,25 @@ def gemm(qa, sa, qb, sb) -> torch.Tensor:
     return dequantize(qa, sa) @ dequantize(qb, sb).T
 
 
+# the block linears whose backward-data GEMM runs on MX-fp8 operands in the HIP path (src/models/ast_hip.py
+# MX_DGRAD): dx = MX(dy) MX(W^T)^T, W^T quantised in blocks of 32 along the output features; the qkv
+# backward-data and every weight gradient stay bf16
+MX_DGRAD = ("proj", "fc1", "fc2")
+
+
+def block_linear_kind(w: torch.Tensor) -> str:
+    """Which ViT block linear a weight [out][in] is, from its shape (D = embedding width)."""
+    o, i = w.shape
+    return {(3 * i): "qkv", i: "proj", (4 * i): "fc1"}.get(o, "fc2" if i == 4 * o else "?")
+
+
 class MXLinear(torch.autograd.Function):
     """Emulation of an fp8-mixed block linear (TEST INFRASTRUCTURE): forward on the MX-fp8 values of the
     bf16-rounded activation (what autocast hands a Linear) and of the f32 weight, bf16 output as autocast's;
-    backward straight through in bf16 (the activations / weights the backward sees are the unquantised
-    ones, as in the HIP path, which keeps the bf16 tensors for its backward GEMMs)."""
+    backward: the weight gradient straight through in bf16 (the activations the backward sees are the
+    unquantised ones, as in the HIP path, which keeps the bf16 tensors for its backward GEMMs), the
+    backward-data product on MX-fp8 operands for the MX_DGRAD linears (MX of the bf16 dy and of W^T, as
+    mia_mx_quantize / mia_mx_quantize_t), bf16 otherwise."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -69,7 +83,12 @@ class MXLinear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         g = gy.to(torch.bfloat16).float().reshape(-1, gy.shape[-1])
         xb = x.to(torch.bfloat16).float().reshape(-1, x.shape[-1])
-        gx = (g @ w.to(torch.bfloat16).float()).to(x.dtype).reshape(x.shape)
+        if block_linear_kind(w) in MX_DGRAD:
+            gq = dequantize(*quantize(g.cpu()))
+            wtq = dequantize(*quantize(w.detach().float().t().contiguous().cpu()))
+            gx = (gq @ wtq.T).float().to(torch.bfloat16).to(g.device).to(x.dtype).reshape(x.shape)
+        else:
+            gx = (g @ w.to(torch.bfloat16).float()).to(x.dtype).reshape(x.shape)
         return gx, (g.T @ xb).to(w.dtype), g.sum(0).to(w.dtype)
 
 

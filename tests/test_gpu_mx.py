@@ -102,6 +102,52 @@ def test_gemm_mxfp8_vs_float64(cuda, M, N, Kd, epi):
     assert err <= tol, f"{epi} {M}x{N}x{Kd}: rel err {err:.3e} > {tol:.1e}"
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,cols", [(32, 3), (768, 77), (3072, 768), (96, 1000)])
+def test_mx_quantize_t_is_quantize_of_the_transpose(cuda, dtype, rows, cols):
+    """mia_mx_quantize_t (the fp8 backward-data operand W^T) byte for byte = the oracle's quantisation of x^T."""
+    g = torch.Generator().manual_seed(rows * 7 + cols)
+    x = _blocky(cols, rows, g, dtype).t().contiguous()  # blocks of 32 along the rows of x = rows of x^T
+    mxt = K.mx_quantize_t(x.to(cuda))
+    torch.cuda.synchronize()
+    q_ref, s_ref = omx.quantize(x.t().contiguous())
+    assert torch.equal(mxt.scales.cpu(), s_ref)
+    assert torch.equal(mxt.q.cpu(), q_ref)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1000, 3072, 768), (513, 768, 3072), (300, 768, 768)])
+def test_gemm_mxfp8_dact_mul_colsum_vs_float64(cuda, M, N, Kd):
+    """The fp8 backward-data of fc2 (x the saved gelu'(u), column sums of the stored bf16 values = fc1's bias
+    gradient) on mia_gemm_mxfp8_ex against the float64 product of the dequantised operands."""
+    g = torch.Generator().manual_seed(M * 5 + N + Kd)
+    qa, sa, qb, sb = _mx_pair(M, N, Kd, g)
+    ref = omx.gemm(qa, sa, qb, sb)
+    d = (torch.rand(M, N, generator=g) * 1.2 - 0.1).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    cs = torch.empty(N, device=cuda)
+    K.gemm_mxfp8(K.MXTensor(*_to(cuda, qa, sa)), K.MXTensor(*_to(cuda, qb, sb)),
+                 K.epilogue(out, N, act=L.DACT_MUL, aux=d.to(cuda), ldaux=N, colsum=cs))
+    torch.cuda.synchronize()
+    want = ref * d.double()
+    got = out.cpu().double()
+    err = float((got - want).abs().max() / want.abs().max())
+    # two bf16 roundings: the product is rounded into the epilogue's bf16 image before the multiply (as in
+    # the bf16 kernel), the result again on store
+    assert err <= 2.0 ** -7, f"{M}x{N}x{Kd}: rel err {err:.3e}"
+    # the column sums are of the stored (rounded) values, in a fixed order
+    cerr = float((cs.cpu().double() - got.sum(0)).abs().max() / got.abs().sum(0).max())
+    assert cerr <= 1e-5, f"colsum rel err {cerr:.3e}"
+
+
+def test_gemm_mxfp8_colsum_needs_the_dact_mul_epilogue(cuda):
+    a = K.MXTensor(torch.zeros(256, 128, dtype=torch.uint8, device=cuda), torch.zeros(256, 4, dtype=torch.uint8,
+                                                                                       device=cuda))
+    out = torch.empty(256, 256, dtype=torch.bfloat16, device=cuda)
+    cs = torch.empty(256, device=cuda)
+    with pytest.raises(RuntimeError, match="gemm_mxfp8"):
+        K.gemm_mxfp8(a, a, K.epilogue(out, 256, colsum=cs))
+
+
 def test_gemm_mxfp8_rejects_bad_shapes(cuda):
     a = K.MXTensor(torch.zeros(256, 96, dtype=torch.uint8, device=cuda), torch.zeros(256, 3, dtype=torch.uint8,
                                                                                       device=cuda))
@@ -170,3 +216,60 @@ def test_gelu_save_epilogue_mx_copy(cuda, mode):
     ref = K.mx_quantize(gu)
     torch.cuda.synchronize()
     assert torch.equal(q.scales, ref.scales) and torch.equal(q.q, ref.q)
+
+
+@pytest.mark.parametrize("rows", [5, 300])
+def test_layernorm_bwd_mx_equals_quantised_bf16_dx2(cuda, rows):
+    """mia_layernorm_bwd_colsum_mx (fp8-mixed backward): dx, dx2, dgamma, dbeta and the column sums equal
+    mia_layernorm_bwd_colsum's, and the MX copy equals mia_mx_quantize(dx2) byte for byte (the proj / fc2
+    backward-data A operand)."""
+    from src.models.ast_hip import _ln_bwd
+    D = 768
+    g = torch.Generator().manual_seed(rows + 11)
+    x = (torch.randn(rows, D, generator=g) * 3 + 1).to(cuda)
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-6)
+    w = (1 + 0.1 * torch.randn(D, generator=g)).to(cuda)
+    dy = torch.randn(rows, D, generator=g).to(torch.bfloat16).to(cuda)
+    base = torch.randn(rows, D, generator=g).to(cuda)
+    out = []
+    for mx in (False, True):
+        dx = base.clone()
+        dx2 = torch.empty(rows, D, dtype=torch.bfloat16, device=cuda)
+        q = K.mx_empty(rows, D, cuda) if mx else None
+        out.append((dx, dx2, q, *_ln_bwd(dy, x, w, mean, rstd, dx, rows, D, True, dx2=dx2, dx2_mx=q)))
+    ref = K.mx_quantize(out[0][1])
+    torch.cuda.synchronize()
+    for a, b in zip(out[0][:2] + out[0][3:], out[1][:2] + out[1][3:]):
+        assert torch.equal(a, b)
+    q = out[1][2]
+    assert torch.equal(q.scales, ref.scales) and torch.equal(q.q, ref.q)
+
+
+@pytest.mark.parametrize("mode", ["bf16_gemm", "mx_gemm"])
+def test_dact_mul_epilogue_mx_copy(cuda, mode):
+    """The fc2 backward-data epilogue (x saved gelu'(u), column sums) with an MX copy of its stored bf16
+    output (fc1's fp8 backward-data A operand): the copy equals mia_mx_quantize of the stored values, and
+    the bf16 output and column sums are unchanged by asking for it."""
+    M, N, Kd = 700, 3072, 768
+    g = torch.Generator().manual_seed(5)
+    d = (torch.rand(M, N, generator=g) * 1.2 - 0.1).to(torch.bfloat16).to(cuda)
+    res = []
+    for with_mx in (False, True):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        cs = torch.empty(N, device=cuda)
+        q = K.mx_empty(M, N, cuda) if with_mx else None
+        E = K.epilogue(out, N, act=L.DACT_MUL, aux=d, ldaux=N, colsum=cs, mx=q)
+        if mode == "mx_gemm":
+            qa, sa, qb, sb = _mx_pair(M, N, Kd, torch.Generator().manual_seed(9))
+            K.gemm_mxfp8(K.MXTensor(*_to(cuda, qa, sa)), K.MXTensor(*_to(cuda, qb, sb)), E)
+        else:
+            gg = torch.Generator().manual_seed(9)
+            a = torch.randn(M, Kd, generator=gg).to(torch.bfloat16).to(cuda)
+            b = (torch.randn(Kd, N, generator=gg) * 0.05).to(torch.bfloat16).to(cuda)
+            K.gemm(K.dense(a, L.KC, M, Kd), K.dense(b, L.RC, Kd, N), E, M, N, Kd, L.BF16)
+        res.append((out, cs, q))
+    ref = K.mx_quantize(res[1][0])
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[1][2].scales, ref.scales) and torch.equal(res[1][2].q, ref.q)
