@@ -272,7 +272,16 @@ class ASTFunction(torch.autograd.Function):
         db_next = None  # column sums of dxb from the LayerNorm backward that wrote it (bf16 mode)
         # fp8-mixed: MX copies of dxb written by the LayerNorm backwards (the first one quantised here)
         use_mx = s["mx"] and ("fc2" in MX_DGRAD or "proj" in MX_DGRAD)
-        dxb_mx = K.mx_quantize(dxb) if use_mx and "fc2" in MX_DGRAD else None
+        dxb_mx = None
+        if use_mx and "fc2" in MX_DGRAD:
+            # = mx_quantize(dxb) byte for byte: all-zero blocks are zero bytes with scale byte 0, and only the
+            # cls rows of dxb are non-zero
+            dxb_mx = K.mx_empty(Tt, D, dev)
+            dxb_mx.q.zero_()
+            dxb_mx.scales.zero_()
+            cq = K.mx_quantize(dxb.view(B, N, D)[:, 0])
+            dxb_mx.q.view(B, N, D)[:, 0] = cq.q
+            dxb_mx.scales.view(B, N, D // 32)[:, 0] = cq.scales
         dxb2_mx = K.mx_empty(Tt, D, dev) if use_mx else None
         for i in reversed(range(nb)):
             sb = s["blocks"][i]

@@ -273,3 +273,4 @@ def test_dact_mul_epilogue_mx_copy(cuda, mode):
     torch.cuda.synchronize()
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     assert torch.equal(res[1][2].scales, ref.scales) and torch.equal(res[1][2].q, ref.q)
+
