@@ -1,7 +1,8 @@
 """Time mia_gemm on the AST linear shapes with the epilogues the AST step uses (one process).
-    TOKENS=310784 python tools/bench_gemm.py [name[:epilogue] ...]
+    TOKENS=310784 python tools/bench_gemm.py [name[@mx][:epilogue[+mxq]] ...]
 (an explicit epilogue overrides the shape's own: plain, bias, gelu, gelu_save, gelu_save_d, dgelu, dmul, dmul_nocs,
-residual, f32 -- the epilogue ablations of one shape)
+residual, f32 -- the epilogue ablations of one shape; "+mxq" adds the epilogue's MX-fp8 copy of the bf16 output;
+"@mx" runs the shape on MX-fp8 operands (mia_gemm_mxfp8_ex), as fp8-mixed does)
 Prints ms and TFLOP/s per shape (random bf16 operands; HIP events on the launch stream)."""
 import os
 import sys
@@ -34,8 +35,10 @@ def main():
     table = {s[0]: s for s in SHAPES}
     for w in want:
         name, _, over = w.partition(":")
+        name, _, prec = name.partition("@")
         _, M, N, Kd, la, lb, epi = table[name]
         epi = over or epi
+        epi, _, mxq = epi.partition("+")
         a = (torch.randn(M, Kd, generator=g, device=dev) if la == L.KC else torch.randn(Kd, M, generator=g, device=dev))
         a = a.to(torch.bfloat16)
         b = (torch.randn(N, Kd, generator=g, device=dev) if lb == L.KC else torch.randn(Kd, N, generator=g, device=dev))
@@ -69,19 +72,30 @@ def main():
         else:
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             E = K.epilogue(out, N, bias=bias if epi == "bias" else None)
-        path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1)
+        if mxq:
+            q = K.mx_empty(M, N, dev)
+            E.mx_q, E.mx_scales = q.q.data_ptr(), q.scales.data_ptr()
+            E._keep = E._keep + (q,)
+        if prec == "mx":
+            qa = K.mx_quantize(a) if la == L.KC else K.mx_quantize_t(a)
+            qb = K.mx_quantize(b) if lb == L.KC else K.mx_quantize_t(b)
+            path = "mx"
+            run = lambda: K.gemm_mxfp8(qa, qb, E)  # noqa: E731
+        else:
+            path = L.load().mia_gemm_path(A, Bo, M, N, Kd, L.BF16, 1)
+            run = lambda: K.gemm(A, Bo, E, M, N, Kd, L.BF16)  # noqa: E731
         for _ in range(2):
-            K.gemm(A, Bo, E, M, N, Kd, L.BF16)
+            run()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(REPS):
-            K.gemm(A, Bo, E, M, N, Kd, L.BF16)
+            run()
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / REPS
         total += ms
-        print(f"path {path} {name:11s} {epi:11s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
+        print(f"path {path} {name:11s} {epi + ('+mxq' if mxq else ''):15s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
               f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
         del a, b, A, Bo, E, out
         torch.cuda.empty_cache()
