@@ -153,12 +153,21 @@ __device__ __forceinline__ uint2 mx_pack8(const float* v, int e) {
 }
 // 8 consecutive values held by each of 4 adjacent lanes (lane & 3 = quarter of the block): the block's
 // exponent from the 4 lanes' amax (every lane of the wave must execute this)
+// (the exchanges are DPP quad permutations -- lane ^ 1, lane ^ 2 inside each group of 4 -- VALU moves instead
+// of the two LDS-crossbar ds_bpermute round trips __shfl_xor compiles to)
 __device__ __forceinline__ int mx_exponent_4lanes(const float* v) {
   float am = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) am = fmaxf(am, fabsf(v[k]));
+  constexpr int XOR1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);  // quad_perm [1, 0, 3, 2]
+  constexpr int XOR2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // quad_perm [2, 3, 0, 1]
+#ifdef MIA_MX_SHFL  // A/B build: the ds_bpermute form
   am = fmaxf(am, __shfl_xor(am, 1, 64));
   am = fmaxf(am, __shfl_xor(am, 2, 64));
+#else
+  am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), XOR1, 0xf, 0xf, false)));
+  am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), XOR2, 0xf, 0xf, false)));
+#endif
   return mx_exponent(am);
 }
 
