@@ -40,6 +40,49 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, void* dst, int
   }
 }
 
+// The same repacking for up to MIA_PACK_BATCH weights in one launch (a training step's per-step bf16 packs
+// are each a few thousand to 131 072 elements: launch-bound, ~4.7 us apiece as separate kernels).  Job j
+// covers the flat range [begin_j, begin_j + total_j); a thread finds its job by a scan of the <= 16 ranges.
+struct PackBatch {
+  MiaPackJob job[MIA_PACK_BATCH];
+  int64_t begin[MIA_PACK_BATCH + 1];
+  int n;
+};
+__global__ void pack_weight_batch_kernel(PackBatch b) {
+  const int64_t total = b.begin[b.n];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int j = 0;
+    while (j + 1 < b.n && i >= b.begin[j + 1]) ++j;
+    const MiaPackJob& J = b.job[j];
+    const int64_t e = i - b.begin[j];
+    const int cout = J.cout, cin = J.cin, kh = J.kh, kw = J.kw;
+    const float* src = J.src;
+    float v;
+    if (J.mode == 0) {
+      const int ci = (int)(e % cin); int64_t q = e / cin;
+      const int kx = (int)(q % kw); q /= kw;
+      const int ky = (int)(q % kh); const int co = (int)(q / kh);
+      v = src[(((int64_t)co * cin + ci) * kh + ky) * kw + kx];
+    } else if (J.mode == 1) {
+      const int co = (int)(e % cout); int64_t q = e / cout;
+      const int kx = (int)(q % kw); q /= kw;
+      const int ky = (int)(q % kh); const int ci = (int)(q / kh);
+      v = src[(((int64_t)co * cin + ci) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
+    } else if (J.mode == 2) {
+      const int half = kw / 2;
+      const int co = (int)(e % cout); int64_t q = e / cout;
+      const int jj = (int)(q % half); q /= half;
+      const int ci = (int)(q % cin); const int p = (int)(q / cin);
+      v = src[((int64_t)co * cin + ci) * kw + 2 * (half - 1 - jj) + p];
+    } else {  // mode 3
+      const int co = (int)(e % cout); int64_t q = e / cout;
+      const int jj = (int)(q % kw); const int ky = (int)(q / kw);
+      v = src[((int64_t)co * kh + ky) * kw + (kw - 1 - jj)];
+    }
+    st_elem(J.dst, J.dtype, e, v);
+  }
+}
+
 // ------------------------------------------------------------------ soft-label CE
 // One block; wave w handles rows w, w+4, ...
 constexpr int CE_NT = 1024;
@@ -576,6 +619,27 @@ extern "C" int mia_pack_weight(const float* src, void* dst, int32_t dtype, int32
   const int64_t total = (int64_t)cout * cin * kh * kw;
   pack_weight_kernel<<<blocks_for(total), 256, 0, as_stream(stream)>>>(src, dst, dtype, cout, cin, kh, kw, mode);
   MIA_LAUNCH_CHECK("pack_weight");
+  return 0;
+}
+
+extern "C" int mia_pack_weights(const MiaPackJob* jobs, int32_t n, mia_stream_t stream) {
+  MIA_CHECK_ARG(jobs && n > 0 && n <= MIA_PACK_BATCH, "pack_weights: 1..%d jobs", MIA_PACK_BATCH);
+  PackBatch b;
+  memset(&b, 0, sizeof(b));
+  b.n = n;
+  b.begin[0] = 0;
+  for (int j = 0; j < n; ++j) {
+    const MiaPackJob& J = jobs[j];
+    MIA_CHECK_ARG(J.src && J.dst && J.cout > 0 && J.cin > 0 && J.kh > 0 && J.kw > 0 && J.mode >= 0 && J.mode <= 3 &&
+                      (J.dtype == MIA_BF16 || J.dtype == MIA_F32),
+                  "pack_weights: job %d: bad arguments (modes 0-3, bf16 / f32)", j);
+    if (J.mode == 2) MIA_CHECK_ARG(J.kh == 1 && J.kw % 2 == 0, "pack_weights: job %d: parity mode needs kh == 1, even kw", j);
+    if (J.mode == 3) MIA_CHECK_ARG(J.cin == 1, "pack_weights: job %d: row-split mode needs cin == 1", j);
+    b.job[j] = J;
+    b.begin[j + 1] = b.begin[j] + (int64_t)J.cout * J.cin * J.kh * J.kw;
+  }
+  pack_weight_batch_kernel<<<blocks_for(b.begin[n]), 256, 0, as_stream(stream)>>>(b);
+  MIA_LAUNCH_CHECK("pack_weights");
   return 0;
 }
 

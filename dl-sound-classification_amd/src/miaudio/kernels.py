@@ -616,6 +616,22 @@ def pack_weight(src: torch.Tensor, dtype: int, mode: int) -> torch.Tensor:
     return out
 
 
+def pack_weights(jobs):
+    """mia_pack_weight for several weights in one launch per 16 (mia_pack_weights): jobs = [(src f32 (cout, cin,
+    kh, kw), dtype, mode)], returns the packed tensors in order."""
+    outs = []
+    for s0 in range(0, len(jobs), L.PACK_BATCH):
+        chunk = jobs[s0:s0 + L.PACK_BATCH]
+        arr = (L.MiaPackJob * len(chunk))()
+        for k, (src, dtype, mode) in enumerate(chunk):
+            cout, cin, kh, kw = src.shape
+            out = torch.empty(src.numel(), dtype=L.torch_dtype(dtype), device=src.device)
+            arr[k] = L.MiaPackJob(src.data_ptr(), out.data_ptr(), dtype, cout, cin, kh, kw, mode)
+            outs.append(out)
+        L.check(L.load().mia_pack_weights(arr, len(chunk), _s()), "mia_pack_weights")
+    return outs
+
+
 def unpack_ohwi_grad(src_ohwi: torch.Tensor, shape, out: torch.Tensor):
     cout, cin, kh, kw = shape
     L.check(L.load().mia_pack_weight(src_ohwi.data_ptr(), out.data_ptr(), L.F32, cout, cin, kh, kw, 4, _s()),

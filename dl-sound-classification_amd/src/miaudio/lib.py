@@ -48,6 +48,14 @@ class MiaEpilogue(C.Structure):
                 ("mx_scales", vp), ("a_colsum", vp)]
 
 
+class MiaPackJob(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("dtype", i32), ("cout", i32), ("cin", i32), ("kh", i32), ("kw", i32),
+                ("mode", i32)]
+
+
+PACK_BATCH = 16  # MIA_PACK_BATCH
+
+
 class MiaMelCfg(C.Structure):
     _fields_ = [("sample_rate", i32), ("n_fft", i32), ("win_length", i32), ("hop", i32),
                 ("n_mels", i32), ("normalize", i32), ("top_db", f32), ("target_mean", f32),
@@ -106,6 +114,7 @@ SIGNATURES = {
     "mia_fe_conv2_wgrad": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, vp, i64, vp]),
     "mia_fe_conv1_wgrad_bn": (C.c_int, [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
     "mia_pack_weight": (C.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "mia_pack_weights": (C.c_int, [P(MiaPackJob), i32, vp]),
     "mia_dropout": (C.c_int, [vp, i32, i64, f32, C.c_uint64, vp]),
     "mia_soft_ce": (C.c_int, [vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "mia_adam_workspace_bytes": (i64, [i32]),

@@ -125,10 +125,15 @@ class EnvNetFunction(torch.autograd.Function):
             return K.bn_fwd_stats(y, P, C, mod.weight, mod.bias, mod.running_mean, mod.running_var,
                                   mod.momentum if mod.momentum is not None else 0.1, mod.eps, training)
 
+        # every conv weight's forward operand (OHWI, compute dtype) in one launch; kept for the backward's
+        # (1, 2)-conv GEMMs, which take the same operand
+        wpk = dict(zip([0, 4] + [8 + 8 * b + o for b in range(4) for o in (0, 4)],
+                       K.pack_weights([(p[i], cd, 0) for i in [0, 4] + [8 + 8 * b + o for b in range(4) for o in (0, 4)]])))
+        saved["wpk"] = wpk
         # ---- frontend conv1: CONVROW over the (B, T/2, 2) view of the waveform
         fe = K.probe("frontend.fwd", *_frontend_work(B, g, tdt, backward=False))
         fe.__enter__()
-        w1 = K.pack_weight(p[0], cd, 0)
+        w1 = wpk[0]
         y1 = torch.empty(B * W1, 32, dtype=tdt, device=dev)
         if cd == L.BF16:
             # wave-persistent conv1 with the BN1 batch statistics accumulated in its epilogue
@@ -145,7 +150,7 @@ class EnvNetFunction(torch.autograd.Function):
             K.gemm(A, Bo, K.epilogue(y1, 32, bias=p[1]), B * W1, 32, 64, cd, tag="conv1.fwd")
             bn1 = bn(0, y1, B * W1, 32)
         # ---- conv2 (stride 2) with BN1+ReLU fused into the operand load
-        w2 = K.pack_weight(p[4], cd, 0)
+        w2 = wpk[4]
         y2 = torch.empty(B * W2, 64, dtype=tdt, device=dev)
         if cd == L.BF16:
             K.fe_conv2_fwd(y1, bn1.scale, bn1.shift, w2, p[5], y2, B, W1, W2, tag="conv2.fwd")
@@ -180,7 +185,7 @@ class EnvNetFunction(torch.autograd.Function):
             (H, W), (ha, wa), (hb, wb), (hp, wp) = g["trunk"][blk]
             _, _, cin, cout, kh, kw = TRUNK[2 * blk]
             pa = 8 + 8 * blk
-            wa_ = K.pack_weight(p[pa], cd, 0)
+            wa_ = wpk[pa]
             ya = torch.empty(B * ha * wa, cout, dtype=tdt, device=dev)
             dense_w2 = cd == L.BF16 and kh == 1 and kw == 2 and cin > 1  # blocks 3-4: (1, 2) convs
             conv3_st = None
@@ -205,7 +210,7 @@ class EnvNetFunction(torch.autograd.Function):
             else:
                 bna = bn(2 + 2 * blk, ya, B * ha * wa, cout)
             _, _, cin2, cout2, kh2, kw2 = TRUNK[2 * blk + 1]
-            wb_ = K.pack_weight(p[pa + 4], cd, 0)
+            wb_ = wpk[pa + 4]
             yb = torch.empty(B * hb * wb, cout2, dtype=tdt, device=dev)
             act = None
             conv8_st = None
@@ -358,6 +363,12 @@ class EnvNetFunction(torch.autograd.Function):
             emit(40 + 2 * li, 42 + 2 * li)
 
         # ---- trunk backward
+        # the flipped / parity / row-split operands the backward-data passes below may take, in one launch
+        # (the forward's OHWI packs are reused as they are)
+        wpk = s["wpk"]
+        bjobs = [(8 + 8 * b + o, 1) for b in range(4) for o in (0, 4)] + [(4, 2)]
+        bjobs += [(8 + 8 * b, 3) for b in range(4) if TRUNK[2 * b][2] == 1]
+        wbk = dict(zip(bjobs, K.pack_weights([(p[i], cd, m) for i, m in bjobs])))
         dpool = dcur  # (B, 84480) in NCHW-flat order of the last pool
         for blk in (3, 2, 1, 0):
             ts = s["trunk"][blk]
@@ -384,7 +395,7 @@ class EnvNetFunction(torch.autograd.Function):
             da = torch.empty(Pa, cout, dtype=tdt, device=dev)
             if ts["act"] is not None:
                 # (1, 2) conv: shifted dY once, then wgrad and dgrad as two dense GEMMs
-                K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, K.pack_weight(p[pa + 4], cd, 0), dWb, da,
+                K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, wpk[pa + 4], dWb, da,
                                tag=f"t{blk}b")
             else:
                 K.gemm(K.dense(dyb, L.RC, Pb, cout2),
@@ -392,7 +403,7 @@ class EnvNetFunction(torch.autograd.Function):
                               scale=ts["bna"].scale, shift=ts["bna"].shift),
                        K.epilogue(dWb, Kb), cout2, Kb, Pb, cd, tag=f"t{blk}b.wgrad")
                 # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
-                wbf = K.pack_weight(p[pa + 4], cd, 1)
+                wbf = wbk[(pa + 4, 1)]
                 Kdb = kh2 * kw2 * cout2
                 if _use_conv8(cd, cin2, cout2, kh2, kw2):
                     K.trunk_conv8(dyb, wbf, da, B, hb, wb, ph=kh2 - 1, pw=kw2 - 1, tag=f"t{blk}b.dgrad")
@@ -415,7 +426,7 @@ class EnvNetFunction(torch.autograd.Function):
             dense_w2 = ts["act"] is not None
             if dense_w2:
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
-                K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, K.pack_weight(p[pa], cd, 0),
+                K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, wpk[pa],
                                dWa, dinp, tag=f"t{blk}a")
             elif cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0:
                 # conv3 weight gradient: wave-persistent, dY read once (csrc/conv3w.hip)
@@ -439,7 +450,7 @@ class EnvNetFunction(torch.autograd.Function):
                 K.conv1ch_dgrad(dya, p[pa], B, ha, wa, dinp, tag=f"t{blk}a.dgrad")
             elif cin == 1:
                 # 1-channel 8x8 conv: P[b][r][iw][ky] = sum_{j,co} dya[b][r][iw+j-7][co] W[co][0][ky][7-j]
-                wr = K.pack_weight(p[pa], cd, 3)
+                wr = wbk[(pa, 3)]
                 Pm = torch.empty(B * ha * W, kh, dtype=torch.float32, device=dev)
                 K.gemm(K.conv(dya, L.KC, B, ha, wa, cout, ha, W, 1, kw, pw=kw - 1),
                        K.dense(wr, L.KC, kh, kw * cout), K.epilogue(Pm, kh), B * ha * W, kh, kw * cout, cd,
@@ -447,7 +458,7 @@ class EnvNetFunction(torch.autograd.Function):
                 dinp = torch.empty(B, H, W, dtype=tdt, device=dev)
                 K.col2im_rows(Pm, B, ha, W, kh, dinp)
             else:
-                waf = K.pack_weight(p[pa], cd, 1)
+                waf = wbk[(pa, 1)]
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
                 Kda = kh * kw * cout
                 K.gemm(K.conv(dya, L.KC, B, ha, wa, cout, H, W, kh, kw, ph=kh - 1, pw=kw - 1),
@@ -480,7 +491,7 @@ class EnvNetFunction(torch.autograd.Function):
         K.unpack_ohwi_grad(dW2, p[4].shape, gw2)
         grads[4] = gw2
         # stride-2 dgrad as two stride-1 parity convolutions
-        wpar = K.pack_weight(p[4], cd, 2)
+        wpar = wbk[(4, 2)]
         da1 = torch.empty(P1, 32, dtype=tdt, device=dev)
         if cd == L.BF16:
             K.fe_conv2_dgrad(dy2, wpar, da1, B, W1, W2, tag="conv2.dgrad")

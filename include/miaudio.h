@@ -404,6 +404,15 @@ int mia_drop_last_col(const void* src, int64_t rows, int32_t w, int32_t c, void*
  * mode 4: inverse of mode 0 on f32 gradients: src (cout,kh,kw,cin) -> dst (cout,cin,kh,kw). */
 int mia_pack_weight(const float* src, void* dst, int32_t dtype, int32_t cout, int32_t cin,
                     int32_t kh, int32_t kw, int32_t mode, mia_stream_t stream);
+/* mia_pack_weight for up to MIA_PACK_BATCH weights in ONE launch (modes 0-3, bf16 or f32 outputs): the
+ * per-step weight packs of a training step are launch-bound tiny kernels. */
+#define MIA_PACK_BATCH 16
+typedef struct MiaPackJob {
+  const float* src;
+  void* dst;
+  int32_t dtype, cout, cin, kh, kw, mode;
+} MiaPackJob;
+int mia_pack_weights(const MiaPackJob* jobs, int32_t n, mia_stream_t stream);
 
 /* out[m][n] = act(sum_s ws[s][m][n] * alpha + bias[n]) with MiaEpilogue semantics —
  * split-K combine; exposed for the FC layers. */

@@ -174,3 +174,22 @@ def test_bf16_eval_with_running_statistics_tracks_autocast(cuda):
     top2 = z32.topk(2, dim=1).values
     decided = (top2[:, 0] - top2[:, 1]) > 2 * (z - z32).abs().max(1).values
     assert torch.equal(z.argmax(1)[decided], z32.argmax(1)[decided])
+
+
+@pytest.mark.parametrize("dtype", [1, 0])  # MIA_BF16, MIA_F32
+def test_pack_weights_batch_equals_single_packs(cuda, dtype):
+    """mia_pack_weights (one launch for up to 16 weights, the EnvNet step's per-step packs) equals
+    mia_pack_weight of each job byte for byte, every mode and shape the model packs; > 16 jobs split."""
+    from src.miaudio import kernels as K
+    g = torch.Generator().manual_seed(7)
+    shapes = [((32, 1, 1, 64), 0), ((64, 32, 1, 16), 0), ((64, 32, 1, 16), 2), ((32, 1, 8, 8), 0), ((32, 1, 8, 8), 3),
+              ((32, 1, 8, 8), 1), ((32, 32, 8, 8), 0), ((32, 32, 8, 8), 1), ((64, 32, 1, 4), 1), ((64, 64, 1, 4), 0),
+              ((128, 64, 1, 2), 0), ((128, 128, 1, 2), 1), ((256, 128, 1, 2), 0), ((256, 256, 1, 2), 1),
+              ((256, 256, 1, 2), 0), ((64, 64, 1, 4), 1), ((32, 32, 8, 8), 1), ((128, 64, 1, 2), 1)]
+    ws = [torch.randn(*sh, generator=g).to(cuda) for sh, _ in shapes]
+    outs = K.pack_weights([(w, dtype, m) for w, (_, m) in zip(ws, shapes)])
+    refs = [K.pack_weight(w, dtype, m) for w, (_, m) in zip(ws, shapes)]
+    torch.cuda.synchronize()
+    assert len(outs) == len(shapes)
+    for o, r in zip(outs, refs):
+        assert torch.equal(o, r)
