@@ -76,6 +76,26 @@ __global__ __launch_bounds__(256) void shift_pad2_kernel(const bf16* __restrict_
   }
 }
 
+// dst = [one zero pixel] + dy re-laid on the input grid: dst[1 + r*w + x] = dy[r*(w-1) + x] for x < w-1, zero
+// at x = w-1 (one 16-B piece per thread); the optional `zp` (zc bf16) is zeroed too -- the pad pixel after the
+// forward input, which the weight-gradient view reads against a zero gradient and so must be finite
+__global__ __launch_bounds__(256) void pad_w2_kernel(const u32x4* __restrict__ dy, int64_t rows, int w, int c16,
+                                                     u32x4* __restrict__ dst, u32x4* __restrict__ zp, int zc16) {
+  const int64_t total = (1 + rows * w) * c16;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / c16;
+    const int k = (int)(i - pix * c16);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (pix > 0) {
+      const int64_t q = pix - 1, r = q / w;
+      const int x = (int)(q - r * w);
+      if (x < w - 1) v = dy[(r * (w - 1) + x) * c16 + k];
+    }
+    dst[i] = v;
+    if (zp && i < zc16) zp[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
 // dst[r][x] = src[r][x] for x < w-1 (drops the padded last column of a (1, 2)-conv forward
 // computed over every input pixel), 16 B per thread
 __global__ __launch_bounds__(256) void drop_last_col_kernel(const u32x4* __restrict__ src, int64_t rows, int w,
@@ -115,6 +135,18 @@ extern "C" int mia_shift_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t
   shift_pad2_kernel<<<grid_for(rows * w * (c / 8)), 256, 0, as_stream(stream)>>>(
       reinterpret_cast<const bf16*>(dy), rows, w, c, reinterpret_cast<bf16*>(out));
   MIA_LAUNCH_CHECK("shift_pad_w2");
+  return 0;
+}
+
+extern "C" int mia_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t c, void* dst, void* zero_pixel,
+                          int32_t zc, mia_stream_t stream) {
+  MIA_CHECK_ARG(dy && dst && rows > 0 && w >= 2 && c > 0 && c % 8 == 0 && zc % 8 == 0 && (zc == 0 || zero_pixel),
+                "pad_w2: bad arguments");
+  MIA_CHECK_ARG(al16(dy) && al16(dst) && (!zero_pixel || al16(zero_pixel)), "pad_w2: 16-byte aligned pointers");
+  pad_w2_kernel<<<grid_for((1 + rows * w) * (c / 8)), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const u32x4*>(dy), rows, w, c / 8, reinterpret_cast<u32x4*>(dst),
+      reinterpret_cast<u32x4*>(zero_pixel), zc / 8);
+  MIA_LAUNCH_CHECK("pad_w2");
   return 0;
 }
 

@@ -8,6 +8,8 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import os
+
 import torch
 
 from . import lib as L
@@ -590,16 +592,33 @@ def conv_w2_fwd(x: torch.Tensor, rows: int, w: int, cin: int, wpk: torch.Tensor,
     L.check(L.load().mia_drop_last_col(ypad.data_ptr(), rows, w, cout, out.data_ptr(), _s()), "mia_drop_last_col")
 
 
+W2_SHIFT = os.environ.get("MIA_W2_SHIFT", "0") == "1"  # A/B switch: the interleaved shifted-copy form
+
+
 def trunk_bwd_w2(dy: torch.Tensor, a: torch.Tensor, rows: int, w: int, cout: int, cin: int, wpk: torch.Tensor,
-                 dw: torch.Tensor, dx: torch.Tensor, tag: str = ""):
-    """Backward of a (1, 2) conv, stride 1 (EnvNet trunk blocks 3-4): one pass builds the shifted
-    gradient Ashift[q][co*2+kx] = dy[q-kx][co] over the input pixels, then two dense GEMMs:
-    dw (cout, 2*cin) OHWI f32 = Ashift^T a, and dx (rows*w, cin) bf16 = Ashift W (W = wpk (cout, 2*cin),
-    read as the (2*cout, cin) K-major matrix it already is)."""
+                 dw: torch.Tensor, dx: torch.Tensor, tag: str = "", wflip: torch.Tensor | None = None):
+    """Backward of a (1, 2) conv, stride 1 (EnvNet trunk blocks 3-4).  One pass lays dy on the input grid
+    (G = [zero pixel] + dy with a zero last column per row, mia_pad_w2; it also zeroes a's pad pixel), then two
+    dense GEMMs through overlapping views of G and a (rows of 2 pixels at a 1-pixel stride):
+    dw (cout, 2*cin) OHWI f32 = G[1:]^T [a[q], a[q+1]], and dx (rows*w, cin) bf16 = [G[q], G[q+1]] Wflip with
+    Wflip = the mode-1 pack (cin, 2*cout), [ci][kx'][co] = W[co][ci][0][1-kx'] -- half the bytes of the
+    interleaved shifted copy Ashift[q][co*2+kx] = dy[q-kx][co] of the previous form (MIA_W2_SHIFT=1, which
+    uses wpk (cout, 2*cin) read as the (2*cout, cin) K-major matrix).  a must carry one pad pixel."""
     assert dy.dtype == torch.bfloat16 and a.dtype == torch.bfloat16 and dw.dtype == torch.float32
     assert dy.numel() == rows * (w - 1) * cout and a.numel() == rows * w * cin and dw.numel() == cout * 2 * cin
     assert dx.numel() == rows * w * cin and dx.dtype == torch.bfloat16 and wpk.numel() == cout * 2 * cin
     P = rows * w
+    if not W2_SHIFT and wflip is not None:
+        assert a.untyped_storage().nbytes() - a.storage_offset() * 2 >= (P + 1) * cin * 2, "a needs a pad pixel"
+        G = workspace((P + 1) * cout * 2, dy.device, "w2shift")[: (P + 1) * cout * 2].view(torch.bfloat16)
+        L.check(L.load().mia_pad_w2(dy.data_ptr(), rows, w, cout, G.data_ptr(), a.data_ptr() + P * cin * 2, cin, _s()),
+                "mia_pad_w2")
+        G1 = G[cout:]
+        gemm(dense(G1, L.RC, P, cout), dense(a, L.RC, P, 2 * cin, ld=cin), epilogue(dw, 2 * cin), cout, 2 * cin, P,
+             L.BF16, tag=f"{tag}.wgrad" if tag else None)
+        gemm(dense(G, L.KC, P, 2 * cout, ld=cout), dense(wflip, L.KC, cin, 2 * cout), epilogue(dx, cin), P, cin,
+             2 * cout, L.BF16, tag=f"{tag}.dgrad" if tag else None)
+        return
     ash = workspace(P * 2 * cout * 2, dy.device, "w2shift")[: P * 2 * cout * 2].view(torch.bfloat16)
     L.check(L.load().mia_shift_pad_w2(dy.data_ptr(), rows, w, cout, ash.data_ptr(), _s()), "mia_shift_pad_w2")
     gemm(dense(ash, L.RC, P, 2 * cout), dense(a, L.RC, P, cin), epilogue(dw, cin), 2 * cout, cin, P, L.BF16,

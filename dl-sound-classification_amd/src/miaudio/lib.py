@@ -102,6 +102,7 @@ SIGNATURES = {
     "mia_fe_conv2_dgrad": (C.c_int, [vp, vp, vp, i32, i32, i32, vp]),
     "mia_bn_relu_apply": (C.c_int, [vp, i64, i32, vp, vp, vp, vp]),
     "mia_shift_pad_w2": (C.c_int, [vp, i64, i32, i32, vp, vp]),
+    "mia_pad_w2": (C.c_int, [vp, i64, i32, i32, vp, vp, i32, vp]),
     "mia_drop_last_col": (C.c_int, [vp, i64, i32, i32, vp, vp]),
     "mia_fe_conv1_fwd": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),
     "mia_fe_conv3_fwd": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]),

@@ -395,7 +395,7 @@ class EnvNetFunction(torch.autograd.Function):
             da = torch.empty(Pa, cout, dtype=tdt, device=dev)
             if ts["act"] is not None:
                 # (1, 2) conv: shifted dY once, then wgrad and dgrad as two dense GEMMs
-                K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, wpk[pa + 4], dWb, da,
+                K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, wpk[pa + 4], dWb, da, wflip=wbk[(pa + 4, 1)],
                                tag=f"t{blk}b")
             else:
                 K.gemm(K.dense(dyb, L.RC, Pb, cout2),
@@ -427,7 +427,7 @@ class EnvNetFunction(torch.autograd.Function):
             if dense_w2:
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
                 K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, wpk[pa],
-                               dWa, dinp, tag=f"t{blk}a")
+                               dWa, dinp, tag=f"t{blk}a", wflip=wbk[(pa, 1)])
             elif cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0:
                 # conv3 weight gradient: wave-persistent, dY read once (csrc/conv3w.hip)
                 K.conv3_wgrad(ts["inp"], dya, dWa, B, H, W, tag=f"t{blk}a.wgrad")

@@ -392,6 +392,11 @@ int mia_bn_relu_apply(const void* x, int64_t P, int32_t C, const float* scale, c
 /* out[r][x][2c+kx] = dy[r][x-kx][c] (0 <= x-kx < w-1, else 0): dy bf16 (rows, w-1, c), out bf16
  * (rows, w, 2c), c % 8 == 0, 16-byte aligned. */
 int mia_shift_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t c, void* out, mia_stream_t stream);
+/* The (1, 2)-conv backward's gradient on the input grid: dst (1 + rows*w pixels x c, bf16) = one zero pixel, then
+ * dy (rows x (w-1) x c) re-laid with a zero at each row's last column; zero_pixel (zc bf16, may be null) is
+ * zeroed too.  Both backward GEMMs then read dst through overlapping dense views (trunk_bwd_w2). */
+int mia_pad_w2(const void* dy, int64_t rows, int32_t w, int32_t c, void* dst, void* zero_pixel, int32_t zc,
+               mia_stream_t stream);
 /* dst[r][x] = src[r][x] for x < w-1: src bf16 (rows, w, c) -> dst (rows, w-1, c); c % 8 == 0. */
 int mia_drop_last_col(const void* src, int64_t rows, int32_t w, int32_t c, void* dst, mia_stream_t stream);
 
