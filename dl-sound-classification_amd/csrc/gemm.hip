@@ -1699,11 +1699,14 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
   // plain backward-data GEMMs): 16 lanes cover one 256-B output row, 4 rows per store instruction
   const bool save = g.e.act == MIA_ACT_GELU_SAVE || g.e.act == MIA_ACT_GELU_SAVE_D;
   const bool save_d = g.e.act == MIA_ACT_GELU_SAVE_D;
+  // drop-mode row map (MIA_RM_DROP): plain / bias / ReLU output only
+  const bool drop = g.e.rm_inner && g.e.rm_offset == MIA_RM_DROP && g.e.rm_istride == 1 &&
+                    (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU);
   const bool plain16 = g.split == 1 && g.e.dtype == MIA_BF16 &&
                        (g.e.act == MIA_ACT_NONE || g.e.act == MIA_ACT_RELU || g.e.act == MIA_ACT_GELU ||
                         (save && g.e.aux_dtype == MIA_BF16 && (g.e.ldaux & 7) == 0 &&
                          ((reinterpret_cast<uintptr_t>(g.e.aux)) & 15) == 0)) &&
-                       !g.e.accumulate && !g.e.rm_inner &&
+                       !g.e.accumulate && (!g.e.rm_inner || drop) &&
                        g.e.alpha == 1.f && m0 + 128 <= g.M && n0 + 128 <= g.N && (g.e.ldc & 7) == 0 &&
                        ((reinterpret_cast<uintptr_t>(g.e.ptr)) & 15) == 0;
   if (plain16) {
@@ -1752,7 +1755,13 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       }
 #pragma unroll
       for (int c = 0; c < 8; ++c) v[c] = relu ? fmaxf(v[c], 0.f) : (gelu ? gelu_erf(v[c]) : v[c]);
-      *reinterpret_cast<uint4*>(out + (m0 + row) * g.e.ldc + n0 + col) = pack(v);
+      int64_t prow = m0 + row;
+      if (drop) {
+        const int64_t x = prow % g.e.rm_inner;
+        if (x >= g.e.rm_outer) continue;
+        prow = (prow / g.e.rm_inner) * g.e.rm_outer + x;
+      }
+      *reinterpret_cast<uint4*>(out + prow * g.e.ldc + n0 + col) = pack(v);
     }
     return;
   }

@@ -70,7 +70,15 @@ static __device__ __forceinline__ void epi_store(const EpiDev& e, int64_t m, int
     default: break;
   }
   int64_t prow = m;
-  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+  if (e.rm_inner) {
+    if (e.rm_offset == MIA_RM_DROP) {  // drop mode: the last row of every rm_inner group is not stored
+      const int64_t x = m % e.rm_inner;
+      if (x >= e.rm_outer) return;
+      prow = (m / e.rm_inner) * e.rm_outer + x;
+    } else {
+      prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+    }
+  }
   const int64_t idx = prow * e.ldc + n;
   if (e.accumulate) v += ld_elem(e.ptr, e.dtype, idx);
   st_elem(e.ptr, e.dtype, idx, v);
@@ -122,7 +130,15 @@ static __device__ __forceinline__ void st16(void* p, int dtype, int64_t idx, con
 // element.
 static __device__ __forceinline__ void epi_store16(const EpiDev& e, int64_t m, int64_t n0, int64_t N, const float* v) {
   int64_t prow = m;
-  if (e.rm_inner) prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+  if (e.rm_inner) {
+    if (e.rm_offset == MIA_RM_DROP) {
+      const int64_t x = m % e.rm_inner;
+      if (x >= e.rm_outer) return;
+      prow = (m / e.rm_inner) * e.rm_outer + x;
+    } else {
+      prow = (m / e.rm_inner) * e.rm_outer + (m % e.rm_inner) * e.rm_istride + e.rm_offset;
+    }
+  }
   const int64_t idx = prow * e.ldc + n0;
   const bool uses_aux = e.act == MIA_DACT_NZ || e.act == MIA_DACT_GELU || e.act == MIA_ACT_ADD_AUX ||
                         e.act == MIA_ACT_GELU_SAVE || e.act == MIA_ACT_GELU_SAVE_D || e.act == MIA_DACT_MUL;

@@ -54,6 +54,8 @@ struct MArgs {
   float* acs_part;    // A-operand column sums (RC A only): [split][M] f32, written by the bn == 0 tiles
   uint8_t* mxq;       // optional MX-fp8 copy of a bf16 output: e4m3 [M][N] (row stride N) ...
   uint8_t* mxs;       // ... and its scales [M][N / 32]
+  int64_t drop_w;     // EPI_PLAIN with a drop-mode row map (MIA_RM_DROP): row m -> m - m / drop_w, rows with
+                      // m % drop_w == drop_w - 1 not stored (0: off)
 };
 
 typedef unsigned mg_u32x4 __attribute__((ext_vector_type(4)));
@@ -413,6 +415,13 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
             *reinterpret_cast<uint2*>(g.mxq + m * g.N + n) = p;
             if ((cc & 3) == 0) g.mxs[m * (g.N >> 5) + (n >> 5)] = (uint8_t)(e + 127);
           }
+        }
+      }
+      if constexpr (EPI == EPI_PLAIN) {
+        if (g.drop_w) {
+          const int64_t x = m % g.drop_w;
+          if (ok && x != g.drop_w - 1) mg_st16(reinterpret_cast<bf16*>(g.out) + (m - m / g.drop_w) * g.ldc + n, o);
+          continue;
         }
       }
       if (ok) mg_st16(reinterpret_cast<bf16*>(g.out) + m * g.ldc + n, o);
@@ -897,7 +906,10 @@ namespace mgemm {
 
 // Which epilogue kind the kernel would run for E (-1: not this kernel)
 int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
-  if (E.accumulate || E.rm_inner || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
+  // a drop-mode row map (MIA_RM_DROP) only on a plain / bias bf16 output without an MX copy
+  const bool drop = E.rm_inner && E.rm_offset == MIA_RM_DROP && E.rm_istride == 1 && E.rm_outer == E.rm_inner - 1 &&
+                    E.act == MIA_ACT_NONE && E.dtype == MIA_BF16 && !E.mx_q && !E.colsum;
+  if (E.accumulate || (E.rm_inner && !drop) || E.sqsum || E.alpha != 1.f || !E.ptr) return -1;
   if (E.mx_q && (!E.mx_scales || E.dtype != MIA_BF16 || E.ldc != N || N % 32 ||
                  (E.colsum && E.act != MIA_DACT_MUL) ||
                  !(E.act == MIA_ACT_NONE || E.act == MIA_ACT_GELU || E.act == MIA_ACT_GELU_SAVE ||
@@ -981,6 +993,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   mg_geometry(M, N, K, a.split, a.kper);
   a.nbm = (int)cdiv(M, MG_BM); a.nbn = (int)cdiv(N, MG_BN);
   a.out = E.ptr; a.ldc = E.ldc; a.out_f32 = E.dtype == MIA_F32;
+  a.drop_w = E.rm_inner && E.rm_offset == MIA_RM_DROP ? E.rm_inner : 0;
   a.bias = E.bias; a.aux = E.aux; a.ldaux = E.ldaux;
   a.mxq = reinterpret_cast<uint8_t*>(E.mx_q); a.mxs = reinterpret_cast<uint8_t*>(E.mx_scales);
   const int need_ws = a.split > 1 || E.colsum || E.a_colsum;

@@ -578,7 +578,8 @@ def bn_relu_apply(x: torch.Tensor, P: int, C: int, bn: BNState, out: torch.Tenso
 def conv_w2_fwd(x: torch.Tensor, rows: int, w: int, cin: int, wpk: torch.Tensor, bias, out: torch.Tensor,
                 tag: str | None = None):
     """(1, 2) conv forward, stride 1 (EnvNet trunk blocks 3-4), as one dense GEMM over every input
-    pixel (rows of the im2col view overlap: ld = cin, length 2*cin) + a drop of the last column.
+    pixel (rows of the im2col view overlap: ld = cin, length 2*cin) whose epilogue drops each row's last
+    column (drop-mode row map, MIA_RM_DROP; MIA_W2_DROPCOPY=1: a full-grid output + mia_drop_last_col).
     x bf16 (rows*w, cin) whose storage holds ONE extra pixel (read by the dropped last output);
     wpk bf16 (cout, 2*cin) OHWI; out bf16 (rows*(w-1), cout)."""
     cout = wpk.numel() // (2 * cin)
@@ -586,6 +587,11 @@ def conv_w2_fwd(x: torch.Tensor, rows: int, w: int, cin: int, wpk: torch.Tensor,
     assert x.numel() == rows * w * cin and out.numel() == rows * (w - 1) * cout
     assert x.untyped_storage().nbytes() - x.storage_offset() * 2 >= (rows * w + 1) * cin * 2, "x needs a pad pixel"
     P = rows * w
+    if not W2_DROPCOPY:
+        # the epilogue's drop-mode row map stores the w - 1 valid columns of every row straight into out
+        gemm(dense(x, L.KC, P, 2 * cin, ld=cin), dense(wpk, L.KC, cout, 2 * cin),
+             epilogue(out, cout, bias=bias, rowmap=(w, w - 1, 1, L.RM_DROP)), P, cout, 2 * cin, L.BF16, tag=tag)
+        return
     ypad = workspace(P * cout * 2, x.device, "w2fwd")[: P * cout * 2].view(torch.bfloat16)
     gemm(dense(x, L.KC, P, 2 * cin, ld=cin), dense(wpk, L.KC, cout, 2 * cin), epilogue(ypad, cout, bias=bias),
          P, cout, 2 * cin, L.BF16, tag=tag)
@@ -593,6 +599,7 @@ def conv_w2_fwd(x: torch.Tensor, rows: int, w: int, cin: int, wpk: torch.Tensor,
 
 
 W2_SHIFT = os.environ.get("MIA_W2_SHIFT", "0") == "1"  # A/B switch: the interleaved shifted-copy form
+W2_DROPCOPY = os.environ.get("MIA_W2_DROPCOPY", "0") == "1"  # A/B switch: full-grid forward output + column drop
 
 
 def trunk_bwd_w2(dy: torch.Tensor, a: torch.Tensor, rows: int, w: int, cout: int, cin: int, wpk: torch.Tensor,

@@ -54,6 +54,7 @@ class MiaPackJob(C.Structure):
 
 
 PACK_BATCH = 16  # MIA_PACK_BATCH
+RM_DROP = -1  # MIA_RM_DROP: MiaEpilogue.rm_offset sentinel of the drop-mode row map
 
 
 class MiaMelCfg(C.Structure):

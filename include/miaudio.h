@@ -29,6 +29,7 @@ extern "C" {
 typedef void* mia_stream_t; /* hipStream_t */
 
 enum { MIA_F32 = 0, MIA_BF16 = 1, MIA_U8 = 2 };
+#define MIA_RM_DROP (-1) /* MiaEpilogue.rm_offset sentinel: drop-mode row map */
 enum { MIA_OP_DENSE = 0, MIA_OP_CONV = 1, MIA_OP_CONVROW = 2 };
 enum { MIA_LAYOUT_KC = 0, MIA_LAYOUT_RC = 1 };
 enum { MIA_PRE_NONE = 0, MIA_PRE_AFFINE = 1, MIA_PRE_AFFINE_RELU = 2, MIA_PRE_GELU = 3 };
@@ -60,6 +61,9 @@ typedef struct MiaOperand {
  *   v = alpha*acc (+ bias[n]); act; (v += old C if accumulate); store as dtype at
  *   ptr[prow(m)*ldc + n] with prow(m) = m if rm_inner == 0 else
  *   (m / rm_inner)*rm_outer + (m % rm_inner)*rm_istride + rm_offset.
+ *   rm_offset == MIA_RM_DROP (drop mode; plain / bias / ReLU epilogues, rm_istride 1): prow(m) =
+ *   (m / rm_inner)*rm_outer + m % rm_inner and rows with m % rm_inner >= rm_outer are not stored -- a (1, 2)
+ *   conv computed over every input pixel (rm_inner = w) stores its w - 1 valid columns per row.
  *   DACT_NZ  : v *= (aux[m][n] != 0) * act_scale   (ReLU+dropout backward from saved output)
  *   DACT_GELU: v *= gelu'(aux[m][n])                (GELU backward from saved pre-activation)
  *   ADD_AUX  : v += aux[m][n]                       (residual connection into a new tensor)
@@ -70,7 +74,7 @@ typedef struct MiaEpilogue {
   void* ptr;
   int32_t dtype, act, accumulate, aux_dtype;
   int64_t ldc;
-  int64_t rm_inner, rm_outer, rm_istride, rm_offset;
+  int64_t rm_inner, rm_outer, rm_istride, rm_offset;  /* rm_offset MIA_RM_DROP: drop mode (above) */
   const float* bias;
   const void* aux;
   int64_t ldaux;

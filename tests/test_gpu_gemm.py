@@ -734,11 +734,14 @@ def test_fe_conv2_wgrad(cuda, n, w1, pre):
     assert rel(got, ref) < 1e-3
 
 
-@pytest.mark.parametrize("B,H,W,cin,cout", [(3, 4, 37, 64, 128), (2, 10, 67, 256, 256)])
+@pytest.mark.parametrize("B,H,W,cin,cout", [(3, 4, 37, 64, 128), (2, 10, 67, 256, 256), (8, 10, 138, 128, 256)])
 def test_trunk_w2_dense(cuda, B, H, W, cin, cout):
     """(1, 2) conv (EnvNet trunk blocks 3-4) as dense GEMMs: forward over every input pixel with
-    overlapping im2col rows + last-column drop, and the backward (shifted dY once, then wgrad and
-    dgrad GEMMs) vs float64 restatements on the same bf16 operands; BN+ReLU materialisation."""
+    overlapping im2col rows whose epilogue drops each row's last column (drop-mode row map; the last case
+    runs on the 256x256 kernel, the others on the 128x128 one with ragged edge tiles), and the backward in
+    both forms -- dY laid on the input grid + overlapping views (mia_pad_w2, the default) and the
+    interleaved shifted copy -- vs float64 restatements on the same bf16 operands; BN+ReLU
+    materialisation."""
     g = torch.Generator().manual_seed(W + cin)
     x = torch.randn(B * H * W, cin, generator=g).to(torch.bfloat16)
     dy = (torch.randn(B * H * (W - 1), cout, generator=g) * 0.1).to(torch.bfloat16)
@@ -754,7 +757,12 @@ def test_trunk_w2_dense(cuda, B, H, W, cin, cout):
     K.conv_w2_fwd(a, B * H, W, cin, wpk, bias.to(cuda), y)
     dw = torch.full((cout, 2 * cin), float("nan"), device=cuda)
     dx = torch.full((B * H * W, cin), float("nan"), dtype=torch.bfloat16, device=cuda)
-    K.trunk_bwd_w2(dy.to(cuda), a, B * H, W, cout, cin, wpk, dw, dx)
+    K.trunk_bwd_w2(dy.to(cuda), a, B * H, W, cout, cin, wpk, dw, dx)  # shifted-copy form (no wflip)
+    dw2 = torch.full((cout, 2 * cin), float("nan"), device=cuda)
+    dx2 = torch.full((B * H * W, cin), float("nan"), dtype=torch.bfloat16, device=cuda)
+    apad = a.as_strided((cin,), (1,), a.storage_offset() + B * H * W * cin)
+    apad.fill_(float("nan"))  # the input-grid form must zero the pad pixel it multiplies by a zero gradient
+    K.trunk_bwd_w2(dy.to(cuda), a, B * H, W, cout, cin, wpk, dw2, dx2, wflip=K.pack_weight(Wt.to(cuda), L.BF16, 1))
     torch.cuda.synchronize()
     ar = torch.relu(x.float() * sc + sh).to(torch.bfloat16)
     # fused multiply-add in the kernel vs mul+add here: at most one bf16 rounding step apart
@@ -765,13 +773,14 @@ def test_trunk_w2_dense(cuda, B, H, W, cin, cout):
     yref = sum(torch.einsum("rxi,oi->rxo", a4[:, kx:kx + W - 1], wb[:, :, kx]) for kx in range(2)) + bias.double()
     assert rel(y.double().cpu().view(B * H, W - 1, cout), yref) < 1e-2
     ref = torch.stack([torch.einsum("rxo,rxi->oi", d4, a4[:, kx:kx + W - 1]) for kx in range(2)], 1)  # (co, kx, ci)
-    got = dw.double().cpu().view(cout, 2, cin)
-    assert torch.isfinite(got).all()
-    assert rel(got, ref) < 1e-3
     dxref = torch.zeros(B * H, W, cin, dtype=torch.float64)
     for kx in range(2):
         dxref[:, kx:kx + W - 1] += torch.einsum("rxo,oi->rxi", d4, wb[:, :, kx])
-    assert rel(dx.double().cpu().view(B * H, W, cin), dxref) < 1e-2
+    for dwx, dxx in ((dw, dx), (dw2, dx2)):
+        got = dwx.double().cpu().view(cout, 2, cin)
+        assert torch.isfinite(got).all()
+        assert rel(got, ref) < 1e-3
+        assert rel(dxx.double().cpu().view(B * H, W, cin), dxref) < 1e-2
 
 
 def _tile_sqsums(out, M, N):
