@@ -42,7 +42,9 @@ struct C8Args {
   const bf16* w;      // (32 co, 8 ky, 8 kx, 32 ci)
   const float* bias;  // (32) or null
   bf16* y;            // (n, oh, ow, 32)
-  float* part;        // [waves][32][2] BN shifted sums about bias, or null
+  float* part;        // [waves][32][2] BN shifted sums about bias (STATS) or ReLU+BN backward sums (RED), or null
+  const bf16* bx;     // RED: the BN input at the output pixels (n, oh, ow, 32)
+  const float *bsc, *bsh, *bmu, *bis;  // RED: its BN scale, shift, mean, invstd (32 each)
   int n, h, wd, ph, pw, oh, ow, nchunk;
   int nfull0, nsplit;  // items < nfull0 cover all output rows; the rest are row parts (nsplit per chunk)
 };
@@ -64,15 +66,26 @@ __device__ __forceinline__ u32x4 cook(u32x4 u, bool ok, const float* sc, const f
 #ifndef C8_EDGE
 #define C8_EDGE 1
 #endif
-template <bool PRE, bool STATS, int JU>
+// RED (backward-data only): the epilogue also forms the ReLU+BN backward sums of the stored gradient
+// dA = dX against the BN input bx of the forward (mask relu(bx*scale+shift) > 0, xhat = (bx-mean)*invstd):
+// sum dA*mask and sum dA*mask*xhat per channel, as mia_bn_relu_bwd_reduce computes them from a second read
+// of dA.  The bx row of output row r-7 is loaded when input row r starts, so its latency sits under the
+// row's MFMAs.
+template <bool PRE, bool STATS, bool RED, int JU>
 __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv8_kernel(C8Args g) {
   __shared__ __attribute__((aligned(16))) char smem[C8_WB + 4 * C8_STRIP];
-  __shared__ __attribute__((aligned(16))) float prm[96];  // pre-op scale, shift, bias (kept out of VGPRs)
+  __shared__ __attribute__((aligned(16))) float prm[224];  // pre-op scale, shift, bias, RED's BN (out of VGPRs)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 32) {
     prm[t] = g.ps ? g.ps[t] : 1.f;
     prm[32 + t] = g.pt ? g.pt[t] : 0.f;
     prm[64 + t] = g.bias ? g.bias[t] : 0.f;
+    if constexpr (RED) {
+      prm[96 + t] = g.bsc[t];
+      prm[128 + t] = g.bsh[t];
+      prm[160 + t] = g.bmu[t];
+      prm[192 + t] = g.bis[t];
+    }
   }
 
   // weights -> fragment order: fragment f = (ky*8 + kx)*2 + c, piece [lane] = W[lane&31][ky][kx][16c + 8(lane>>5) .. +8]
@@ -96,6 +109,7 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
 
   f32x16 acc[8][2];
   u32x4 raw[C8_LDC];
+  u32x4 bxr[2][2];  // RED: bx of the output row being retired, [pixel tile][channel half]
   uint32_t rok = 0;
 
   for (int item = gw; item < items; item += nw) {
@@ -137,6 +151,15 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
               cook(raw[s], (rok >> s) & 1u, PRE ? sc : nullptr, sh);
       }
     };
+    auto load_bx = [&](int oy) __attribute__((always_inline)) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int ox = x0 + 32 * tt + (lane & 31);
+        const int64_t off = ox < g.ow ? (((int64_t)b * g.oh + oy) * g.ow + ox) * 32 + c0 : 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bxr[tt][h] = *reinterpret_cast<const u32x4*>(g.bx + off + 16 * h);
+      }
+    };
     // output row oy from accumulator slot S: bias, bf16 store, BN statistics
     auto emit = [&](const f32x16 (&a)[2], int oy) __attribute__((always_inline)) {
       float bv[16];
@@ -171,6 +194,18 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
                 s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
                 s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
               }
+              if constexpr (RED) {
+                const uint32_t xw = bxr[tt][h][i];
+                const float xv[2] = {__uint_as_float(xw << 16), __uint_as_float(xw & 0xffff0000u)};
+                const float dv[2] = {(float)ylo, (float)yhi};
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                  const int c = c0 + 16 * h + 2 * i + k;
+                  const float gk = fmaf(xv[k], prm[96 + c], prm[128 + c]) > 0.f ? dv[k] : 0.f;
+                  s1[e + k] += gk;
+                  s2[e + k] = fmaf(gk, (xv[k] - prm[160 + c]) * prm[192 + c], s2[e + k]);
+                }
+              }
             }
             *reinterpret_cast<u32x4*>(dst + 16 * h) = u32x4{w4[0], w4[1], w4[2], w4[3]};
           }
@@ -199,6 +234,9 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         wave_sync();
       }
       if (r + 1 < r_hi) load_row(r + 1);
+      if constexpr (RED) {
+        if (r - 7 >= oy_lo) load_bx(r - 7);
+      }
       if (live) {
         // (kx, c) blocks of 16 MFMAs; the 10 fragments of block j+1 are read while block j computes
         // (interleaved one DS read per MFMA), so every LDS read has >= 6 MFMAs of cover
@@ -265,7 +303,7 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     }
   }
 
-  if constexpr (STATS) {
+  if constexpr (STATS || RED) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
@@ -303,7 +341,8 @@ extern "C" int mia_trunk_conv8(const void* x, const float* pre_scale, const floa
   MIA_CHECK_ARG(oh > 0 && ow > 0, "trunk_conv8: output is empty");
   MIA_CHECK_ARG((int64_t)n * h * wd * 4 < (1ll << 40), "trunk_conv8: input too large");
   C8Args a{reinterpret_cast<const bf16*>(x), pre_scale, pre_shift, reinterpret_cast<const bf16*>(w), bias,
-           reinterpret_cast<bf16*>(y), partial, n, h, wd, ph, pw, oh, ow, (int)cdiv(ow, C8_PX), 0, 1};
+           reinterpret_cast<bf16*>(y), partial, nullptr, nullptr, nullptr, nullptr, nullptr,
+           n, h, wd, ph, pw, oh, ow, (int)cdiv(ow, C8_PX), 0, 1};
   MIA_CHECK_ARG((int64_t)n * a.nchunk * 8 < (1ll << 31), "trunk_conv8: too many items");
   // balance the last round: split the chunks left over after the full rounds into row parts
   const int nw = 4 * nblocks, full = n * a.nchunk, rem = full % nw;
@@ -313,12 +352,50 @@ extern "C" int mia_trunk_conv8(const void* x, const float* pre_scale, const floa
   // (kx, c) block loop unrolled by 2 only (double-buffer parity static): a 16x smaller body than the
   // full unroll, measured 3 % faster on the forward (instruction-cache pressure) and equal on dgrad
   if (pre_scale) {
-    if (partial) conv8_kernel<true, true, 2><<<nblocks, C8_NT, 0, s>>>(a);
-    else conv8_kernel<true, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
+    if (partial) conv8_kernel<true, true, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
+    else conv8_kernel<true, false, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
   } else {
-    if (partial) conv8_kernel<false, true, 2><<<nblocks, C8_NT, 0, s>>>(a);
-    else conv8_kernel<false, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
+    if (partial) conv8_kernel<false, true, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
+    else conv8_kernel<false, false, false, 2><<<nblocks, C8_NT, 0, s>>>(a);
   }
   MIA_LAUNCH_CHECK("trunk_conv8");
+  return 0;
+}
+
+namespace {
+// per-wave partials [nw][32][2] -> dbeta[c] = sum q0, dgamma[c] = sum q1 (one block per channel, f64 sums)
+__global__ void c8_red_final_kernel(const float* __restrict__ part, int nw, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x;
+  const double s1 = block_sum_strided(part + c * 2, nw, 64);
+  const double s2 = block_sum_strided(part + c * 2 + 1, nw, 64);
+  if (threadIdx.x == 0) {
+    dbeta[c] = (float)s1;
+    dgamma[c] = (float)s2;
+  }
+}
+}  // namespace
+
+extern "C" int mia_trunk_conv8_dgrad_bn(const void* dy, const void* w, void* dx, int32_t nblocks, int32_t n,
+                                        int32_t h, int32_t wd, const void* bx, const float* scale,
+                                        const float* shift, const float* mean, const float* invstd, float* dgamma,
+                                        float* dbeta, float* partial, mia_stream_t stream) {
+  MIA_CHECK_ARG(dy && w && dx && bx && scale && shift && mean && invstd && dgamma && dbeta && partial && n > 0 &&
+                    h > 0 && wd > 0 && nblocks > 0,
+                "trunk_conv8_dgrad_bn: bad arguments");
+  MIA_CHECK_ARG(al16(dy) && al16(w) && al16(dx) && al16(bx), "trunk_conv8_dgrad_bn: dy/w/dx/bx must be 16-byte aligned");
+  const int oh = h + 7, ow = wd + 7;
+  MIA_CHECK_ARG((int64_t)n * oh * ow * 4 < (1ll << 40), "trunk_conv8_dgrad_bn: input too large");
+  C8Args a{reinterpret_cast<const bf16*>(dy), nullptr, nullptr, reinterpret_cast<const bf16*>(w), nullptr,
+           reinterpret_cast<bf16*>(dx), partial, reinterpret_cast<const bf16*>(bx), scale, shift, mean, invstd,
+           n, h, wd, 7, 7, oh, ow, (int)cdiv(ow, C8_PX), 0, 1};
+  MIA_CHECK_ARG((int64_t)n * a.nchunk * 8 < (1ll << 31), "trunk_conv8_dgrad_bn: too many items");
+  const int nw = 4 * nblocks, full = n * a.nchunk, rem = full % nw;
+  a.nfull0 = full - rem;
+  if (rem > 0) a.nsplit = (int)std::max(1, std::min(std::min(nw / rem, 4), oh / 8 > 0 ? oh / 8 : 1));
+  hipStream_t s = as_stream(stream);
+  conv8_kernel<false, false, true, 2><<<nblocks, C8_NT, 0, s>>>(a);
+  MIA_LAUNCH_CHECK("trunk_conv8_dgrad_bn");
+  c8_red_final_kernel<<<32, 256, 0, s>>>(partial, nw, dgamma, dbeta);
+  MIA_LAUNCH_CHECK("trunk_conv8_dgrad_bn final");
   return 0;
 }

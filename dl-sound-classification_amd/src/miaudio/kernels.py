@@ -480,6 +480,27 @@ def trunk_conv8(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, n: int, h: in
     return (part, 4 * nblk) if stats else None
 
 
+def trunk_conv8_dgrad_bn(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, n: int, h: int, wd: int,
+                         bx: torch.Tensor, bn: BNState, tag: str | None = None):
+    """conv4 backward-data (dy (n*h*wd, 32) -> dx (n*(h+7)*(wd+7), 32), w the layout-1 flipped pack) with the
+    ReLU+BN backward sums of bn (input bx, dx's shape) formed in its epilogue: returns (dgamma, dbeta) as
+    bn_relu_bwd_reduce(dx, None, bx, ...) does."""
+    oh, ow = h + 7, wd + 7
+    assert dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dx.dtype == torch.bfloat16
+    assert bx.dtype == torch.bfloat16 and bx.numel() == dx.numel() and bx.is_contiguous()
+    assert dy.numel() == n * h * wd * 32 and w.numel() == 32 * 2048 and dx.numel() == n * oh * ow * 32
+    assert dy.is_contiguous() and w.is_contiguous() and dx.is_contiguous()
+    nblk = 256
+    part = workspace(4 * nblk * 64 * 4, dy.device, "c8red")
+    g = torch.empty(2, 32, dtype=torch.float32, device=dy.device)
+    with probe(tag or "", 2.0 * n * oh * ow * 32 * 2048, dy.numel() * 2 + dx.numel() * 2 + bx.numel() * 2):
+        L.check(L.load().mia_trunk_conv8_dgrad_bn(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nblk, n, h, wd,
+                                                  bx.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(),
+                                                  bn.mean.data_ptr(), bn.invstd.data_ptr(), g[0].data_ptr(),
+                                                  g[1].data_ptr(), part.data_ptr(), _s()), "mia_trunk_conv8_dgrad_bn")
+    return g[0], g[1]  # dgamma, dbeta
+
+
 def conv3_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, n: int, h: int, wd: int,
                 tag: str | None = None):
     """Weight gradient of EnvNet trunk conv3 (1 -> 32, 8x8), bf16: x (n, h, wd), dy (n*(h-7)*(wd-7), 32)

@@ -14,6 +14,7 @@ Reference op sequence: src/models/envnet_v2.py:14-85.
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
@@ -21,6 +22,8 @@ from ..miaudio import kernels as K
 from ..miaudio import lib as L
 
 _SEED = itertools.count(0x5EED)
+# A/B switch: conv4's backward-data without the fused ReLU+BN backward sums (a separate reduce pass)
+C8_BNSEP = os.environ.get("MIA_C8_BNSEP", "0") == "1"
 FC1_CHUNK_ROWS = 256  # rows of FC1's weight gradient per data-parallel all-reduce (256 x 84480 f32 = 86.5 MB)
 
 
@@ -393,6 +396,7 @@ class EnvNetFunction(torch.autograd.Function):
             dWb = torch.empty(cout2, Kb, dtype=torch.float32, device=dev)
             Pa = B * ha * wa
             da = torch.empty(Pa, cout, dtype=tdt, device=dev)
+            red = None  # (dgamma, dbeta) of bn_a when the backward-data kernel formed them
             if ts["act"] is not None:
                 # (1, 2) conv: shifted dY once, then wgrad and dgrad as two dense GEMMs
                 K.trunk_bwd_w2(dyb, ts["act"], B * ha, wa, cout2, cin2, wpk[pa + 4], dWb, da, wflip=wbk[(pa + 4, 1)],
@@ -405,7 +409,10 @@ class EnvNetFunction(torch.autograd.Function):
                 # dgrad b -> grad of relu(bn_a(ya)), then ReLU/BN backward
                 wbf = wbk[(pa + 4, 1)]
                 Kdb = kh2 * kw2 * cout2
-                if _use_conv8(cd, cin2, cout2, kh2, kw2):
+                if _use_conv8(cd, cin2, cout2, kh2, kw2) and not C8_BNSEP:
+                    # conv4: the ReLU+BN backward sums of bn_a come out of the backward-data epilogue
+                    red = K.trunk_conv8_dgrad_bn(dyb, wbf, da, B, hb, wb, ts["ya"], ts["bna"], tag=f"t{blk}b.dgrad")
+                elif _use_conv8(cd, cin2, cout2, kh2, kw2):
                     K.trunk_conv8(dyb, wbf, da, B, hb, wb, ph=kh2 - 1, pw=kw2 - 1, tag=f"t{blk}b.dgrad")
                 else:
                     K.gemm(K.conv(dyb, L.KC, B, hb, wb, cout2, ha, wa, kh2, kw2, ph=kh2 - 1, pw=kw2 - 1),
@@ -414,7 +421,7 @@ class EnvNetFunction(torch.autograd.Function):
             gwb = torch.empty_like(p[pa + 4])
             K.unpack_ohwi_grad(dWb, p[pa + 4].shape, gwb)
             grads[pa + 4] = gwb
-            dga, dba = K.bn_relu_bwd_reduce(da, None, ts["ya"], Pa, cout, ts["bna"])
+            dga, dba = red if red is not None else K.bn_relu_bwd_reduce(da, None, ts["ya"], Pa, cout, ts["bna"])
             grads[pa + 2], grads[pa + 3] = dga, dba
             dbias_a = torch.empty(cout, dtype=torch.float32, device=dev)
             K.bn_relu_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba, dbias_a)

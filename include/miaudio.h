@@ -331,6 +331,16 @@ int mia_trunk_conv8(const void* x, const float* pre_scale, const float* pre_shif
                     void* y, float* partial, int32_t nblocks, int32_t n, int32_t h, int32_t wd, int32_t ph, int32_t pw,
                     mia_stream_t stream);
 
+/* conv4 backward-data (mia_trunk_conv8 with x = dY (n, h, wd, 32), ph = pw = 7, w = layout-1 flipped weights ->
+ * dx (n, h+7, wd+7, 32)) fused with the ReLU+BN backward reductions of mia_bn_relu_bwd_reduce (replaces the
+ * BatchNorm2d + ReLU backward of src/models/envnet_v2.py:34-36 for conv3's BN): bx is that BN's input (the
+ * conv3 output, dx's shape), scale / shift / mean / invstd its batch statistics; dgamma[c] = sum dx*m*xhat,
+ * dbeta[c] = sum dx*m with m = [bx*scale + shift > 0], xhat = (bx - mean)*invstd, over the stored bf16 dx.
+ * partial: f32 [4*nblocks][32][2] workspace. */
+int mia_trunk_conv8_dgrad_bn(const void* dy, const void* w, void* dx, int32_t nblocks, int32_t n, int32_t h,
+                             int32_t wd, const void* bx, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, float* dgamma, float* dbeta, float* partial, mia_stream_t stream);
+
 /* Weight gradient of the EnvNet-v2 trunk conv3 (Conv2d(1, 32, (8, 8)), replaces the cuDNN backward-weight
  * of src/models/envnet_v2.py:31): dw[co][ky*8+kx] = sum dy[b][oy][ox][co] * x[b][oy+ky][ox+kx].  x bf16
  * (n, h, wd) (wd % 4 == 0, 8-byte aligned), dy bf16 (n, h-7, wd-7, 32) 16-byte aligned, dw f32 (32, 64);

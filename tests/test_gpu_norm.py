@@ -311,6 +311,37 @@ def test_trunk_conv8_dgrad(cuda, n, h, wd):
     assert rel(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("n,h,wd", [(2, 50, 846), (3, 3, 30), (1, 1, 1), (5, 17, 70)])
+def test_trunk_conv8_dgrad_bn_reduce(cuda, n, h, wd):
+    """conv4 backward-data with the ReLU+BN backward sums in its epilogue: dx bit-identical to the plain
+    backward-data kernel, (dgamma, dbeta) == mia_bn_relu_bwd_reduce over that dx and == float64 sums."""
+    g = torch.Generator(device=cuda).manual_seed(3 * h + wd + n)
+    dy = torch.randn(n, h, wd, 32, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(32, 32, 8, 8, generator=g, device=cuda) * 0.03
+    wf = K.pack_weight(W, L.BF16, 1)
+    P = n * (h + 7) * (wd + 7)
+    bx = (torch.randn(P, 32, generator=g, device=cuda) * 1.3 + 0.2).to(torch.bfloat16)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda) * 0.5
+    bn = K.bn_fwd_stats(bx, P, 32, gamma, beta, None, None, 0.1, 1e-5, True)
+    dx0 = torch.full((P, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    dx1 = torch.full((P, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    K.trunk_conv8(dy, wf, dx0, n, h, wd, ph=7, pw=7)
+    dg, db = K.trunk_conv8_dgrad_bn(dy, wf, dx1, n, h, wd, bx, bn)
+    rg, rb = K.bn_relu_bwd_reduce(dx0, None, bx, P, 32, bn)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0.view(torch.int16), dx1.view(torch.int16))
+    xd = bx.double()
+    m = (bx.float() * bn.scale + bn.shift > 0).double()
+    gd = dx0.double() * m
+    ref_b = gd.sum(0)
+    ref_g = (gd * (xd - bn.mean.double()) * bn.invstd.double()).sum(0)
+    tol_b = 1e-5 * dx0.double().abs().sum(0) + 1e-6
+    tol_g = 1e-5 * (gd * (xd - bn.mean.double()) * bn.invstd.double()).abs().sum(0) + 1e-6
+    for got, ref, tol in ((db, ref_b, tol_b), (dg, ref_g, tol_g), (rb, ref_b, tol_b), (rg, ref_g, tol_g)):
+        assert ((got.double() - ref).abs() <= tol).all(), (got.double() - ref).abs().max()
+
+
 @pytest.mark.parametrize("n,h,wd", [(2, 64, 860), (3, 9, 40), (1, 8, 12)])
 def test_conv3_wgrad(cuda, n, h, wd):
     """Wave-persistent conv3 (1 -> 32, 8x8) weight gradient vs float64 torch on the same bf16 operands."""
