@@ -361,7 +361,8 @@ def test_conv3_wgrad(cuda, n, h, wd):
 
 
 @pytest.mark.parametrize("n,h,w,kw,C", [(3, 1, 55102, 64, 64), (2, 1, 300, 64, 64), (2, 1, 70, 7, 64),
-                                        (2, 1, 64 * 130, 64, 64), (2, 10, 279, 2, 64), (2, 10, 139, 2, 128)])
+                                        (2, 1, 64 * 130, 64, 64), (2, 10, 279, 2, 64), (2, 10, 139, 2, 128),
+                                        (3, 1, 1000, 16, 64), (2, 1, 200, 72, 64), (4, 1, 16640 // 8, 64, 64)])
 def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     """One-pass maxpool-on-raw-winners + BN statistics (then relu(bn(winner))) == BN statistics pass +
     maxpool of relu(bn(x)); argmax equal wherever the pooled value is positive (elsewhere the routed
@@ -396,6 +397,12 @@ def test_pool_raw_stats_matches_pool_fwd(cuda, n, h, w, kw, C):
     assert (out1.float() - out2.float()).abs().max() <= 2e-2 * out2.float().abs().max()
     pos = out2 > 0
     assert torch.equal(am1[pos], am2[pos])
+    # every window: the first position of the max of sign(gamma) * x, and the raw value there, bit for bit
+    xw = x[:, :, :ow * kw].reshape(n, h, ow, kw, C)
+    ref_am = (xw.float() * torch.sign(gamma)).argmax(dim=3)
+    assert torch.equal(am1.long(), ref_am)
+    ref_win = torch.gather(xw, 3, ref_am.unsqueeze(3)).squeeze(3)
+    assert torch.equal(win.view(torch.int16), ref_win.view(torch.int16))
 
 
 @pytest.mark.parametrize("geom", [(2, 1, 640, 64, 1, 64), (3, 1, 1001, 64, 1, 64)])
