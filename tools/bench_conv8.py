@@ -34,6 +34,7 @@ libs = {"product": L.load()}
 for path in filter(None, os.environ.get("CONV8_LIBS", "").split(",")):
     lib = C.CDLL(str(REPO / path))
     lib.mia_trunk_conv8.argtypes = L.SIGNATURES["mia_trunk_conv8"][1]
+    lib.mia_trunk_conv8_dgrad_bn.argtypes = L.SIGNATURES["mia_trunk_conv8_dgrad_bn"][1]
     libs[Path(path).stem] = lib
 s = L.stream_ptr()
 
@@ -41,6 +42,17 @@ s = L.stream_ptr()
 def fwd(lib):
     L.check(lib.mia_trunk_conv8(x.data_ptr(), sc.data_ptr(), sh.data_ptr(), wp.data_ptr(), bias.data_ptr(),
                                 y.data_ptr(), part.data_ptr(), 256, B, H, W, 0, 0, s), "fwd")
+
+
+bxr = (torch.randn(B * H * W, 32, generator=g, device=dev) * 0.7).to(torch.bfloat16)
+bn = K.BNState(torch.zeros(32, device=dev), torch.ones(32, device=dev), sc, sh)
+gbeta = torch.empty(2, 32, device=dev)
+
+
+def dgrad_bn(lib):
+    L.check(lib.mia_trunk_conv8_dgrad_bn(dy.data_ptr(), wf.data_ptr(), dx.data_ptr(), 256, B, OH, OW, bxr.data_ptr(),
+                                         sc.data_ptr(), sh.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                         gbeta[0].data_ptr(), gbeta[1].data_ptr(), part.data_ptr(), s), "dgrad_bn")
 
 
 def dgrad(lib):
@@ -54,16 +66,20 @@ for name, lib in libs.items():
     dgrad(lib)
     torch.cuda.synchronize()
     got = (y.clone(), dx.clone(), part.clone())
+    dgrad_bn(lib)
+    torch.cuda.synchronize()
+    got += (dx.clone(), gbeta.clone())
     if ref is None:
         ref = got
     else:
         print(f"{name}: outputs {'equal to' if all(torch.equal(a, b) for a, b in zip(got, ref)) else 'DIFFER from'} "
               f"the product library's", flush=True)
 flop = 2.0 * B * OH * OW * 32 * 2048
-times = {(n, k): [] for n in libs for k in ("fwd", "dgrad")}
+KINDS = [("fwd", fwd), ("dgrad", dgrad), ("dgbn", dgrad_bn)]
+times = {(n, k): [] for n in libs for k, _ in KINDS}
 for _ in range(int(os.environ.get("ROUNDS", 3))):
     for name, lib in libs.items():
-        for kind, fn in (("fwd", fwd), ("dgrad", dgrad)):
+        for kind, fn in KINDS:
             fn(lib)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -74,5 +90,7 @@ for _ in range(int(os.environ.get("ROUNDS", 3))):
             torch.cuda.synchronize()
             times[(name, kind)].append(e0.elapsed_time(e1) / 10)
 for (name, kind), ts in times.items():
+    if not ts:
+        continue
     ms = min(ts)
     print(f"{name:16s} conv8.{kind:5s} {ms:7.3f} ms {flop / ms / 1e9:7.1f} TF/s", flush=True)
