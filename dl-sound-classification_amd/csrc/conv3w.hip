@@ -21,9 +21,16 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 struct W3Args {
   const bf16* x;   // (n, h, wd) 1-channel image
-  const bf16* dy;  // (n, h-7, wd-7, 32)
+  const bf16* dy;  // (n, h-7, wd-7, 32); BN: the gradient of relu(bn(ya)) (dA)
   float* part;     // [waves][32][64]
   int n, h, wd, oh, ow, nseg;
+  // BN (mia_conv3_wgrad_bn): dY = the ReLU+BN backward of dA (mia_bn_relu_bwd_apply's arithmetic), formed while
+  // staging, written to dyo and summed per channel into bpart [waves][32] (the conv bias gradient)
+  const bf16* ya;
+  bf16* dyo;
+  float* bpart;
+  const float *gamma, *scale, *shift, *mean, *invstd, *dgamma, *dbeta;
+  int64_t P;
 };
 
 __device__ __forceinline__ bf16x8 tr_frag(const char* p0, int stride) {
@@ -33,6 +40,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p0, int stride) {
   return __builtin_bit_cast(bf16x8, c);
 }
 
+template <bool BN>
 __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
   constexpr int ROWB = 80, CPYB = 704;  // 80-B rows (conflict-free staging writes), copies 704 B apart (48 banks: conflict-free reads)
   __shared__ __attribute__((aligned(16))) char strip[4][4 * CPYB];
@@ -48,7 +56,28 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
 
   // staging: lane l (l - 40 for l >= 40) loads input row l / 5, samples 8q .. 8q+11 (q = l % 5) as three 8-byte
   // loads (past the row end -> 0); every lane loads two 16-B dY chunks (px = q >> 2, 8 channels)
-  struct Raw { u32x2 v[3]; u32x4 d[2]; };
+  struct Raw { u32x2 v[3]; u32x4 d[2]; u32x4 y[BN ? 2 : 1]; uint32_t ok; };
+  // BN: per-channel constants as bn_bwd_apply_kernel<true> forms them (in LDS: registers would cost the
+  // kernel its occupancy), [scale, shift, gamma*invstd, mean, invstd, dbeta/P, dgamma/P][channel]
+  __shared__ __attribute__((aligned(16))) float bnp[7][32];
+  float bs1[8];
+  if constexpr (BN) {
+    if (threadIdx.x < 32) {
+      const int c = threadIdx.x;
+      const float invP = 1.f / (float)g.P;
+      const float is = g.invstd[c];
+      bnp[0][c] = g.scale[c];
+      bnp[1][c] = g.shift[c];
+      bnp[2][c] = (g.gamma ? g.gamma[c] : 1.f) * is;
+      bnp[3][c] = g.mean[c];
+      bnp[4][c] = is;
+      bnp[5][c] = g.dbeta[c] * invP;
+      bnp[6][c] = g.dgamma[c] * invP;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bs1[i] = 0.f;
+    __syncthreads();
+  }
   auto load = [&](int it) __attribute__((always_inline)) {
     Raw R;
     it = it < items ? it : items - 1;
@@ -63,19 +92,55 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
       const int c = col + 4 * k;
       R.v[k] = c + 4 <= g.wd ? *reinterpret_cast<const u32x2*>(src + c) : u32x2{0u, 0u};
     }
-    const bf16* drow = g.dy + ((int64_t)b * g.oh + oy) * g.ow * 32;
+    const int64_t drow = ((int64_t)b * g.oh + oy) * g.ow * 32;
+    R.ok = 0;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int qq = lane + 64 * s;
       const int px = seg * 32 + (qq >> 2);
-      R.d[s] = px < g.ow ? *reinterpret_cast<const u32x4*>(drow + (int64_t)px * 32 + (qq & 3) * 8)
-                         : u32x4{0u, 0u, 0u, 0u};
+      const int64_t off = drow + (int64_t)px * 32 + (qq & 3) * 8;
+      R.d[s] = px < g.ow ? *reinterpret_cast<const u32x4*>(g.dy + off) : u32x4{0u, 0u, 0u, 0u};
+      if constexpr (BN) R.y[s] = px < g.ow ? *reinterpret_cast<const u32x4*>(g.ya + off) : u32x4{0u, 0u, 0u, 0u};
+      R.ok |= (uint32_t)(px < g.ow) << s;
     }
+    (void)drow;
     return R;
   };
   const int i16 = lane & 15, gq = lane >> 4, h = lane >> 5;
   const int n = lane & 31;  // tap within an N tile: ky = 4*nt + (n >> 3), kx = n & 7
-  auto run = [&](const Raw& R) __attribute__((always_inline)) {
+  // BN: dY chunk s of item `it` from dA and ya (zero past the row end), stored to dyo and summed
+  auto bn_chunk = [&](const Raw& R, int s, int it) __attribute__((always_inline)) -> u32x4 {
+    if (!((R.ok >> s) & 1u)) return u32x4{0u, 0u, 0u, 0u};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t dw = R.d[s][k], yw = R.y[s][k];
+      float gv[2] = {__uint_as_float(dw << 16), __uint_as_float(dw & 0xffff0000u)};
+      const float xv[2] = {__uint_as_float(yw << 16), __uint_as_float(yw & 0xffff0000u)};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = 2 * k + j, c = (lane & 3) * 8 + i;
+        gv[j] = fmaf(xv[j], bnp[0][c], bnp[1][c]) > 0.f ? gv[j] : 0.f;
+        gv[j] = bnp[2][c] * (gv[j] - bnp[5][c] - (xv[j] - bnp[3][c]) * bnp[4][c] * bnp[6][c]);
+        bs1[i] += gv[j];
+      }
+      const bf16 lo = (bf16)gv[0], hi = (bf16)gv[1];
+      o[k] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    }
+    const int seg = it % g.nseg, rest = it / g.nseg;
+    const int oy = rest % g.oh, b = rest / g.oh;
+    const int qq = lane + 64 * s;
+    const int px = seg * 32 + (qq >> 2);
+    const u32x4 v = {o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<u32x4*>(g.dyo + (((int64_t)b * g.oh + oy) * g.ow + px) * 32 + (qq & 3) * 8) = v;
+    return v;
+  };
+  auto run = [&](const Raw& R, int it) __attribute__((always_inline)) {
+    u32x4 dv[2] = {R.d[0], R.d[1]};
+    if constexpr (BN) {
+      dv[0] = bn_chunk(R, 0, it);
+      dv[1] = bn_chunk(R, 1, it);
+    }
     wave_sync();  // the previous item's fragment reads are done (common.h)
     if (lane < 40) {  // lanes 40..63 hold duplicates: writing them too cost LDS cycles (0.355 -> 0.292 ms)
       const int l = lane;
@@ -96,7 +161,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int qq = lane + 64 * s;
-      *reinterpret_cast<u32x4*>(dt + (qq >> 2) * 64 + (qq & 3) * 16) = R.d[s];
+      *reinterpret_cast<u32x4*>(dt + (qq >> 2) * 64 + (qq & 3) * 16) = dv[s];
     }
     wave_sync();
     const int kx = n & 7, cp = kx & 3;
@@ -123,11 +188,11 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
     Raw ra = load(it), rb;
     for (;;) {
       rb = load(it + nw);
-      run(ra);
+      run(ra, it);
       it += nw;
       if (it >= items) break;
       ra = load(it + nw);
-      run(rb);
+      run(rb, it);
       it += nw;
       if (it >= items) break;
     }
@@ -141,6 +206,23 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
       const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
       dst[co * 64 + nt * 32 + n] = acc[nt][r];
     }
+  if constexpr (BN) {
+    // lanes with equal lane & 3 hold the same channels
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int m = 4; m < 64; m <<= 1) bs1[i] += __shfl_xor(bs1[i], m, 64);
+    if (lane < 4) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g.bpart[(int64_t)gw * 32 + lane * 8 + i] = bs1[i];
+    }
+  }
+}
+
+// dbias[c] = sum over the waves' partials (f64, fixed order)
+__global__ void conv3_bias_final_kernel(const float* __restrict__ bpart, int nw, float* __restrict__ dbias) {
+  const double s = block_sum_strided(bpart + blockIdx.x, nw, 32);
+  if (threadIdx.x == 0) dbias[blockIdx.x] = (float)s;
 }
 
 // dw[e] = sum of the slabs (fixed order, bit-reproducible), e = co*64 + tap, in two coalesced stages:
@@ -176,11 +258,43 @@ extern "C" int mia_conv3_wgrad(const void* x, const void* dy, float* dw, float* 
            (int)cdiv(wd - 7, 32)};
   MIA_CHECK_ARG((int64_t)n * a.oh * a.nseg < (1ll << 31), "conv3_wgrad: too many items");
   hipStream_t s = as_stream(stream);
-  conv3_wgrad_kernel<<<nwaves / 4, 256, 0, s>>>(a);
+  conv3_wgrad_kernel<false><<<nwaves / 4, 256, 0, s>>>(a);
   MIA_LAUNCH_CHECK("conv3_wgrad");
   double* tmp = reinterpret_cast<double*>(part + (int64_t)nwaves * 2048);
   conv3_wgrad_reduce1_kernel<<<dim3(8, C3_G), 256, 0, s>>>(part, nwaves, tmp);
   conv3_wgrad_reduce2_kernel<<<8, 256, 0, s>>>(tmp, dw);
   MIA_LAUNCH_CHECK("conv3_wgrad_reduce");
+  return 0;
+}
+
+extern "C" int64_t mia_conv3_wgrad_workspace_bytes(int32_t nwaves) {
+  return (int64_t)nwaves * 2048 * 4 + (int64_t)C3_G * 2048 * 8 + (int64_t)nwaves * 32 * 4;
+}
+
+extern "C" int mia_conv3_wgrad_bn(const void* x, const void* da, const void* ya, void* dy, float* dw, float* dbias,
+                                  float* part, int32_t nwaves, int32_t n, int32_t h, int32_t wd, const float* gamma,
+                                  const float* scale, const float* shift, const float* mean, const float* invstd,
+                                  const float* dgamma, const float* dbeta, mia_stream_t stream) {
+  MIA_CHECK_ARG(x && da && ya && dy && dw && dbias && part && n > 0 && h >= 8 && wd >= 8,
+                "conv3_wgrad_bn: bad arguments");
+  MIA_CHECK_ARG(scale && shift && mean && invstd && dgamma && dbeta, "conv3_wgrad_bn: null BN statistics");
+  MIA_CHECK_ARG(nwaves > 0 && nwaves % 4 == 0, "conv3_wgrad_bn: nwaves must be a positive multiple of 4");
+  MIA_CHECK_ARG(wd % 4 == 0, "conv3_wgrad_bn: image width must be a multiple of 4 (8-byte row alignment)");
+  MIA_CHECK_ARG(((reinterpret_cast<uintptr_t>(da) | reinterpret_cast<uintptr_t>(ya) | reinterpret_cast<uintptr_t>(dy)) &
+                 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0,
+                "conv3_wgrad_bn: da / ya / dy must be 16-byte and x 8-byte aligned");
+  W3Args a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(da), part, n, h, wd, h - 7, wd - 7,
+           (int)cdiv(wd - 7, 32), reinterpret_cast<const bf16*>(ya), reinterpret_cast<bf16*>(dy), nullptr,
+           gamma, scale, shift, mean, invstd, dgamma, dbeta, (int64_t)n * (h - 7) * (wd - 7)};
+  MIA_CHECK_ARG((int64_t)n * a.oh * a.nseg < (1ll << 31), "conv3_wgrad_bn: too many items");
+  double* tmp = reinterpret_cast<double*>(part + (int64_t)nwaves * 2048);
+  a.bpart = reinterpret_cast<float*>(tmp + (int64_t)C3_G * 2048);
+  hipStream_t s = as_stream(stream);
+  conv3_wgrad_kernel<true><<<nwaves / 4, 256, 0, s>>>(a);
+  MIA_LAUNCH_CHECK("conv3_wgrad_bn");
+  conv3_wgrad_reduce1_kernel<<<dim3(8, C3_G), 256, 0, s>>>(part, nwaves, tmp);
+  conv3_wgrad_reduce2_kernel<<<8, 256, 0, s>>>(tmp, dw);
+  conv3_bias_final_kernel<<<32, 256, 0, s>>>(a.bpart, nwaves, dbias);
+  MIA_LAUNCH_CHECK("conv3_wgrad_bn reduce");
   return 0;
 }

@@ -516,6 +516,28 @@ def conv3_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, n: int, h: 
                                          _s()), "mia_conv3_wgrad")
 
 
+def conv3_wgrad_bn(x: torch.Tensor, da: torch.Tensor, ya: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor,
+                   dbias: torch.Tensor, n: int, h: int, wd: int, gamma, bn: BNState, dgamma, dbeta,
+                   tag: str | None = None):
+    """conv3_wgrad with dY formed from the ReLU+BN backward of conv3's BN while staging: dy = the
+    bn_relu_bwd_apply of da (gradient of relu(bn(ya))) -- written out (may be da itself) -- and dbias its
+    column sum, in the same pass as the weight gradient dw."""
+    oh, ow = h - 7, wd - 7
+    for t in (da, ya, dy):
+        assert t.dtype == torch.bfloat16 and t.numel() == n * oh * ow * 32 and t.is_contiguous()
+    assert x.dtype == torch.bfloat16 and x.numel() == n * h * wd and x.is_contiguous()
+    assert dw.dtype == torch.float32 and dw.numel() == 32 * 64 and dbias.dtype == torch.float32 and dbias.numel() == 32
+    nw = 4096
+    lib = L.load()
+    part = workspace(int(lib.mia_conv3_wgrad_workspace_bytes(nw)), x.device, "conv3w")
+    with probe(tag or "", 2.0 * n * oh * ow * 32 * 64, x.numel() * 2 + da.numel() * 6):
+        L.check(lib.mia_conv3_wgrad_bn(x.data_ptr(), da.data_ptr(), ya.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+                                       dbias.data_ptr(), part.data_ptr(), nw, n, h, wd, L.ptr(gamma),
+                                       bn.scale.data_ptr(), bn.shift.data_ptr(), bn.mean.data_ptr(),
+                                       bn.invstd.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _s()),
+                "mia_conv3_wgrad_bn")
+
+
 def bn_finalize_shifted(partial: torch.Tensor, nblk: int, P: int, C: int, kshift: torch.Tensor, gamma, beta,
                         running_mean, running_var, momentum: float, eps: float) -> BNState:
     """Training-mode BN statistics from shifted partial sums (mia_bn_finalize_shifted)."""

@@ -110,6 +110,8 @@ SIGNATURES = {
     "mia_pool_raw_stats": (C.c_int, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp]),
     "mia_pool_apply": (C.c_int, [vp, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp]),
     "mia_conv3_wgrad": (C.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "mia_conv3_wgrad_workspace_bytes": (C.c_int64, [i32]),
+    "mia_conv3_wgrad_bn": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mia_trunk_conv8": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "mia_trunk_conv8_dgrad_bn": (C.c_int, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mia_bn_finalize_shifted": (C.c_int, [vp, i32, i64, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, i32, vp, vp, vp,

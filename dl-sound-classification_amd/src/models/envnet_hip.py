@@ -24,6 +24,8 @@ from ..miaudio import lib as L
 _SEED = itertools.count(0x5EED)
 # A/B switch: conv4's backward-data without the fused ReLU+BN backward sums (a separate reduce pass)
 C8_BNSEP = os.environ.get("MIA_C8_BNSEP", "0") == "1"
+# A/B switch: conv3's ReLU+BN backward as its own pass instead of inside the conv3 weight-gradient kernel
+C3_BNSEP = os.environ.get("MIA_C3_BNSEP", "0") == "1"
 FC1_CHUNK_ROWS = 256  # rows of FC1's weight gradient per data-parallel all-reduce (256 x 84480 f32 = 86.5 MB)
 
 
@@ -424,18 +426,27 @@ class EnvNetFunction(torch.autograd.Function):
             dga, dba = red if red is not None else K.bn_relu_bwd_reduce(da, None, ts["ya"], Pa, cout, ts["bna"])
             grads[pa + 2], grads[pa + 3] = dga, dba
             dbias_a = torch.empty(cout, dtype=torch.float32, device=dev)
-            K.bn_relu_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba, dbias_a)
             grads[pa + 1] = dbias_a
             dya = da
-            # wgrad a
             Ka = kh * kw * cin
             dWa = torch.empty(cout, Ka, dtype=torch.float32, device=dev)
             dense_w2 = ts["act"] is not None
-            if dense_w2:
+            c3w = cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0
+            if c3w and not C3_BNSEP:
+                # conv3: the ReLU+BN backward applied while the weight-gradient kernel stages dY (in place)
+                K.conv3_wgrad_bn(ts["inp"], da, ts["ya"], da, dWa, dbias_a, B, H, W, bns[2 + 2 * blk].weight,
+                                 ts["bna"], dga, dba, tag=f"t{blk}a.wgrad")
+            else:
+                K.bn_relu_bwd_apply(da, ts["ya"], da, Pa, cout, bns[2 + 2 * blk].weight, ts["bna"], dga, dba,
+                                    dbias_a)
+            # wgrad a
+            if c3w and not C3_BNSEP:
+                pass  # formed above
+            elif dense_w2:
                 dinp = torch.empty(B * H * W, cin, dtype=tdt, device=dev)
                 K.trunk_bwd_w2(dya, ts["inp"].reshape(B * H * W, cin), B * H, W, cout, cin, wpk[pa],
                                dWa, dinp, tag=f"t{blk}a", wflip=wbk[(pa, 1)])
-            elif cin == 1 and cd == L.BF16 and kh == 8 and kw == 8 and cout == 32 and W % 4 == 0:
+            elif c3w:
                 # conv3 weight gradient: wave-persistent, dY read once (csrc/conv3w.hip)
                 K.conv3_wgrad(ts["inp"], dya, dWa, B, H, W, tag=f"t{blk}a.wgrad")
             else:

@@ -348,6 +348,17 @@ int mia_trunk_conv8_dgrad_bn(const void* dy, const void* w, void* dx, int32_t nb
 int mia_conv3_wgrad(const void* x, const void* dy, float* dw, float* part, int32_t nwaves, int32_t n, int32_t h,
                     int32_t wd, mia_stream_t stream);
 
+/* mia_conv3_wgrad with the ReLU+BN backward of conv3's BN (BatchNorm2d + ReLU of src/models/envnet_v2.py:31-33;
+ * mia_bn_relu_bwd_apply's arithmetic) formed while staging dY: dy = BN backward of da (the gradient of
+ * relu(ya*scale + shift)), gamma, mean, invstd, dgamma, dbeta as mia_bn_relu_bwd_apply takes them, is written
+ * to dy (n, h-7, wd-7, 32) bf16 (may alias da) and summed per channel into dbias f32 (32).  da, ya, dy 16-byte
+ * aligned; part: f32 workspace of mia_conv3_wgrad_workspace_bytes(nwaves) bytes, 8-byte aligned. */
+int64_t mia_conv3_wgrad_workspace_bytes(int32_t nwaves);
+int mia_conv3_wgrad_bn(const void* x, const void* da, const void* ya, void* dy, float* dw, float* dbias, float* part,
+                       int32_t nwaves, int32_t n, int32_t h, int32_t wd, const float* gamma, const float* scale,
+                       const float* shift, const float* mean, const float* invstd, const float* dgamma,
+                       const float* dbeta, mia_stream_t stream);
+
 /* BatchNorm finalize from per-block shifted sums partial[nblk][C][2] about kshift[c]: writes mean,
  * invstd, the fused scale/shift (gamma*invstd, beta - mean*gamma*invstd) and updates the running
  * statistics (momentum, unbiased variance) exactly as mia_bn_fwd_stats.  Training mode only. */

@@ -343,6 +343,36 @@ def test_trunk_conv8_dgrad_bn_reduce(cuda, n, h, wd):
 
 
 @pytest.mark.parametrize("n,h,wd", [(2, 64, 860), (3, 9, 40), (1, 8, 12)])
+def test_conv3_wgrad_bn_equals_apply_then_wgrad(cuda, n, h, wd):
+    """conv3 weight gradient with the ReLU+BN backward formed while staging dY (in place) == the separate
+    bn_relu_bwd_apply pass followed by conv3_wgrad: dY and dW bit-identical, the bias gradient to f32 order."""
+    g = torch.Generator(device=cuda).manual_seed(h * 5 + wd + n)
+    x = torch.randn(n, h, wd, generator=g, device=cuda).to(torch.bfloat16)
+    oh, ow = h - 7, wd - 7
+    P = n * oh * ow
+    da = torch.randn(P, 32, generator=g, device=cuda).to(torch.bfloat16)
+    ya = (torch.randn(P, 32, generator=g, device=cuda) * 1.2 + 0.1).to(torch.bfloat16)
+    gamma = torch.rand(32, generator=g, device=cuda) + 0.5
+    beta = torch.randn(32, generator=g, device=cuda) * 0.5
+    bn = K.bn_fwd_stats(ya, P, 32, gamma, beta, None, None, 0.1, 1e-5, True)
+    dg, db = K.bn_relu_bwd_reduce(da, None, ya, P, 32, bn)
+    dy0 = torch.empty_like(da)
+    db0 = torch.empty(32, device=cuda)
+    K.bn_relu_bwd_apply(da, ya, dy0, P, 32, gamma, bn, dg, db, db0)
+    dw0 = torch.full((32, 64), float("nan"), device=cuda)
+    K.conv3_wgrad(x, dy0, dw0, n, h, wd)
+    dy1 = da.clone()
+    dw1 = torch.full((32, 64), float("nan"), device=cuda)
+    db1 = torch.full((32,), float("nan"), device=cuda)
+    K.conv3_wgrad_bn(x, dy1, ya, dy1, dw1, db1, n, h, wd, gamma, bn, dg, db)
+    torch.cuda.synchronize()
+    assert torch.equal(dy0.view(torch.int16), dy1.view(torch.int16))
+    assert torch.equal(dw0, dw1)
+    tol = 1e-5 * dy0.float().abs().sum(0) + 1e-6
+    assert ((db0 - db1).abs() <= tol).all(), (db0 - db1).abs().max()
+
+
+@pytest.mark.parametrize("n,h,wd", [(2, 64, 860), (3, 9, 40), (1, 8, 12)])
 def test_conv3_wgrad(cuda, n, h, wd):
     """Wave-persistent conv3 (1 -> 32, 8x8) weight gradient vs float64 torch on the same bf16 operands."""
     g = torch.Generator(device=cuda).manual_seed(h * 7 + wd + n)
