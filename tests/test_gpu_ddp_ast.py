@@ -50,14 +50,18 @@ def _worker(rank, world, port, compute, q):
             probs = m(spec)
             _, dprobs, _ = K.soft_ce(probs, y, input_sigmoid=False)
             probs.backward(dprobs)
+            return spec.detach().clone(), probs.detach().clone()
 
         step()  # warm-up
         m.zero_grad(set_to_none=True)
-        step()
+        s1, o1 = step()
         plain = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         m.zero_grad(set_to_none=True)
-        step()  # the same step again: the plain gradients must be bit-reproducible (else nothing below can hold)
+        s2, o2 = step()  # the same step again: the plain gradients must be bit-reproducible (else nothing below can hold)
         nondet = [n for n, p in m.named_parameters() if not torch.equal(p.grad, plain[n])]
+        if nondet:  # where it starts: the input spectrogram, the forward output, or the backward only
+            nondet = [f"{len(nondet)} of {len(plain)} differ; spec equal {torch.equal(s1, s2)}, "
+                      f"probs equal {torch.equal(o1, o2)}; last: {nondet[-3:]}"] + nondet
         m.zero_grad(set_to_none=True)
         same_init = []
         for n, p in m.named_parameters():  # identical initial weights on both ranks (the reducer broadcasts rank 0's)

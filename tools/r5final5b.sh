@@ -1,3 +1,3 @@
 set -o pipefail
-export PTAG=r5final4
+export PTAG=r5final5
 LEGS="envnet" bash tools/gpu_profile.sh
