@@ -374,11 +374,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy,
                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                                     void* dx, int dxdt, int accumulate, float* __restrict__ partial,
                                                     int64_t rows, int D, int rows_per_block) {
-  // partial layout: [gridDim.x][2][D] (dgamma, dbeta) accumulated by each block in LDS
-  __shared__ float pg[2][1024];
+  // partial layout: [gridDim.x][2][D] (dgamma, dbeta): each wave's sums staged in LDS, added in wave order
+  // (fixed order: an LDS atomicAdd of the four waves' sums made dgamma / dbeta differ from run to run)
+  __shared__ float pw[NT / 64][2][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 2 * D; i += NT) pg[i / D][i % D] = 0.f;
-  __syncthreads();
   float ag[PER], ab[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
@@ -418,10 +417,16 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const void* __restrict__ dy,
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int d = lane + 64 * i;
-    if (d < D) { atomicAdd(&pg[0][d], ag[i]); atomicAdd(&pg[1][d], ab[i]); }
+    if (d < D) { pw[wave][0][d] = ag[i]; pw[wave][1][d] = ab[i]; }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * D; i += NT) partial[(int64_t)blockIdx.x * 2 * D + i] = pg[i / D][i % D];
+  for (int i = threadIdx.x; i < 2 * D; i += NT) {
+    const int q = i / D, d = i % D;
+    float a = pw[0][q][d];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) a += pw[w][q][d];
+    partial[(int64_t)blockIdx.x * 2 * D + i] = a;
+  }
 }
 
 // Vectorised LayerNorm backward for D = 64*PER (PER % 4 == 0): lane owns PER contiguous features

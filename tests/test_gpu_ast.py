@@ -113,7 +113,7 @@ def test_attention_running_max_paths(cuda, profile):
         assert rel(dqkv[i], ref) < 1.2e-1, ("dq", "dk", "dv")[i]
 
 
-@pytest.mark.parametrize("D", [768, 384])
+@pytest.mark.parametrize("D", [768, 384, 1000])
 def test_layernorm(cuda, D):
     from src.models.ast_hip import _ln, _ln_bwd
     g = torch.Generator().manual_seed(D)
@@ -129,7 +129,11 @@ def test_layernorm(cuda, D):
     yo, m, r, _ = _ln(tx, tw, tb, torch.float32, 300, D)
     dx = torch.ones(300, D, device=cuda)
     dg, db, cs = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx, 300, D, True)
+    dx2 = torch.ones(300, D, device=cuda)
+    dg2, db2, _ = _ln_bwd(dy.to(cuda), tx, tw, m, r, dx2, 300, D, True)
     torch.cuda.synchronize()
+    # reproducible bit for bit (both the vectorised D = 768 kernel and the generic one)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2) and torch.equal(dx, dx2)
     assert cs is None
     assert rel(yo, y) < 1e-5
     assert rel(dx - 1.0, xr.grad) < 1e-4
