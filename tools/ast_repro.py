@@ -1,0 +1,72 @@
+"""Reproducibility probe of the plain AST training step (the setting of tests/test_gpu_ddp_ast.py, one process):
+the same step K times; reports every repetition whose input spectrogram, output or parameter gradients differ
+from the first, with the first differing parameters and NaN counts.
+    python tools/ast_repro.py [K] [bf16|fp8]"""
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "dl-sound-classification_amd"))
+sys.path.insert(0, str(REPO))
+import torch  # noqa: E402
+
+from oracle.synth import synth_waveform  # noqa: E402
+from src.datasets.augment import spec_augment_mixup  # noqa: E402
+from src.datasets.features import GpuLogMel  # noqa: E402
+from src.miaudio import kernels as K  # noqa: E402
+from src.models.ast import ASTModel  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+compute = sys.argv[2] if len(sys.argv) > 2 else "bf16"
+dev = torch.device("cuda", 0)
+torch.manual_seed(42)
+m = ASTModel(num_classes=10, depth=2, compute_dtype=compute).to(dev).train()
+B = 8
+wav = torch.from_numpy(synth_waveform(71, B, 220_500)).to(dev)
+labels = torch.tensor([(3 * i) % 10 for i in range(B)], device=dev)
+logmel = GpuLogMel(44_100, 128, True, 0.0, 0.5)
+g = torch.Generator(device=dev)
+
+
+def step():
+    g.manual_seed(1234)
+    raw = logmel(wav)
+    raw_c = raw.clone()
+    again = logmel(wav)  # the same call back to back: differs only if log-mel itself is not reproducible
+    if not torch.equal(again, raw_c):
+        d = again != raw_c
+        print(f"  back-to-back log-mel calls differ: {int(d.sum())} values, max |diff| "
+              f"{float((again - raw_c).abs().max()):.3g}", flush=True)
+    del again
+    spec, y = spec_augment_mixup(raw, labels, 10, 192, 48, 0.5, 0.25, gen=g)
+    spec_c = spec.clone()
+    probs = m(spec)
+    spec_f = spec.clone()
+    _, dprobs, _ = K.soft_ce(probs, y, input_sigmoid=False)
+    probs.backward(dprobs)
+    out = ((raw_c, spec_c, spec_f, spec.detach().clone(), y.clone()), probs.detach().clone(),
+           {n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    m.zero_grad(set_to_none=True)
+    return out
+
+
+step()
+s0, o0, g0 = step()
+bad = 0
+for r in range(reps):
+    s1, o1, g1 = step()
+    diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    seq = [torch.equal(a, b) for a, b in zip(s0, s1)]
+    if diff or not all(seq) or not torch.equal(o0, o1):
+        bad += 1
+        nan = {n: int(torch.isnan(g1[n]).sum()) for n in diff[:3]}
+        if not seq[0]:
+            d = s0[0] != s1[0]
+            idx = d.nonzero()
+            print(f"  logmel: {int(d.sum())} of {d.numel()} differ, clips {sorted(set(idx[:, 0].tolist()))}, mels "
+                  f"{idx[:, 1].min().item()}..{idx[:, 1].max().item()}, frames {idx[:, 2].min().item()}.."
+                  f"{idx[:, 2].max().item()}, max |diff| {float((s0[0] - s1[0]).abs().max()):.3g}", flush=True)
+        print(f"rep {r}: equal logmel / augmented / after fwd / after bwd / targets {seq}, "
+              f"probs equal {torch.equal(o0, o1)}, "
+              f"{len(diff)} grads differ, first {diff[:4]}, last {diff[-3:]}, nan {nan}", flush=True)
+print(f"ast_repro {compute}: {bad} of {reps} repetitions differ", flush=True)
