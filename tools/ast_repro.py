@@ -26,17 +26,49 @@ wav = torch.from_numpy(synth_waveform(71, B, 220_500)).to(dev)
 labels = torch.tensor([(3 * i) % 10 for i in range(B)], device=dev)
 logmel = GpuLogMel(44_100, 128, True, 0.0, 0.5)
 g = torch.Generator(device=dev)
+FRAMES = 1 + 220_500 // 160
+NBM = None
+
+
+def _ws():
+    global NBM
+    from src.miaudio import lib as L
+    lib = L.load()
+    nbytes = int(lib.mia_logmel_workspace_bytes(B, FRAMES))
+    if NBM is None:  # B * nbm * 4 + 16 + B * 16 * 2 * 8 + 16 = nbytes
+        NBM = (nbytes - 32 - B * 256) // (4 * B)
+    return K.workspace(nbytes, dev, "logmel")[:nbytes]
 
 
 def step():
     g.manual_seed(1234)
     raw = logmel(wav)
     raw_c = raw.clone()
+    ws1 = _ws().clone()
     again = logmel(wav)  # the same call back to back: differs only if log-mel itself is not reproducible
+    ws2 = _ws().clone()
     if not torch.equal(again, raw_c):
         d = again != raw_c
         print(f"  back-to-back log-mel calls differ: {int(d.sum())} values, max |diff| "
               f"{float((again - raw_c).abs().max()):.3g}", flush=True)
+        frames = raw.shape[2]
+        nbm = -(-frames // 32) if False else None
+        bm1, bm2 = ws1[:B * NBM * 4].view(torch.float32).view(B, NBM), ws2[:B * NBM * 4].view(torch.float32).view(B, NBM)
+        off = -(-(B * NBM * 4) // 16) * 16
+        p1 = ws1[off:off + B * 16 * 16].view(torch.float64).view(B, 16, 2)
+        p2 = ws2[off:off + B * 16 * 16].view(torch.float64).view(B, 16, 2)
+        db = (bm1 != bm2).nonzero().tolist()
+        dp = (p1 != p2).nonzero().tolist()
+        print(f"  blockmax entries differing (clip, chunk): {db[:8]}; values {[(bm1[c, k].item(), bm2[c, k].item()) for c, k in db[:3]]}",
+              flush=True)
+        print(f"  partial entries differing (clip, part, q): {dp[:8]}; values "
+              f"{[(p1[c, k, q].item(), p2[c, k, q].item()) for c, k, q in dp[:3]]}", flush=True)
+        # the fft_mel_db output itself: recompute the clip's max from the un-normalised values is not possible
+        # here (normalised in place), so compare the two outputs' per-clip means / stds
+        for c in sorted(set(d.nonzero()[:, 0].tolist())):
+            print(f"  clip {c}: mean {raw_c[c].mean().item():.6f} / {again[c].mean().item():.6f}, "
+                  f"std {raw_c[c].std().item():.6f} / {again[c].std().item():.6f}, min {raw_c[c].min().item():.5f} / "
+                  f"{again[c].min().item():.5f}", flush=True)
     del again
     spec, y = spec_augment_mixup(raw, labels, 10, 192, 48, 0.5, 0.25, gen=g)
     spec_c = spec.clone()
