@@ -40,13 +40,22 @@ def _ws():
     return K.workspace(nbytes, dev, "logmel")[:nbytes]
 
 
+WSUM = wav.double().sum(1)
+WBITS = wav.clone()
+
+
 def step():
     g.manual_seed(1234)
+    if not torch.equal(wav, WBITS):
+        print(f"  waveform changed before the step: rows {(wav != WBITS).any(1).nonzero().flatten().tolist()}", flush=True)
     raw = logmel(wav)
     raw_c = raw.clone()
     ws1 = _ws().clone()
     again = logmel(wav)  # the same call back to back: differs only if log-mel itself is not reproducible
     ws2 = _ws().clone()
+    if not torch.equal(wav, WBITS):
+        print(f"  waveform changed around the log-mel calls: rows {(wav != WBITS).any(1).nonzero().flatten().tolist()}",
+              flush=True)
     if not torch.equal(again, raw_c):
         d = again != raw_c
         print(f"  back-to-back log-mel calls differ: {int(d.sum())} values, max |diff| "
