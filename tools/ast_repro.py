@@ -24,7 +24,8 @@ m = ASTModel(num_classes=10, depth=2, compute_dtype=compute).to(dev).train()
 B = 8
 wav = torch.from_numpy(synth_waveform(71, B, 220_500)).to(dev)
 labels = torch.tensor([(3 * i) % 10 for i in range(B)], device=dev)
-logmel = GpuLogMel(44_100, 128, True, 0.0, 0.5)
+import os  # noqa: E402
+logmel = GpuLogMel(44_100, 128, os.environ.get("LOGMEL_NORM", "1") == "1", 0.0, 0.5)  # LOGMEL_NORM=0: no per-clip stats
 g = torch.Generator(device=dev)
 FRAMES = 1 + 220_500 // 160
 NBM = None
