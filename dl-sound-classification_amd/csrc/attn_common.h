@@ -246,11 +246,19 @@ typedef const __attribute__((address_space(1))) void* glb_vp;
 // every LDS location and puts vmcnt(0) in front of the next ds_read -- in these kernels the NEXT tile's
 // DMA, so every tile waited for its successor's load.  Here the kernels' own counted vmcnt + barrier
 // order the DMA against its readers (each issue site says which), and M0 is saved and restored.
+// The wait states the compiler pads around its own LDS-DMA are written into the string, since nothing inside
+// an asm statement is padded (gfx9 manually-inserted wait states):
+//  * s_nop 0 between the M0 write and the buffer_load ... lds that reads it (SALU writes M0 -> LDS-DMA: 1 state;
+//    the builtin form emits exactly this nop).  Without it the DMA may take the PREVIOUS M0 -- `keep`, the
+//    value this statement restores -- and write its 1 KB to a stale LDS address;
+//  * s_nop 4 opening the string: the descriptor / soffset SGPRs may come from a v_readfirstlane the compiler
+//    placed just before (VALU writes SGPR -> VMEM reads that SGPR: 5 states).
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, const void* lds, unsigned voff, unsigned soff) {
   const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_vp)lds);
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "s"(a), "v"(voff), "s"(rsrc), "s"(soff)
       : "memory");

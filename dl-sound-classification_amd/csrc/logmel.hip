@@ -36,7 +36,7 @@ constexpr int NC = 512;         // complex FFT size
 constexpr int HOP = 160;
 constexpr int WIN = 400;
 constexpr int NMEL_MAX = 128;
-constexpr int SEG = (FB - 1) * HOP + WIN;  // 5360 samples
+constexpr int SEG = (FB - 1) * HOP + WIN;  // 2800 samples
 constexpr int SPT = (SEG + LNT - 1) / LNT;  // segment samples per thread
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -80,6 +80,56 @@ __device__ __forceinline__ void dft8(f2 (&v)[8]) {
 __device__ __forceinline__ int swz(int i) { return i ^ ((i >> 3) & 7); }
 
 
+// Hand-off between the FFT stages of one wave through its own LDS buffer: every LDS operation of this wave has
+// completed (lgkmcnt(0)) before the next is issued.  One wave's LDS operations execute in order, so the wave
+// barrier alone already orders them; the drain makes each hand-off independent of that ordering and of any
+// interruption of the wave between a stage's writes and the next stage's reads.
+__device__ __forceinline__ void lds_handoff() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Sum over the 64 lanes, the same value in every lane and in every call (fixed order): DPP butterflies inside
+// each 16-lane row (xor 1, xor 2, half-row mirror, row mirror), then the four row sums by readlane.
+template <int CTRL> __device__ __forceinline__ float dpp_row_add(float v) {
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_row_add<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_row_add<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_row_add<0x141>(v);  // row_half_mirror
+  v = dpp_row_add<0x140>(v);  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// Per-frame self-check of the FFT (x = the 400 windowed samples at n = 0..399 of the 1024-point frame, X its DFT,
+// P_k = |X_k|^2, F = sum_{k<1024} P_k = P_0 + P_512 + 2 sum_{k=1..511} P_k):
+//  * Parseval: F = 1024 sum_n x_n^2;
+//  * a checksum that must vanish: sum_{k<1024} (-1)^k P_k = 1024 sum_n x_n x_{(n + 512) mod 1024} = 0 (the
+//    circular autocorrelation at lag 512 of a frame that is zero past n = 399).
+// Both read only the power spectrum the band loop uses, so they cost no registers across the FFT.  f32 rounding
+// measured on 2 400 windowed frames (noise, tones, chirps, DC, sparse, 1e4-loud; scipy single precision):
+// Parseval <= 3.3e-7 relative, |checksum| <= 1.7e-7 F; the bounds leave two orders of magnitude for the
+// radix-8 Stockham's own rounding and still see one typical bin's power move by 1 %.  A frame that fails is recomputed (up to LOGMEL_TRIES times); err words:
+// [0] frames still failing, [1..3] the first one (clip + 1, frame, wave), [4] frames that passed on a retry,
+// [5..7] the first of those.
+constexpr float PARSEVAL_REL = 1e-4f;
+constexpr float CHECKSUM_REL = 2e-5f;
+constexpr int LOGMEL_TRIES = 3;
+
+__device__ __forceinline__ void logmel_record(uint32_t* err, int slot, int clip, int frame, int wave) {
+  atomicAdd(err + slot, 1u);
+  if (atomicCAS(err + slot + 1, 0u, (uint32_t)clip + 1u) == 0u) {
+    __hip_atomic_store(err + slot + 2, (uint32_t)frame, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(err + slot + 3, (uint32_t)wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ __forceinline__ int reflect_idx(int n, int T) {
   if (n < 0) n = -n;
   if (n >= T) n = 2 * (T - 1) - n;
@@ -101,7 +151,8 @@ __constant__ const f2 W16[8] = {{1.f, 0.f},
 __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) void fft_mel_db_kernel(const float* __restrict__ wav, int64_t ld, int T,
                                                             int frames, int nbm, int nitems, int n_mels,
                                                             MelTables tb, float* __restrict__ out,
-                                                            float* __restrict__ blockmax) {
+                                                            float* __restrict__ blockmax, uint32_t* __restrict__ err,
+                                                            int64_t fault_frame, int fault_tries) {
   __shared__ float seg[SEG];
   __shared__ f2 buf[LW][NC];             // one in-place Stockham buffer per wave
   __shared__ float tile[NMEL_MAX][FB + 1];
@@ -111,6 +162,7 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   __shared__ int bs[NMEL_MAX], bl[NMEL_MAX], bo[NMEL_MAX];
   __shared__ int goff[NMEL_MAX / 64 + 1];
   __shared__ float redmax[LW];
+  __shared__ f2 tw64[64];
   __shared__ int w_lds_s;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -165,12 +217,12 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const int u = 2 * (lane + 64 * r);
     win[r] = u < WIN ? f2{tb.window[u], tb.window[u + 1]} : f2{0.f, 0.f};
   }
-  f2 tw1[8], tw2[8];
+  // stage-1 twiddles W512^(8 (lane % 8) r) = W64^((lane % 8) r): 64 distinct values, read from LDS (8 addresses
+  // per read, broadcast); the stage-2 twiddles W512^(lane r) stay in registers
+  if (t < 64) tw64[t] = tb.tw512[(NC / 64) * t];
+  f2 tw2[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    tw1[r] = tb.tw512[((lane % 8) * (NC / 64) * r) & (NC - 1)];
-    tw2[r] = tb.tw512[(lane * (NC / 512) * r) & (NC - 1)];
-  }
+  for (int r = 0; r < 8; ++r) tw2[r] = tb.tw512[(lane * (NC / 512) * r) & (NC - 1)];
   // real-split twiddles W1024^(lane + 64 q) = W1024^lane * W16^q (one per lane in registers)
   f2 tws0 = tb.tw1024[lane];
 
@@ -203,11 +255,15 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const int b = it / nbm;
     const int f0 = (it - b * nbm) * FB;
     float lmax = -INFINITY;
+    int attempt = 0;  // a frame whose FFT fails its self-check is recomputed (k is not advanced)
 #pragma unroll 1
-    for (int k = 0; k < FB / LW; ++k) {
+    for (int k = 0; k < FB / LW;) {
       const int fi = wave * (FB / LW) + k;
       if (f0 + fi >= frames) break;  // wave-uniform
+      float pk[8];
+      float pn = 0.f;
       // stage 0 (Ns = 1) reads z[j + 64 r] straight from the segment, z[n] = 0 for n >= 200
+      float et = 0.f;  // this lane's share of sum_n x_n^2 (Parseval)
       {
         f2 v[8];
 #pragma unroll
@@ -218,13 +274,15 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           else
             v[r] = f2{0.f, 0.f};
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) et = fmaf(v[r].x, v[r].x, fmaf(v[r].y, v[r].y, et));
         dft8(v);
 #pragma unroll
         for (int r = 0; r < 8; ++r) d[swz(lane * 8 + r)] = v[r];
       }
-      wave_sync();
-      // stages 1 (Ns = 8) and 2 (Ns = 64), in place: every lane's reads land before any lane's writes
-      // (one wave, program order), so the single buffer needs no ping-pong
+      lds_handoff();
+      // stages 1 (Ns = 8) and 2 (Ns = 64), in place: each stage's reads complete before its writes
+      // (data dependence through dft8) and its writes complete before the next stage's reads (lds_handoff)
 #pragma unroll
       for (int st = 1; st < 3; ++st) {
         const int Ns = st == 1 ? 8 : 64;
@@ -233,42 +291,61 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const f2 a = d[swz(lane + 64 * r)];
-          v[r] = r ? cmul(a, st == 1 ? tw1[r] : tw2[r]) : a;
+          v[r] = r ? cmul(a, st == 1 ? tw64[((lane & 7) * r) & 63] : tw2[r]) : a;
         }
         dft8(v);
-        wave_sync();
+        lds_handoff();
         const int idxD = (lane / Ns) * Ns * 8 + jm;
 #pragma unroll
         for (int r = 0; r < 8; ++r) d[swz(idxD + r * Ns)] = v[r];
-        wave_sync();
+        lds_handoff();
+      }
+      // test-only fault injection (MIA_LOGMEL_FAULT, see mia_logmel_fwd): one spectrum value of one frame
+      // scaled by 1.05 on its first `fault_tries` attempts
+      if (fault_tries > attempt && (int64_t)b * frames + f0 + fi == fault_frame) {
+        if (lane == 5) d[swz(5 + 64 * 3)] *= 1.05f;
+        lds_handoff();
       }
       // Z in d (natural order). Real-FFT split -> power P[k] (k = 0..512), kept in registers, then
       // written over the (consumed) spectrum as floats.  X[k] = 0.5 (e - i W^k o) with
       // e = Z[k] + conj(Z[N-k]), o = Z[k] - conj(Z[N-k]); |X|^2 = 0.25 |e - i W^k o|^2.
-      float pk[8];
       asm volatile("" : "+v"(tws0));  // derived per frame (not hoisted: registers)
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int k = lane + 64 * q;
-        const f2 zk = d[swz(k)];
-        const f2 zc = d[swz((NC - k) & (NC - 1))] * f2{1.f, -1.f};
+        const int kb = lane + 64 * q;  // bin
+        const f2 zk = d[swz(kb)];
+        const f2 zc = d[swz((NC - kb) & (NC - 1))] * f2{1.f, -1.f};
         const f2 tq = q ? cmul(tws0, W16[q]) : tws0;
         const f2 wo = cmul(tq, zk - zc);
-        const f2 X = (zk + zc) - wo.yx * f2{-1.f, 1.f};  // e - i wo = (e.x + wo.y, e.y - wo.x)
+        const f2 X = (zk + zc) - wo.yx * f2{-1.f, 1.f};  // e - i wo = (e.x + wo.y, e.y - wo.x) = 2 X[k]
         pk[q] = 0.25f * (X.x * X.x + X.y * X.y);
       }
-      float pn = 0.f;
       if (lane == 0) {
         const f2 z0 = d[0];
         const float xn = z0.x - z0.y;  // X[512]
         pn = xn * xn;
       }
-      wave_sync();
+      // self-check sums: bins 1..511 count twice (their mirror images 513..1023), bins 0 and 512 once;
+      // (-1)^k = (-1)^lane for k = lane + 64 q
+      float fs = pn - (lane == 0 ? pk[0] : 0.f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) fs = fmaf(2.f, pk[q], fs);
+      const float e_t = wave_sum_dpp(et);
+      const float e_f = wave_sum_dpp(fs);
+      const float chk = wave_sum_dpp((lane & 1) ? -fs : fs);
+      const bool ok = fabsf(e_f * (1.f / NFFT) - e_t) <= PARSEVAL_REL * e_t && fabsf(chk) <= CHECKSUM_REL * e_f;
+      lds_handoff();  // the spectrum reads are done (P overwrites it below; a retry rewrites it)
+      if (!ok && attempt + 1 < LOGMEL_TRIES) {  // wave-uniform
+        ++attempt;
+        continue;
+      }
+      if ((attempt > 0 || !ok) && err && lane == 0) logmel_record(err, ok ? 4 : 0, b, f0 + fi, wave);
+      attempt = 0;
       float* P = reinterpret_cast<float*>(d);
 #pragma unroll
       for (int q = 0; q < 8; ++q) P[lane + 64 * q] = pk[q];
       if (lane == 0) P[NC] = pn;
-      wave_sync();
+      lds_handoff();
       for (int m = lane; m < n_mels; m += 64) {
         const int ks = bs[m], kl = bl[m], off = bo[m];
         float acc = 0.f;
@@ -291,7 +368,8 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         tile[m][fi] = db;
         lmax = fmaxf(lmax, db);
       }
-      wave_sync();
+      lds_handoff();
+      ++k;
     }
     lmax = wave_max(lmax);
     if (lane == 0) redmax[wave] = lmax;
@@ -428,7 +506,7 @@ extern "C" int mia_logmel_fwd(const float* wav, int64_t B, int64_t T, int64_t ld
                               const MiaMelCfg* cfg, const float* window, const void* tw512,
                               const void* tw1024, const int32_t* band_start,
                               const int32_t* band_len, const int32_t* band_off,
-                              const float* band_w, float* out, void* workspace,
+                              const float* band_w, float* out, void* workspace, uint32_t* err,
                               mia_stream_t stream) {
   MIA_CHECK_ARG(wav && cfg && window && tw512 && tw1024 && band_start && band_len && band_off &&
                     band_w && out && workspace,
@@ -448,10 +526,22 @@ extern "C" int mia_logmel_fwd(const float* wav, int64_t B, int64_t T, int64_t ld
   MelTables tb{window, reinterpret_cast<const f2*>(tw512), reinterpret_cast<const f2*>(tw1024),
                band_start, band_len, band_off, band_w};
   hipStream_t s = as_stream(stream);
+  // Test-only fault injection for the FFT self-check: MIA_LOGMEL_FAULT="<clip>,<frame>,<tries>" corrupts that
+  // frame's spectrum on its first <tries> attempts (tests/test_gpu_logmel.py); unset in every product run.
+  int64_t fault_frame = -1;
+  int fault_tries = 0;
+  if (const char* f = getenv("MIA_LOGMEL_FAULT")) {
+    long long c = -1, fr = -1;
+    int tr = 0;
+    if (sscanf(f, "%lld,%lld,%d", &c, &fr, &tr) == 3 && c >= 0 && fr >= 0) {
+      fault_frame = c * frames + fr;
+      fault_tries = tr;
+    }
+  }
   // three 4-wave workgroups per CU (LDS 43 KB, 152 VGPRs), persistent over the (clip, chunk) items
   const unsigned grid = (unsigned)std::min<int64_t>(nitems, 3 * mia::cu_count());
   fft_mel_db_kernel<<<grid, LNT, 0, s>>>(wav, ld_wav, (int)T, frames, nbm, (int)nitems, cfg->n_mels, tb, out,
-                                        blockmax);
+                                        blockmax, err, fault_frame, fault_tries);
   MIA_LAUNCH_CHECK("fft_mel_db");
   const int64_t per_clip = (int64_t)cfg->n_mels * frames;
   if (cfg->normalize) {

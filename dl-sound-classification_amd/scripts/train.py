@@ -93,26 +93,27 @@ def train(cfg) -> dict:
 def launch_ranks(n: int, argv: list[str]) -> int:
     """``trainer.devices=N`` without a launcher: start one process per device through
     torch.distributed.run on this node (rendezvous on 127.0.0.1), as Lightning's DDP strategy re-launches
-    the script per rank (reference train.py:190-194).  Runs before this process touches the GPU."""
-    import socket
+    the script per rank (reference train.py:190-194).  Runs before this process touches the GPU.  The c10d
+    rendezvous store binds port 0 itself (no probe-then-close race for a free port)."""
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    import uuid
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", f"--rdzv-id={uuid.uuid4()}",
+           "--local-addr", "127.0.0.1", os.path.abspath(__file__), *argv]
     return subprocess.call(cmd)
 
 
 def main(argv=None):
+    """Train / test from the config tree.  With ``trainer.devices > 1`` outside a launcher: the launcher's exit
+    code (0 = every rank finished); otherwise train()'s result."""
     argv = list(sys.argv[1:] if argv is None else argv)
     cfg = compose(os.path.join(ROOT, "configs"), "training", argv)
     devices = cfg.trainer.get("devices", 1)
     if isinstance(devices, int) and devices > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(devices, argv))
+        return launch_ranks(devices, argv)
     return train(cfg)
 
 
 if __name__ == "__main__":
-    main()
+    res = main()
+    sys.exit(res if isinstance(res, int) else 0)

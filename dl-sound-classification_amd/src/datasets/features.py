@@ -90,5 +90,6 @@ class GpuLogMel:
             L.check(lib.mia_logmel_fwd(wav.data_ptr(), B, T, T, self.cfg, t["window"].data_ptr(),
                                        t["tw512"].data_ptr(), t["tw1024"].data_ptr(), t["band_start"].data_ptr(),
                                        t["band_len"].data_ptr(), t["band_off"].data_ptr(), t["band_w"].data_ptr(),
-                                       out.data_ptr(), ws.data_ptr(), L.stream_ptr()), "mia_logmel_fwd")
+                                       out.data_ptr(), ws.data_ptr(), K.logmel_err_word(wav.device).data_ptr(),
+                                       L.stream_ptr()), "mia_logmel_fwd")
         return out

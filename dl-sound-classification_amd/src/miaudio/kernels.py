@@ -52,6 +52,39 @@ def check_attention_errors() -> None:
         if int(w.item()) != 0:
             raise RuntimeError(f"attention backward on {key}: a dQ hand-off wait timed out (mia_attn_bwd_onepass); "
                                "the gradients of that step are invalid")
+    check_logmel_errors()
+
+
+_LOGMEL_ERR: dict = {}
+
+
+def logmel_err_word(device) -> torch.Tensor:
+    """The 8 sticky u32 words of the log-mel FFT self-check on ``device`` (mia_logmel_fwd ``err``: [0] frames that
+    failed Parseval / the vanishing checksum on all 3 tries, [1..3] the first (clip + 1, frame, wave), [4] frames
+    that passed on a retry, [5..7] the first of those).  The library never clears them."""
+    key = str(device)
+    w = _LOGMEL_ERR.get(key)
+    if w is None:
+        w = _LOGMEL_ERR[key] = torch.zeros(8, dtype=torch.int32, device=device)
+    return w
+
+
+def logmel_error_counts() -> dict:
+    """{device: (failed, retried, first_failed (clip, frame, wave) | None, first_retried | None)}.  Host sync."""
+    res = {}
+    for key, w in _LOGMEL_ERR.items():
+        v = [int(x) for x in w.cpu().tolist()]
+        res[key] = (v[0], v[4], (v[1] - 1, v[2], v[3]) if v[1] else None, (v[5] - 1, v[6], v[7]) if v[5] else None)
+    return res
+
+
+def check_logmel_errors() -> None:
+    """Raise if a log-mel frame failed its in-kernel FFT self-check on every try since start-up (its features are
+    invalid); frames that passed on a retry are reported by ``logmel_error_counts`` only.  Host sync."""
+    for key, (bad, _, first, _) in logmel_error_counts().items():
+        if bad:
+            raise RuntimeError(f"log-mel on {key}: {bad} frame(s) failed the FFT self-check on every try (first: "
+                               f"clip {first[0]}, frame {first[1]}, wave {first[2]}); their features are invalid")
 
 
 # ------------------------------------------------------------------------------------ GEMM

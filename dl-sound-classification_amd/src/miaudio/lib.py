@@ -83,7 +83,7 @@ SIGNATURES = {
     "mia_attn_fwd_mx": (C.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "mia_splitk_reduce": (C.c_int, [vp, i32, i64, i64, P(MiaEpilogue), vp]),
     "mia_logmel_workspace_bytes": (i64, [i64, i64]),
-    "mia_logmel_fwd": (C.c_int, [vp, i64, i64, i64, P(MiaMelCfg), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "mia_logmel_fwd": (C.c_int, [vp, i64, i64, i64, P(MiaMelCfg), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mia_bn_partial_bytes": (i64, [i64, i32]),
     "mia_bn_fwd_stats": (C.c_int, [vp, i32, i64, i32, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp, vp]),
     "mia_bn_relu_bwd_reduce": (C.c_int, [vp, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]),

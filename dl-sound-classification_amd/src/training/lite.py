@@ -253,6 +253,11 @@ class Trainer:
         return int(lim) if (isinstance(lim, int) or float(lim) > 1) else max(1, int(math.ceil(float(lim) * n)))
 
     def save_checkpoint(self, path):
+        if self.ddp is not None and self.ddp.sharded:
+            # fc1_exchange="shard": outside its own slice this rank's f32 FC1 rows and Adam moments are stale
+            # until the collective sync_sharded() (every rank, e.g. the epoch end) gathers them
+            raise RuntimeError("save_checkpoint: sharded FC1 rows are stale on this rank; call "
+                               "trainer.ddp.sync_sharded() on every rank first")
         m = self._module
         torch.save({"state_dict": m.state_dict(), "epoch": m.current_epoch, "global_step": m.global_step,
                     "optimizer_states": [self.optimizer.state_dict()] if self.optimizer else [],

@@ -195,7 +195,12 @@ int mia_gemm_path(const MiaOperand* A, const MiaOperand* B, int64_t M, int64_t N
  * Constant device tables built once by the caller: window[win_length] (periodic Hann),
  * tw512[512] / tw1024[513] complex twiddles exp(-2 pi i q/512), exp(-2 pi i k/1024) as float2,
  * mel bands: band_start/band_len/band_off[n_mels] into band_w[nnz] (htk filterbank, norm=None).
- * workspace: mia_logmel_workspace_bytes(B, frames) bytes. */
+ * workspace: mia_logmel_workspace_bytes(B, frames) bytes.
+ * err: NULL, or 8 caller-owned u32 words, zero before the first call and never cleared by the library.
+ * Every frame's FFT is checked in the kernel (Parseval, and sum_k (-1)^k X_k = 1024 x_512 = 0) and
+ * recomputed when a check fails: err[0] counts frames that still failed after 3 tries (their output is
+ * invalid), err[1..3] = (clip + 1, frame, wave) of the first; err[4] counts frames that passed on a retry,
+ * err[5..7] the first of those. */
 typedef struct MiaMelCfg {
   int32_t sample_rate, n_fft, win_length, hop, n_mels, normalize;
   float top_db, target_mean, target_std;
@@ -204,7 +209,7 @@ int64_t mia_logmel_workspace_bytes(int64_t B, int64_t frames);
 int mia_logmel_fwd(const float* wav, int64_t B, int64_t T, int64_t ld_wav, const MiaMelCfg* cfg,
                    const float* window, const void* tw512, const void* tw1024,
                    const int32_t* band_start, const int32_t* band_len, const int32_t* band_off,
-                   const float* band_w, float* out, void* workspace, mia_stream_t stream);
+                   const float* band_w, float* out, void* workspace, uint32_t* err, mia_stream_t stream);
 
 /* BatchNorm (train mode) — nn.BatchNorm2d after every conv (envnet_v2.py:16,20,32,35).
  * x: (P, C) channels-last.  stats out: mean[C], invstd[C]; running stats updated with

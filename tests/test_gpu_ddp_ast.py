@@ -90,7 +90,8 @@ def _worker(rank, world, port, compute, q):
             parts = [torch.empty_like(v) for _ in range(world)]
             dist.all_gather(parts, v)
             same.append(torch.equal(parts[0], parts[1]))
-        q.put((rank, red.last_fired, len(plain), nz, mism, all(same), (nondet[:5], all(same_init)), None))
+        lm = K.logmel_error_counts().get(str(dev), (0, 0, None, None))  # the in-kernel FFT self-check
+        q.put((rank, red.last_fired, len(plain), nz, mism, all(same), (nondet[:5], all(same_init), lm), None))
         dist.destroy_process_group()
     except Exception:
         import traceback
@@ -115,7 +116,9 @@ def test_grad_allreducer_ast_two_ranks(compute):
         assert p.exitcode == 0
     for r, (fired, nparam, nz, mism, same, diag, err) in res.items():
         assert err is None, (r, err)
-        nondet, same_init = diag
+        nondet, same_init, lm = diag
+        print(f"rank {r}: log-mel self-check (failed, retried, first failed, first retried) = {lm}")
+        assert lm[0] == 0, f"rank {r}: log-mel frames failed the FFT self-check on every try: {lm}"
         assert not nondet, f"rank {r}: plain AST {compute} gradients differ between two identical steps: {nondet}"
         assert same_init, f"rank {r}: the ranks built different initial weights"
         assert fired > 0, "no gradient left through _grad_ready inside the AST backward"

@@ -65,3 +65,60 @@ def test_batch256_properties(cuda):
     assert float((out[:, 0, :] - out[:, 0, :1]).abs().max()) == 0.0
     ref = olog.logmel(wav[:2].cpu().numpy()).numpy()
     np.testing.assert_allclose(out[:2].cpu().numpy(), ref, atol=ATOL)
+
+
+# ---- the in-kernel FFT self-check (Parseval + the vanishing lag-512 autocorrelation of the power spectrum) ----
+def _fresh_err_word(monkeypatch, cuda):
+    from src.miaudio import kernels as K
+    w = torch.zeros(8, dtype=torch.int32, device=cuda)
+    monkeypatch.setitem(K._LOGMEL_ERR, str(cuda), w)
+    return w
+
+
+def test_self_check_silent_on_clean_batches(cuda, monkeypatch):
+    """Full-size clips, ragged and near-silent rows: no frame fails or is retried, and two calls agree bit for bit."""
+    w = _fresh_err_word(monkeypatch, cuda)
+    wav = torch.from_numpy(hash_uniform(78, (64, 220_500))).to(cuda)
+    mel = GpuLogMel()
+    a = mel(wav)
+    b = mel(wav)
+    quiet = np.stack([synth_waveform(3, 1, 20_000)[0] * 1e-4, np.zeros(20_000, np.float32)])
+    mel(torch.from_numpy(quiet).to(cuda))
+    GpuLogMel(normalize=False)(torch.from_numpy(synth_waveform(5000, 3, 5000)).to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert w.cpu().tolist() == [0] * 8
+
+
+def test_self_check_repairs_a_transient_fault(cuda, monkeypatch):
+    """One spectrum value of clip 1, frame 293 scaled by 1.05 on the first attempt only (MIA_LOGMEL_FAULT): the
+    check catches it, the frame is recomputed, the output is bit-identical to a clean call, and err[4..7] record
+    (clip 1 + 1, frame 293, wave 1) -- frame 293 is item 18's frame 5, i.e. wave 1's."""
+    from src.miaudio import kernels as K
+    wav = torch.from_numpy(synth_waveform(71, 2, 220_500)).to(cuda)
+    mel = GpuLogMel()
+    clean = mel(wav).clone()
+    w = _fresh_err_word(monkeypatch, cuda)
+    monkeypatch.setenv("MIA_LOGMEL_FAULT", "1,293,1")
+    again = mel(wav)
+    torch.cuda.synchronize()
+    assert w.cpu().tolist() == [0, 0, 0, 0, 1, 2, 293, 1]
+    assert torch.equal(again, clean)
+    K.check_logmel_errors()  # a repaired frame is not an error
+
+
+def test_self_check_flags_a_persistent_fault(cuda, monkeypatch):
+    """The same fault on every attempt: err[0..3] record it and check_logmel_errors raises; only that clip differs."""
+    from src.miaudio import kernels as K
+    wav = torch.from_numpy(synth_waveform(71, 2, 220_500)).to(cuda)
+    mel = GpuLogMel(normalize=False)
+    clean = mel(wav).clone()
+    w = _fresh_err_word(monkeypatch, cuda)
+    monkeypatch.setenv("MIA_LOGMEL_FAULT", "1,293,3")
+    bad = mel(wav)
+    torch.cuda.synchronize()
+    assert w.cpu().tolist() == [1, 2, 293, 1, 0, 0, 0, 0]
+    diff = (bad != clean).nonzero()
+    assert diff.shape[0] > 0 and set(diff[:, 0].tolist()) == {1} and set(diff[:, 2].tolist()) == {293}
+    with pytest.raises(RuntimeError, match="clip 1, frame 293, wave 1"):
+        K.check_logmel_errors()

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5 GPU pass (through gpurun from the repo root).  STAGES picks the steps; each GPU step has its own
+# Staged GPU pass (through gpurun from the repo root).  STAGES picks the steps; each GPU step has its own
 # limit and the chain stops at the first failure (a timeout / abort / fault ends the call).
-#   STAGES="new bench attnpmc" NEW="tests/x.py" bash tools/gpu_r5.sh <tag>
+#   STAGES="new bench attnpmc" NEW="tests/x.py" bash tools/gpu_stages.sh <tag>
 TAG=${1:-r5}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
