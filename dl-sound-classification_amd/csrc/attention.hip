@@ -250,6 +250,9 @@ __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], cons
     f[9] = row_frag(F_ + 512 + qr * 8);
   };
   load(0, fr[0]);
+  // S / dP of both query halves first: half 1's ten MFMAs issue before half 0's exp / dS VALU, so that VALU
+  // runs under them instead of in front of half 0's dV / dK products
+  f32x16 scs[2], dps[2];
 #pragma unroll
   for (int sq = 0; sq < 2; ++sq) {
     const bf16x8 (&f)[10] = fr[sq];
@@ -260,9 +263,13 @@ __device__ __forceinline__ void dkdv_tile(f32x16 (&dk)[2], f32x16 (&dv)[2], cons
       sc = mfma(f[ks], kf[ks], sc);
       dp = mfma(f[4 + ks], vf[ks], dp);
     }
-    sc = mfma(f[8], one, sc);
-    dp = mfma(f[9], one, dp);
+    scs[sq] = mfma(f[8], one, sc);
+    dps[sq] = mfma(f[9], one, dp);
     if (sq == 0) load(1, fr[1]);
+  }
+#pragma unroll
+  for (int sq = 0; sq < 2; ++sq) {
+    f32x16 sc = scs[sq], dp = dps[sq];
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r]);
     if (qvalid < 64) {  // the sequence's last, partial query tile: rows past it contribute nothing
@@ -375,6 +382,8 @@ constexpr int BWD_Q = 128;
 // tile (the last key tile: the kernel walks the keys backwards) passes at run time; the loop passes 64
 __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const bf16* V_, const bf16x8 (&qf)[4],
                                         const bf16x8 (&gf)[4], float nl, float nd, int kvalid, int lane) {
+  // S / dP of both key halves first: half 1's MFMAs issue before half 0's exp / dS VALU (as dkdv_tile)
+  f32x16 scs[2], dps[2];
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh) {
     const int kr = 32 * kh + (lane & 31);
@@ -385,6 +394,12 @@ __device__ __forceinline__ void dq_tile(f32x16 (&acc)[2], const bf16* K_, const 
       sc = mfma(frag_row_sw(K_, kr, ks, lane), qf[ks], sc);
       dp = mfma(frag_row_sw(V_, kr, ks, lane), gf[ks], dp);
     }
+    scs[kh] = sc;
+    dps[kh] = dp;
+  }
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    f32x16 sc = scs[kh], dp = dps[kh];
     // the lane's column is one query: its row constants are two per-lane scalars (VALU adds beside the
     // other waves' MFMAs instead of two fifth-k-step MFMAs per key half)
 #pragma unroll

@@ -131,8 +131,17 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / REPS
         total += ms
+        digest = ""
+        if os.environ.get("CHECKSUM"):  # outputs of this build, to compare builds bit for bit across processes
+            import hashlib
+            h = hashlib.sha1(out.cpu().contiguous().view(torch.uint8).numpy().tobytes())
+            if epi in ("gelu_save", "gelu_save_d"):
+                h.update(u.cpu().contiguous().view(torch.uint8).numpy().tobytes())
+            if E.colsum:
+                h.update(cs.cpu().numpy().tobytes())
+            digest = "  sha1 " + h.hexdigest()[:16]
         print(f"path {path} {name:11s} {epi + ('+mxq' if mxq else ''):15s} M={M:6d} N={N:5d} K={Kd:6d}  {ms:7.3f} ms  "
-              f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
+              f"{2 * M * N * Kd / ms / 1e9:7.1f} TF/s{digest}", flush=True)
         del a, b, A, Bo, E, out
         torch.cuda.empty_cache()
     print(f"total {total:.3f} ms per block (x12 per step)")
