@@ -325,6 +325,40 @@ def time_leg(step, probe_tags, args, world, dev, warmup, steps):
     return elapsed, float(loss), kstats
 
 
+ATTN_KERNELS = ("attn_fwd_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel")
+
+
+def attention_summary(model: str, ks: dict, peak_tf: float):
+    """The north-star attention figure two ways: the credited rate of forward + backward live (SURVEY.md §8(d):
+    4 N^2 d H per clip forward, twice that backward, the backward's S / dP recompute not credited) against the
+    bf16 MFMA peak, and the hardware MFMA utilisation of the three attention kernels from the committed
+    rocprofv3 SQ pass of the same bench command (profiles/<round>_sq_<model>.json, tools/sq_summary.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x the run's own clock x duration)), time-weighted."""
+    f, b = ks.get("attn.fwd"), ks.get("attn.bwd")
+    res = {}
+    if f and b:
+        fl = f["flop"] * f["launches_per_step"] + b["flop"] * b["launches_per_step"]
+        t = f["ms"] * f["launches_per_step"] + b["ms"] * b["launches_per_step"]
+        res["credited_tflops"] = round(fl / (t * 1e-3) / 1e12, 1)
+        res["credited_frac"] = round(fl / (t * 1e-3) / 1e12 / peak_tf, 4)
+        res["ms_per_step"] = round(t, 3)
+    files = sorted((REPO / "profiles").glob(f"r*_sq_{model}.json"))
+    if files:
+        table = json.loads(files[-1].read_text())["kernels"]
+        per, wsum, tsum = {}, 0.0, 0.0
+        for name, e in table.items():
+            hit = next((k for k in ATTN_KERNELS if k in name), None)
+            if hit and e.get("mfma_util") is not None:
+                per[hit] = {"mfma_busy": e["mfma_util"], "clock_ghz": e.get("clock_ghz_pmc_run"),
+                            "ms_per_step": e.get("ms_trace")}
+                wsum += e["mfma_util"] * (e.get("ms_trace") or 0.0)
+                tsum += e.get("ms_trace") or 0.0
+        if per:
+            res["mfma_busy"] = {"source": files[-1].name, "kernels": per,
+                                "time_weighted": round(wsum / tsum, 4) if tsum else None}
+    return res or None
+
+
 def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_clip, args, workload,
                roof_tag=None):
     ms = elapsed / steps * 1e3
@@ -354,6 +388,8 @@ def leg_result(model, B, world, steps, warmup, elapsed, loss, kstats, flop_per_c
         out["comm"] = comm
     if model == "envnet":
         out["frontend_path"] = frontend_summary(regions, B)
+    if model.startswith("ast"):
+        out["attention"] = attention_summary(model, ks, peak_tf)
     if out["dominant_kernel"] is None:
         out.pop("dominant_kernel")
     return out

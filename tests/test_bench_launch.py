@@ -49,3 +49,18 @@ def test_check_world():
     bench.check_world(2, 2)
     with pytest.raises(SystemExit):
         bench.check_world(8, 1)
+
+
+def test_attention_summary_credited_and_counter_figures():
+    """The AST legs' attention object: credited rate from the probed launches (forward + backward FLOPs of
+    SURVEY §8(d) over their live time) and the MFMA-busy figures of the committed SQ profile."""
+    ks = {"attn.fwd": {"ms": 2.0, "launches_per_step": 12.0, "flop": 2.0e12},
+          "attn.bwd": {"ms": 6.0, "launches_per_step": 12.0, "flop": 4.0e12}}
+    res = bench.attention_summary("ast", ks, 2500.0)
+    assert res["credited_tflops"] == 750.0 and res["credited_frac"] == 0.3 and res["ms_per_step"] == 96.0
+    busy = res["mfma_busy"]
+    assert busy["source"].endswith("_sq_ast.json")
+    assert set(busy["kernels"]) == set(bench.ATTN_KERNELS)
+    assert all(0.0 < k["mfma_busy"] < 1.0 for k in busy["kernels"].values())
+    assert 0.0 < busy["time_weighted"] < 1.0
+    assert bench.attention_summary("ast", {}, 2500.0)["mfma_busy"]  # counters alone when nothing was probed
