@@ -56,6 +56,7 @@ struct MArgs {
   uint8_t* mxs;       // ... and its scales [M][N / 32]
   int64_t drop_w;     // EPI_PLAIN with a drop-mode row map (MIA_RM_DROP): row m -> m - m / drop_w, rows with
                       // m % drop_w == drop_w - 1 not stored (0: off)
+  int group_m;        // tile order (mg_tile_of): 0 = column block fastest, > 0 = groups of group_m row blocks
 };
 
 typedef unsigned mg_u32x4 __attribute__((ext_vector_type(4)));
@@ -465,6 +466,24 @@ __device__ __forceinline__ float frag_sum(bf16x8 f, float c) {
 // ACS (RC A operand, the split-K weight gradients): also the column sums over k of A -- the bias gradient of
 // the linear -- from the K-tiles in LDS: wave (wr, wc) sums rows 16 wc .. 16 wc + 15 and 64 + 16 wc .. of its
 // 128-row half (the four wc waves read the same A rows), two extra transposed fragment reads per k-step
+// Logical tile -> (row block, column block).  Default: column block fastest (a row block of A is read by all its
+// column tiles at about the same time, from the XCD's L2).  group_m > 0 (mg_group_m): groups of group_m row
+// blocks with the row block fastest inside a group, so the XCD's concurrent tiles share fewer B column blocks
+// (gpurun_out r6gm / r6gm2: fc2.dgrad -2.3 %; the N = 768 shapes are 1-4 % slower with it).  Either order runs
+// every tile's own K loop unchanged: the output is bit-identical.
+__device__ __forceinline__ void mg_tile_of(const MArgs& g, int rem, int& bm, int& bn) {
+  if (g.group_m > 0) {
+    const int gsz = g.group_m * g.nbn;
+    const int grp = rem / gsz, off = rem - grp * gsz;
+    const int rows = min(g.group_m, g.nbm - grp * g.group_m);
+    bn = off / rows;
+    bm = grp * g.group_m + (off - bn * rows);
+  } else {
+    bm = rem / g.nbn;
+    bn = rem - bm * g.nbn;
+  }
+}
+
 template <int LA, int LB, int EPI, bool ACS = false>
 __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
   __shared__ __attribute__((aligned(1024))) char smem[MG_LDS];
@@ -481,7 +500,8 @@ __global__ __launch_bounds__(MG_NT, 2) void mgemm_kernel(MArgs g) {
   const int per_z = g.nbm * g.nbn;
   const int z = lid / per_z;
   const int rem = lid - z * per_z;
-  const int bm = rem / g.nbn, bn = rem - (rem / g.nbn) * g.nbn;
+  int bm, bn;
+  mg_tile_of(g, rem, bm, bn);
   const int64_t m0 = (int64_t)bm * MG_BM, n0 = (int64_t)bn * MG_BN;
   const int64_t kbeg = (int64_t)z * g.kper;
   const int64_t kend = kbeg + g.kper < g.K ? kbeg + g.kper : g.K;
@@ -672,7 +692,8 @@ __global__ __launch_bounds__(MG_NT, 2) void mxgemm_kernel(MArgs g, MxArgs x) {
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bm = lid / g.nbn, bn = lid - (lid / g.nbn) * g.nbn;
+  int bm, bn;
+  mg_tile_of(g, lid, bm, bn);
   const int64_t m0 = (int64_t)bm * MG_BM, n0 = (int64_t)bn * MG_BN;
   const int nk = (int)(g.K >> 7);
   // e4m3 rows seen as bf16 pairs: the bf16 loaders move 128-B K-tiles unchanged
@@ -904,6 +925,13 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 namespace mgemm {
 
+// Tile order for a launch, a fixed function of the shape and layout: grouped (8 row blocks) for wide unsplit
+// outputs of a k-by-n (RC) B operand -- the backward-data GEMMs of the wide linears (fc2.dgrad 2.43 -> 2.38 ms);
+// the k-contiguous forward shapes measured mixed (qkv.fwd -0.8 %, fc1.fwd +1.7 %, MX-fp8 unchanged: r6gm2)
+int mg_group_m(int nbm, int nbn, int split, int lb) {
+  return split == 1 && lb == MIA_LAYOUT_RC && nbn >= 9 && nbm >= 16 ? 8 : 0;
+}
+
 // Which epilogue kind the kernel would run for E (-1: not this kernel)
 int mg_epi_kind(const MiaEpilogue& E, int64_t N) {
   // a drop-mode row map (MIA_RM_DROP) only on a plain / bias bf16 output without an MX copy
@@ -992,6 +1020,7 @@ int mg_run(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   a.lda = A.ld; a.ldb = B.ld; a.M = M; a.N = N; a.K = K;
   mg_geometry(M, N, K, a.split, a.kper);
   a.nbm = (int)cdiv(M, MG_BM); a.nbn = (int)cdiv(N, MG_BN);
+  a.group_m = mg_group_m(a.nbm, a.nbn, a.split, B.layout);
   a.out = E.ptr; a.ldc = E.ldc; a.out_f32 = E.dtype == MIA_F32;
   a.drop_w = E.rm_inner && E.rm_offset == MIA_RM_DROP ? E.rm_inner : 0;
   a.bias = E.bias; a.aux = E.aux; a.ldaux = E.ldaux;
@@ -1116,6 +1145,7 @@ extern "C" int mia_gemm_mxfp8_ex(const void* a, const void* a_scales, int64_t ld
   g.lda = lda / 2; g.ldb = ldb / 2;  // e4m3 rows seen as bf16 pairs by the loaders
   g.M = M; g.N = N; g.K = K; g.kper = K; g.split = 1;
   g.nbm = (int)cdiv(M, MG_BM); g.nbn = (int)cdiv(N, MG_BN);
+  g.group_m = 0;  // MX-fp8 operands are k-contiguous (mg_group_m)
   g.out = E->ptr; g.ldc = E->ldc; g.out_f32 = E->dtype == MIA_F32;
   g.bias = E->bias; g.aux = E->aux; g.ldaux = E->ldaux;
   g.mxq = reinterpret_cast<uint8_t*>(E->mx_q); g.mxs = reinterpret_cast<uint8_t*>(E->mx_scales);
