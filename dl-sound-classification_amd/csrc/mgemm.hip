@@ -337,7 +337,8 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
     char* img = smem + wave * 16384;
     // the backward epilogues' aux rows (saved gelu'(u) / u) requested before the image pass, so their
     // latency runs under it instead of under the store loop (fc2.dgrad 1.99 -> 1.73 ms at B = 256,
-    // tools/gemm_epi_ab.sh, gpurun_out r5o / r5p)
+    // tools/gemm_epi_ab.sh, gpurun_out r5o / r5p); non-temporal: read once, kept out of the operands' L2
+    // (fc2.dgrad DMUL 2.44 -> 2.41 ms, r6nt; the f32 residual reads of ADD_AUX measured 2-3 % slower that way)
     uint4 ua[16];
     if constexpr (DG) {
 #pragma unroll
@@ -345,7 +346,8 @@ __device__ __forceinline__ void mg_epilogue(const MArgs& g, f32x4 (&acc)[8][4], 
         const int r = 8 * it + (lane >> 3);
         const int64_t m = m0 + wr * 128 + r, n = n0 + wc * 64 + 8 * (lane & 7);
         ua[it] = (m < g.M && n < g.N)
-                     ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)
+                     ? __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const mg_u32x4*>(
+                           reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n)))
                      : make_uint4(0, 0, 0, 0);
       }
     }
