@@ -984,12 +984,16 @@ bool mg_ok(const MiaOperand& A, const MiaOperand& B, const MiaEpilogue& E, int64
   return mg_epi_kind(E, N) >= 0;
 }
 
-// split-K width for the weight gradients (few output tiles, K = tokens): about 3 workgroups per
-// CU, K-slices of at least 1024; a fixed function of the shape (no timing)
+// split-K width for the weight gradients (few output tiles, K = tokens): tiles x split = one round of
+// workgroups on the MI355X's 256 CUs (a constant, not the device's count: the split sets the summation order,
+// so it stays a fixed function of the shape), K-slices of at least 1024.  Measured against the earlier ~3
+// rounds (768) and against 128 / 192 / 384 (tools/gemm_ab.sh, r6sp / r6sp2): fc1.wgrad 1.87 -> 1.78 ms, fc2.wgrad
+// 1.97 -> 1.86, proj.wgrad 0.58 -> 0.52, qkv.wgrad 1.39 -> 1.34 (fewer f32 slabs, no partial last round); a
+// partial round (192, 384) or fewer workgroups than CUs (128) is slower.
 int mg_split(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = cdiv(M, MG_BM) * cdiv(N, MG_BN);
   if (tiles >= 512 || K < 4096) return 1;
-  int64_t s = 768 / tiles;  // the last of the ~3 waves full: 27 tiles x 28, 36 x 21, 9 x 85
+  int64_t s = 256 / tiles;  // 27 tiles x 9, 36 x 7, 9 x 28
   const int64_t smax = K / 1024;
   if (s > smax) s = smax;
   return (int)(s < 1 ? 1 : s);
