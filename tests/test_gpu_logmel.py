@@ -85,6 +85,10 @@ def test_self_check_silent_on_clean_batches(cuda, monkeypatch):
     quiet = np.stack([synth_waveform(3, 1, 20_000)[0] * 1e-4, np.zeros(20_000, np.float32)])
     mel(torch.from_numpy(quiet).to(cuda))
     GpuLogMel(normalize=False)(torch.from_numpy(synth_waveform(5000, 3, 5000)).to(cuda))
+    # near-denormal amplitudes: squares of 1e-21 samples are f32 denormals, Parseval only holds to the floors
+    tiny = synth_waveform(9, 3, 20_000) * np.array([[1e-19], [1e-21], [1e-23]], np.float32)
+    t_out = GpuLogMel(normalize=False)(torch.from_numpy(tiny).to(cuda)).cpu().numpy()
+    np.testing.assert_allclose(t_out, olog.logmel(tiny, normalize=False).numpy(), atol=ATOL, rtol=0)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert w.cpu().tolist() == [0] * 8
