@@ -335,8 +335,10 @@ __global__ __launch_bounds__(LNT) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       const float chk = wave_sum_dpp((lane & 1) ? -fs : fs);
       // absolute floors: a frame whose whole power is ~1e-20 maps every band below amin = 1e-10 (-100 dB) whatever
       // its rounding, and near-denormal samples (amplitude ~1e-21) must not read as a failed check
-      const bool ok = fabsf(e_f * (1.f / NFFT) - e_t) <= fmaf(PARSEVAL_REL, e_t, 1e-24f) &&
-                      fabsf(chk) <= fmaf(CHECKSUM_REL, e_f, 1e-20f);
+      // a non-finite frame (NaN/Inf samples, e_t from the inputs alone) carries NaN to the output as the
+      // reference does; it is not a failed transform
+      const bool ok = (fabsf(e_f * (1.f / NFFT) - e_t) <= fmaf(PARSEVAL_REL, e_t, 1e-24f) &&
+                       fabsf(chk) <= fmaf(CHECKSUM_REL, e_f, 1e-20f)) || !isfinite(e_t);
       lds_handoff();  // the spectrum reads are done (P overwrites it below; a retry rewrites it)
       if (!ok && attempt + 1 < LOGMEL_TRIES) {  // wave-uniform
         ++attempt;

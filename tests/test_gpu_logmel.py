@@ -94,6 +94,22 @@ def test_self_check_silent_on_clean_batches(cuda, monkeypatch):
     assert w.cpu().tolist() == [0] * 8
 
 
+def test_self_check_passes_non_finite_clips(cuda, monkeypatch):
+    """A NaN or Inf sample corrupts its own clip (as in the reference) without reading as a failed transform, and
+    the clean clip beside it is unchanged."""
+    w = _fresh_err_word(monkeypatch, cuda)
+    wav = synth_waveform(13, 3, 20_000)
+    mel = GpuLogMel(normalize=False)
+    clean = mel(torch.from_numpy(wav).to(cuda)).cpu().numpy()
+    wav[1, 7000] = np.nan
+    wav[2, 12000] = np.inf
+    out = mel(torch.from_numpy(wav).to(cuda)).cpu().numpy()
+    torch.cuda.synchronize()
+    assert w.cpu().tolist() == [0] * 8
+    np.testing.assert_array_equal(out[0], clean[0])
+    assert (out[1] != clean[1]).any() and (out[2] != clean[2]).any()
+
+
 def test_self_check_repairs_a_transient_fault(cuda, monkeypatch):
     """One spectrum value of clip 1, frame 293 scaled by 1.05 on the first attempt only (MIA_LOGMEL_FAULT): the
     check catches it, the frame is recomputed, the output is bit-identical to a clean call, and err[4..7] record
