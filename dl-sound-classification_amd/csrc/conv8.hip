@@ -230,6 +230,9 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
       const bool live = iy >= 0 && iy < g.h;  // wave-uniform: padding rows contribute nothing
       if (live) {
         wave_sync();  // the previous row's fragment reads are done (common.h)
+#ifdef C8_PROBE_NOSTAGE  // timing probe only: the strip is never restaged
+        if (g.n < 0)
+#endif
         store_row();
         wave_sync();
       }
@@ -277,6 +280,9 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         }
       }
       constexpr int S = (P + 1) & 7;
+#ifdef C8_PROBE_NOEMIT  // timing probe only (tools/probe/c8_variant.sh): the epilogue never runs
+      if (g.n < 0)
+#endif
       if (r - 7 >= oy_lo) emit(acc[S], r - 7);
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)

@@ -24,6 +24,8 @@
 // (5.1 TB/s), the MFMA work alone 0.30-0.37 ms; the kernel lands at 0.98-1.15 ms.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int F1_DEPTH = 4;  // fe_conv1: waveform items in flight per wave (3 ahead; 0.506 -> 0.49 ms, 6: no gain)
@@ -276,6 +278,211 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     step(item, 1, rawb, okb, rawa, oka);
     item += gridDim.x;
     if (item >= items) break;
+  }
+}
+
+// Warp-specialised form of feconv_kernel: one 8-wave workgroup per CU.  Waves 0-3 only compute (weights in
+// registers, 64 MFMAs per item from the LDS window, the swap epilogue's stores); waves 4-7 only feed: they keep
+// FS_DEPTH items of raw window loads in flight in their own registers and cook (BN1 affine + ReLU, bf16 pack)
+// the next item's window into the other half of the double-buffered LDS window.  One barrier per item hands
+// the window over.  The two roles meet on every SIMD (one compute + one feeder wave each), so the feeders'
+// VALU and load issue run under the compute waves' MFMAs instead of in a phase of their own.
+constexpr int FS_NT = 512;
+constexpr int FS_DEPTH = 3;  // raw window loads in flight per feeder thread (items k+1 .. k+3)
+#ifndef FS_FD
+#define FS_FD 4  // k-steps of B fragments in flight per compute wave
+#endif
+
+// LDS-only workgroup barrier: this wave's LDS operations complete, then s_barrier; the "memory" clobber keeps the
+// compiler from moving memory operations across it, and no vmcnt wait is implied (the feeders' window loads and
+// the compute waves' output stores stay in flight)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int CIN, int KW, int S, bool PRE>
+__global__ __launch_bounds__(FS_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void feconv_ws_kernel(FeArgs g) {
+  using Cfg = FeCfg<CIN, KW, S>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * Cfg::WBYTES];
+  __shared__ __attribute__((aligned(16))) float sbias[FE_N];
+  __shared__ __attribute__((aligned(16))) float spre[2][CIN];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int items = g.n * g.nitem;
+  if ((int)blockIdx.x >= items) return;  // whole block
+  const int nk = (items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;  // items of this workgroup
+  if (t < FE_N) sbias[t] = g.bias ? g.bias[t] : 0.f;
+  if (PRE && t < CIN) {
+    spre[0][t] = g.ps[t];
+    spre[1][t] = g.pt[t];
+  }
+  if (wave < 4) {
+    // ---- compute waves: (channel half nh, pixel half pq) of every item, as in feconv_kernel
+    const int nh = wave & 1, pq = wave >> 1;
+    bf16x8 wf[Cfg::KS];
+    {
+      const bf16* wr = g.w + (int64_t)(nh * 32 + (lane & 31)) * (KW * CIN) + 8 * (lane >> 5);
+#pragma unroll
+      for (int ks = 0; ks < Cfg::KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 16);
+    }
+    const int c0 = nh * 32 + 8 * (lane >> 5);
+    lds_barrier();  // sbias / spre in
+    lds_barrier();  // item 0's window in
+#pragma unroll 1
+    for (int k = 0; k < nk; ++k) {
+      const int item = (int)blockIdx.x + k * (int)gridDim.x;
+      f32x16 acc[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+      const char* win = smem + (k & 1) * Cfg::WBYTES;
+      // B fragments FS_FD k-steps ahead of their MFMAs (a register ring; one wave per SIMD computes, so nothing
+      // else covers an LDS read's latency)
+      auto frag = [&](int ks, int i) __attribute__((always_inline)) {
+        constexpr int KPC = CIN / 16;
+        const int kx = ks / KPC;
+        const int ci = (ks % KPC) * 16 + 8 * (lane >> 5);
+        const int px = pq * 64 + i * 32 + (lane & 31);
+        int slot;
+        if constexpr (S == 1) slot = px + kx;
+        else slot = (kx & 1) * Cfg::HALF + px + (kx >> 1);
+        return *reinterpret_cast<const bf16x8*>(win + slot * Cfg::PSB + ci * 2);
+      };
+#ifdef FS_PROBE_NOCOMPUTE  // timing probe only: no MFMA work (outputs are the bias)
+      if (g.n < 0)
+#endif
+      {
+        bf16x8 fr[FS_FD][2];
+#pragma unroll
+        for (int ks = 0; ks < FS_FD; ++ks)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) fr[ks][i] = frag(ks, i);
+#pragma unroll
+        for (int ks = 0; ks < Cfg::KS; ++ks) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], fr[ks % FS_FD][i], acc[i], 0, 0, 0);
+            if (ks + FS_FD < Cfg::KS) fr[ks % FS_FD][i] = frag(ks + FS_FD, i);
+          }
+        }
+        // pin the ring (the scheduler otherwise sinks each read next to its MFMA): the first FS_FD k-steps' reads,
+        // then per k-step its 2 MFMAs and the 2 reads FS_FD ahead
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * FS_FD, 0);
+#pragma unroll
+        for (int ks = 0; ks < Cfg::KS; ++ks) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          if (ks + FS_FD < Cfg::KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+      }
+      const int b = item / g.nitem;
+      const int m0 = (item - b * g.nitem) * FE_BM + pq * 64;
+      bf16* yb = g.y + (int64_t)b * g.ystride;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v[16];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = acc[i][8 * h + j], hi = acc[i][8 * h + 4 + j];
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+            v[8 * h + j] = __builtin_bit_cast(float, (unsigned)r[0]);
+            v[8 * h + 4 + j] = __builtin_bit_cast(float, (unsigned)r[1]);
+          }
+        const int m = m0 + i * 32 + (lane & 31);
+        if (m < g.wout) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int64_t e = (int64_t)m * FE_N + c0 + 16 * h;
+            if (e < g.ylen) {
+              const f32x4 u0 = *reinterpret_cast<const f32x4*>(sbias + c0 + 16 * h);
+              const f32x4 u1 = *reinterpret_cast<const f32x4*>(sbias + c0 + 16 * h + 4);
+              const u32x4 o = {pack2(v[8 * h] + u0[0], v[8 * h + 1] + u0[1]), pack2(v[8 * h + 2] + u0[2], v[8 * h + 3] + u0[3]),
+                               pack2(v[8 * h + 4] + u1[0], v[8 * h + 5] + u1[1]), pack2(v[8 * h + 6] + u1[2], v[8 * h + 7] + u1[3])};
+              *reinterpret_cast<u32x4*>(yb + e) = o;
+            }
+          }
+        }
+      }
+      lds_barrier();  // this item's window reads are done; the next window is in
+    }
+  } else {
+    // ---- feeder waves: thread ft plays feconv_kernel's thread t for the window loads and the staging
+    const int ft = t - 256;
+    const int cg = ft % Cfg::CG;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(g.x), (short)0, (int)((int64_t)g.n * g.win * CIN * 2), 0x00020000);
+    auto load = [&](int k, u32x4 (&raw)[Cfg::LCH], uint32_t& rok) __attribute__((always_inline)) {
+      int it = (int)blockIdx.x + k * (int)gridDim.x;
+      it = it < items ? it : items - 1;  // past the end: a harmless redundant load
+      const int b = it / g.nitem;
+      const int px0 = (it - b * g.nitem) * FE_BM * S - g.pw;
+      rok = 0;
+#pragma unroll
+      for (int s = 0; s < Cfg::LCH; ++s) {
+        const int q = ft + FE_NT * s;
+        const int p = q / Cfg::CG;
+        const int ix = px0 + p;
+        const bool ok = p < Cfg::WPX && ix >= 0 && ix < g.win;
+        const unsigned off = ok ? (unsigned)((b * g.win + ix) * Cfg::CG + cg) * 16u : 0x80000000u;
+#ifdef FS_PROBE_NOLOAD  // timing probe only: no window loads (the staged windows are zeros)
+        raw[s] = u32x4{0u, 0u, 0u, 0u};
+        (void)off;
+#else
+        raw[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+#endif
+        rok |= (uint32_t)ok << s;
+      }
+    };
+    auto stage = [&](int buf, const u32x4 (&raw)[Cfg::LCH], uint32_t rok) __attribute__((always_inline)) {
+      float sc[8], sh[8];
+      if constexpr (PRE) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(&spre[0][cg * 8 + 4 * h]);
+          const f32x4 c = *reinterpret_cast<const f32x4*>(&spre[1][cg * 8 + 4 * h]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { sc[4 * h + q] = a[q]; sh[4 * h + q] = c[q]; }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < Cfg::LCH; ++s) {
+        const int q = ft + FE_NT * s;
+        const int p = q / Cfg::CG;
+        if (Cfg::NCH % FE_NT == 0 || p < Cfg::WPX)
+          *reinterpret_cast<u32x4*>(smem + buf * Cfg::WBYTES + fe_slot<S, Cfg::HALF>(p) * Cfg::PSB + cg * 16) =
+              fe_cook(raw[s], (rok >> s) & 1u, PRE, sc, sh);
+      }
+    };
+    u32x4 raw[FS_DEPTH][Cfg::LCH];
+    uint32_t rok[FS_DEPTH];
+#pragma unroll
+    for (int d = 0; d < FS_DEPTH; ++d) load(d, raw[d], rok[d]);
+    lds_barrier();  // sbias / spre in
+    stage(0, raw[0], rok[0]);
+    lds_barrier();  // item 0's window in
+    // iteration k: item k + FS_DEPTH's loads into the set item k used, item k + 1's window staged into half
+    // (k + 1) & 1 (its loads were issued FS_DEPTH - 1 items ago), barrier.  Unrolled by 6 = lcm(2, FS_DEPTH)
+    // so the register set and the LDS half are compile-time.
+    auto iter = [&](auto KC, int k) __attribute__((always_inline)) {
+      constexpr int R = decltype(KC)::value;  // k % 6
+      constexpr int SET = R % FS_DEPTH, NXT = (R + 1) % FS_DEPTH;
+      load(k + FS_DEPTH, raw[SET], rok[SET]);
+      if (k + 1 < nk) stage((R + 1) & 1, raw[NXT], rok[NXT]);
+      lds_barrier();  // the staged window is in LDS
+    };
+#pragma unroll 1
+    for (int k = 0; k < nk; k += 6) {
+      iter(std::integral_constant<int, 0>{}, k);
+      if (k + 1 >= nk) break;
+      iter(std::integral_constant<int, 1>{}, k + 1);
+      if (k + 2 >= nk) break;
+      iter(std::integral_constant<int, 2>{}, k + 2);
+      if (k + 3 >= nk) break;
+      iter(std::integral_constant<int, 3>{}, k + 3);
+      if (k + 4 >= nk) break;
+      iter(std::integral_constant<int, 4>{}, k + 4);
+      if (k + 5 >= nk) break;
+      iter(std::integral_constant<int, 5>{}, k + 5);
+    }
   }
 }
 
@@ -842,6 +1049,9 @@ __global__ __launch_bounds__(256) void fw_reduce_kernel(const float* __restrict_
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// conv2 forward form: warp-specialised unless MIA_FECONV_WS=0 (A/B runs, tools/bench_fe.py FE_AB=1)
+bool fe_ws() { const char* e = getenv("MIA_FECONV_WS"); return !(e && e[0] == '0'); }
+
 }  // namespace
 
 extern "C" int mia_fe_conv2_fwd(const void* y1, const float* scale, const float* shift, const void* w,
@@ -859,9 +1069,16 @@ extern "C" int mia_fe_conv2_fwd(const void* y1, const float* scale, const float*
     FeArgs a{reinterpret_cast<const bf16*>(y1) + (int64_t)c * w1 * 32, scale, shift, reinterpret_cast<const bf16*>(w),
              bias, reinterpret_cast<bf16*>(y2) + (int64_t)c * w2 * FE_N, nc, w1, w2, 0, (int)cdiv(w2, FE_BM),
              (int64_t)w2 * FE_N, (int64_t)w2 * FE_N};
-    const int grid = fe_grid(nc * a.nitem);
-    if (scale) feconv_kernel<32, 16, 2, true><<<grid, FE_NT, 0, s>>>(a);
-    else feconv_kernel<32, 16, 2, false><<<grid, FE_NT, 0, s>>>(a);
+    // warp-specialised (one 8-wave workgroup per CU); MIA_FECONV_WS=0 selects the two-workgroup form for A/B runs
+    if (fe_ws()) {
+      const int grid = fe_grid1(nc * a.nitem);
+      if (scale) feconv_ws_kernel<32, 16, 2, true><<<grid, FS_NT, 0, s>>>(a);
+      else feconv_ws_kernel<32, 16, 2, false><<<grid, FS_NT, 0, s>>>(a);
+    } else {
+      const int grid = fe_grid(nc * a.nitem);
+      if (scale) feconv_kernel<32, 16, 2, true><<<grid, FE_NT, 0, s>>>(a);
+      else feconv_kernel<32, 16, 2, false><<<grid, FE_NT, 0, s>>>(a);
+    }
     MIA_LAUNCH_CHECK("fe_conv2_fwd");
   }
   return 0;
@@ -881,6 +1098,7 @@ extern "C" int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, 
     FeArgs a{reinterpret_cast<const bf16*>(dy2) + (int64_t)c * w2 * 64, nullptr, nullptr,
              reinterpret_cast<const bf16*>(wpar), nullptr, reinterpret_cast<bf16*>(da1) + (int64_t)c * w1 * 32, nc,
              w2, wout, 7, (int)cdiv(wout, FE_BM), (int64_t)w1 * 32, (int64_t)w1 * 32};
+    // (the warp-specialised form measured no faster here: its stream side alone takes 0.77 ms, DESIGN round 6)
     feconv_kernel<64, 8, 1, false><<<fe_grid(nc * a.nitem), FE_NT, 0, as_stream(stream)>>>(a);
     MIA_LAUNCH_CHECK("fe_conv2_dgrad");
   }

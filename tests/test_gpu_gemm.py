@@ -689,6 +689,29 @@ def test_fe_conv2_fwd(cuda, n, w1, pre):
     assert rel(got, ref) < 5e-3
 
 
+@pytest.mark.parametrize("n,w1", [(2, 20001), (300, 600)])
+def test_fe_conv2_fwd_forms_bit_identical(cuda, monkeypatch, n, w1):
+    """The warp-specialised conv2 forward (default) and the two-workgroup form (MIA_FECONV_WS=0) run the same
+    MFMA sequence per output: bit-identical outputs, including a ragged last item and more items than CUs."""
+    w2 = (w1 - 16) // 2 + 1
+    g = torch.Generator().manual_seed(w1 + 7 * n)
+    y1 = torch.randn(n * w1, 32, generator=g).to(torch.bfloat16).to(cuda)
+    W = torch.randn(64, 32, 1, 16, generator=g) * 0.05
+    bias = torch.randn(64, generator=g).to(cuda)
+    sc = (torch.rand(32, generator=g) + 0.5).to(cuda)
+    sh = (torch.randn(32, generator=g) * 0.3).to(cuda)
+    wp = K.pack_weight(W.to(cuda), L.BF16, 0)
+    outs = []
+    for form in ("1", "0"):
+        monkeypatch.setenv("MIA_FECONV_WS", form)
+        out = torch.full((n * w2, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        K.fe_conv2_fwd(y1, sc, sh, wp, bias, out, n, w1, w2)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("n,w1", [(2, 20001), (3, 4112), (300, 601)])
 def test_fe_conv2_dgrad(cuda, n, w1):
     """Backward-data of the same conv (both output parities from one staged dY window) vs float64

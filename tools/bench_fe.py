@@ -1,5 +1,6 @@
 """Time the EnvNet frontend conv kernels at the bench shape (B=256, 5 s clips) in isolation.
     python tools/bench_fe.py"""
+import os
 import sys
 from pathlib import Path
 
@@ -49,12 +50,29 @@ flop = 2.0 * B * W2 * 64 * 512
 want = set(sys.argv[1:])
 
 
+def with_ws(fn, on):  # MIA_FECONV_WS A/B (read by the library per call)
+    def run():
+        os.environ["MIA_FECONV_WS"] = "1" if on else "0"
+        fn()
+    return run
+
+
+if os.environ.get("FE_AB"):  # warp-specialised conv2 fwd against the two-workgroup form, alternating
+    f = runs.pop("fe_conv2_fwd")
+    runs["fe_conv2_fwd"] = with_ws(f, False)
+    runs["fe_conv2_fwd_ws"] = with_ws(f, True)
+    byts["fe_conv2_fwd_ws"] = byts["fe_conv2_fwd"]
+    seq = [(k, runs[k]) for k in ["fe_conv2_fwd", "fe_conv2_fwd_ws"] * 3]
+else:
+    seq = list(runs.items())
+
+
 def digest(t):
     v = t.reshape(-1).view(torch.int32).to(torch.int64)
     return int((v * torch.arange(1, v.numel() + 1, device=v.device, dtype=torch.int64).remainder(65521)).sum()) & (2**64 - 1)
 
 
-for name, fn in runs.items():
+for name, fn in seq:
     if want and name not in want:
         continue
     for _ in range(3):
@@ -67,6 +85,6 @@ for name, fn in runs.items():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    out = {"fe_conv3_fwd": y3, "fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name)
+    out = {"fe_conv3_fwd": y3, "fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name.removesuffix("_ws"))
     dg = f"digest {digest(out):x}" if out is not None else ""
     print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s  {dg}", flush=True)
