@@ -11,6 +11,14 @@
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2_cvt __attribute__((ext_vector_type(2)));
+
+// two floats -> two bf16 (round to nearest even, as the (bf16) cast) packed lo | hi << 16: one v_cvt_pk_bf16_f32
+// (the two casts and the shift-or were four VALU instructions)
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_cvt{lo, hi}, bf16x2));
+}
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -217,8 +225,7 @@ __device__ __forceinline__ void store8(void* p, int dtype, int64_t off, const fl
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-      w[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      w[i] = pk_bf16(f[2 * i], f[2 * i + 1]);
     }
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + off) = make_uint4(w[0], w[1], w[2], w[3]);
   } else {

@@ -124,8 +124,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(W3Args g) {
         gv[j] = bnp[2][c] * (gv[j] - bnp[5][c] - (xv[j] - bnp[3][c]) * bnp[4][c] * bnp[6][c]);
         bs1[i] += gv[j];
       }
-      const bf16 lo = (bf16)gv[0], hi = (bf16)gv[1];
-      o[k] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      o[k] = pk_bf16(gv[0], gv[1]);
     }
     const int seg = it % g.nseg, rest = it / g.nseg;
     const int oy = rest % g.oh, b = rest / g.oh;

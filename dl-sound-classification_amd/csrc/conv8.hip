@@ -57,8 +57,7 @@ __device__ __forceinline__ u32x4 cook(u32x4 u, bool ok, const float* sc, const f
   for (int i = 0; i < 4; ++i) {
     const float lo = fmaxf(fmaf(__uint_as_float(u[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
     const float hi = fmaxf(fmaf(__uint_as_float(u[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
-    const bf16 bl = (bf16)lo, bh = (bf16)hi;
-    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+    w4[i] = pk_bf16(lo, hi);
   }
   return u32x4{w4[0], w4[1], w4[2], w4[3]};
 }
@@ -186,18 +185,16 @@ __global__ __launch_bounds__(C8_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) v
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int e = 8 * h + 2 * i;
-              const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
-              w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) |
-                      ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+              w4[i] = pk_bf16(v[e] + bv[e], v[e + 1] + bv[e + 1]);
               if constexpr (STATS) {
-                const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
+                const float d0 = __uint_as_float(w4[i] << 16) - bv[e], d1 = __uint_as_float(w4[i] & 0xffff0000u) - bv[e + 1];
                 s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
                 s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
               }
               if constexpr (RED) {
                 const uint32_t xw = bxr[tt][h][i];
                 const float xv[2] = {__uint_as_float(xw << 16), __uint_as_float(xw & 0xffff0000u)};
-                const float dv[2] = {(float)ylo, (float)yhi};
+                const float dv[2] = {__uint_as_float(w4[i] << 16), __uint_as_float(w4[i] & 0xffff0000u)};
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                   const int c = c0 + 16 * h + 2 * i + k;

@@ -75,16 +75,12 @@ __device__ __forceinline__ u32x4 fe_cook(u32x4 u, bool ok, bool pre, const float
   for (int i = 0; i < 4; ++i) {
     const float lo = fmaxf(fmaf(__uint_as_float(u[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
     const float hi = fmaxf(fmaf(__uint_as_float(u[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
-    const bf16 bl = (bf16)lo, bh = (bf16)hi;
-    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+    w4[i] = pk_bf16(lo, hi);
   }
   return u32x4{w4[0], w4[1], w4[2], w4[3]};
 }
 
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  const bf16 bl = (bf16)lo, bh = (bf16)hi;
-  return (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
-}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return pk_bf16(lo, hi); }
 
 #ifdef FE_STAMP
 __device__ unsigned long long g_fe_st[64 * 4 * 256 * 8];
@@ -538,8 +534,7 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
     return *reinterpret_cast<const f32x2*>(g.x + (int64_t)b * g.t + s0);
   };
   auto run = [&](int it, f32x2 xr) __attribute__((always_inline)) {
-    const bf16 lo = (bf16)xr[0], hi = (bf16)xr[1];
-    const uint32_t d = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    const uint32_t d = pk_bf16(xr[0], xr[1]);
     wave_sync();  // the previous item's fragment reads are done
     sg[lane] = d;
     if (lane >= 1) sg[96 + lane - 1] = d;
@@ -582,11 +577,10 @@ __global__ __launch_bounds__(256) void fe_conv1_kernel(F1Args g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int e = 8 * h + 2 * i;
-        const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
-        w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+        w4[i] = pk_bf16(v[e] + bv[e], v[e + 1] + bv[e + 1]);
         if constexpr (STATS) {
           if (op < g.w1) {
-            const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
+            const float d0 = __uint_as_float(w4[i] << 16) - bv[e], d1 = __uint_as_float(w4[i] & 0xffff0000u) - bv[e + 1];
             s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
             s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
           }
@@ -755,11 +749,10 @@ __global__ __launch_bounds__(256) void fe_conv3_kernel(F3Args g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int e = 8 * h + 2 * i;
-        const bf16 ylo = (bf16)(v[e] + bv[e]), yhi = (bf16)(v[e + 1] + bv[e + 1]);
-        w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, ylo) | ((uint32_t)__builtin_bit_cast(unsigned short, yhi) << 16);
+        w4[i] = pk_bf16(v[e] + bv[e], v[e + 1] + bv[e + 1]);
         if constexpr (STATS) {
           if (ox < g.ow) {
-            const float d0 = (float)ylo - bv[e], d1 = (float)yhi - bv[e + 1];
+            const float d0 = __uint_as_float(w4[i] << 16) - bv[e], d1 = __uint_as_float(w4[i] & 0xffff0000u) - bv[e + 1];
             s1[e] += d0; s2[e] = fmaf(d0, d0, s2[e]);
             s1[e + 1] += d1; s2[e + 1] = fmaf(d1, d1, s2[e + 1]);
           }
@@ -926,9 +919,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
             for (int i = 0; i < 4; ++i) {
               const float lo = fmaxf(fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
               const float hi = fmaxf(fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
-              const bf16 bl = (bf16)lo, bh = (bf16)hi;
-              w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) |
-                      ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+              w4[i] = pk_bf16(lo, hi);
             }
             v = u32x4{w4[0], w4[1], w4[2], w4[3]};
           }

@@ -119,9 +119,7 @@ __device__ __forceinline__ void load_chunk(const OpDev& o, int64_t off, int nval
   if constexpr (TT<T>::dt == MIA_BF16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-      v[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
-             ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      v[i] = pk_bf16(f[2 * i], f[2 * i + 1]);
     }
   } else {
 #pragma unroll
@@ -556,8 +554,7 @@ __device__ __forceinline__ u32x4 cook_raw(const RawChunk& r, bool ok, const floa
   uint32_t w4[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+    w4[i] = pk_bf16(f[2 * i], f[2 * i + 1]);
   }
   return u32x4{w4[0], w4[1], w4[2], w4[3]};
 }
@@ -1082,9 +1079,7 @@ __global__ __launch_bounds__(NT) void tapwgrad_kernel(TapWArgs g) {
           uint32_t w4[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bf16 lo = (bf16)f[2 * i], hi = (bf16)f[2 * i + 1];
-            w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
-                    ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+            w4[i] = pk_bf16(f[2 * i], f[2 * i + 1]);
           }
           v = u32x4{w4[0], w4[1], w4[2], w4[3]};
         }
@@ -1732,8 +1727,7 @@ __global__ __launch_bounds__(NT) void dgemm_kernel(DArgs g) {
       uint32_t w4[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const bf16 bl = (bf16)f[2 * q], bh = (bf16)f[2 * q + 1];
-        w4[q] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+        w4[q] = pk_bf16(f[2 * q], f[2 * q + 1]);
       }
       return make_uint4(w4[0], w4[1], w4[2], w4[3]);
     };

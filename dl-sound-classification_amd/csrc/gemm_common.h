@@ -112,8 +112,7 @@ static __device__ __forceinline__ void st16(void* p, int dtype, int64_t idx, con
     uint32_t w[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const bf16 lo = (bf16)o[2 * c], hi = (bf16)o[2 * c + 1];
-      w[c] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      w[c] = pk_bf16(o[2 * c], o[2 * c + 1]);
     }
     uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx);
     d[0] = make_uint4(w[0], w[1], w[2], w[3]);

@@ -261,9 +261,7 @@ __device__ __forceinline__ void dgelu4(f32x4& v, f32x4 u) {
 }
 
 __device__ __forceinline__ uint2 pack4(f32x4 v) {
-  const bf16 a = (bf16)v[0], b = (bf16)v[1], c = (bf16)v[2], d = (bf16)v[3];
-  return make_uint2((uint32_t)__builtin_bit_cast(unsigned short, a) | ((uint32_t)__builtin_bit_cast(unsigned short, b) << 16),
-                    (uint32_t)__builtin_bit_cast(unsigned short, c) | ((uint32_t)__builtin_bit_cast(unsigned short, d) << 16));
+  return make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
 }
 __device__ __forceinline__ f32x4 unpack4(uint2 u) {
   return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),

@@ -377,8 +377,7 @@ __global__ void ast_patches_kernel(const float* __restrict__ spec, int B, int Fm
       const float* src = spec + ((int64_t)b * Fm + gy * st + ky) * Tf + gx * st + kx;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16 lo = (bf16)src[2 * j], hi = (bf16)src[2 * j + 1];
-        w[j] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+        w[j] = pk_bf16(src[2 * j], src[2 * j + 1]);
       }
     }
     out[i] = uint4{w[0], w[1], w[2], w[3]};

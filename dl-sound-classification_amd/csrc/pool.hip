@@ -156,8 +156,7 @@ __global__ __launch_bounds__(NT) void pool_raw_stats_kernel(const bf16* __restri
     uint32_t o4[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bf16 lo = (bf16)bestraw[2 * i], hi = (bf16)bestraw[2 * i + 1];  // exact: bf16 inputs
-      o4[i] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+      o4[i] = pk_bf16(bestraw[2 * i], bestraw[2 * i + 1]);  // exact: bf16 inputs
     }
     *reinterpret_cast<uint4*>(win + aoff) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
   }
@@ -461,8 +460,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_oct_kernel(const float* 
           g[h] = a[i] * (gi - mb[i] - (xv - mu[i]) * is[i] * mg[i]);
           s1[i] += g[h];
         }
-        const bf16 lo = (bf16)g[0], hi = (bf16)g[1];
-        o4[q] = (uint32_t)__builtin_bit_cast(unsigned short, lo) | ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+        o4[q] = pk_bf16(g[0], g[1]);
       }
       *reinterpret_cast<uint4*>(dx + xoff + (int64_t)j * C) = uint4{o4[0], o4[1], o4[2], o4[3]};
     }
@@ -567,9 +565,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_run_kernel(const float* 
             g[h] = a[i] * (gi - mb[i] - (xv - mu[i]) * is[i] * mg[i]);
             s1[i] += g[h];
           }
-          const bf16 lo = (bf16)g[0], hi = (bf16)g[1];
-          o4[q] = (uint32_t)__builtin_bit_cast(unsigned short, lo) |
-                  ((uint32_t)__builtin_bit_cast(unsigned short, hi) << 16);
+          o4[q] = pk_bf16(g[0], g[1]);
         }
         *reinterpret_cast<uint4*>(dx + xoff[v] + (int64_t)j * C) = uint4{o4[0], o4[1], o4[2], o4[3]};
       }

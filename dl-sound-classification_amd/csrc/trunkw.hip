@@ -21,10 +21,7 @@ namespace {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t pk(float lo, float hi) {
-  const bf16 bl = (bf16)lo, bh = (bf16)hi;
-  return (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
-}
+__device__ __forceinline__ uint32_t pk(float lo, float hi) { return pk_bf16(lo, hi); }
 
 // out = bf16(relu(x * scale + shift)), 8 channels per thread
 __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const bf16* __restrict__ x, int64_t P, int C,

@@ -42,8 +42,7 @@ __device__ __forceinline__ u32x4 bn_relu_pack(u32x4 u, bool ok, const float* sc,
   for (int i = 0; i < 4; ++i) {
     const float lo = fmaxf(fmaf(__uint_as_float(u[i] << 16), sc[2 * i], sh[2 * i]), 0.f);
     const float hi = fmaxf(fmaf(__uint_as_float(u[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]), 0.f);
-    const bf16 bl = (bf16)lo, bh = (bf16)hi;
-    w4[i] = (uint32_t)__builtin_bit_cast(unsigned short, bl) | ((uint32_t)__builtin_bit_cast(unsigned short, bh) << 16);
+    w4[i] = pk_bf16(lo, hi);
   }
   return u32x4{w4[0], w4[1], w4[2], w4[3]};
 }
