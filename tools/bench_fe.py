@@ -85,6 +85,7 @@ for name, fn in seq:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    out = {"fe_conv3_fwd": y3, "fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1}.get(name.removesuffix("_ws"))
+    out = {"fe_conv3_fwd": y3, "fe_conv1_fwd": y1c, "fe_conv2_fwd": y2, "fe_conv2_dgrad": da1,
+           "fe_conv2_wgrad": dw}.get(name.removesuffix("_ws"))
     dg = f"digest {digest(out):x}" if out is not None else ""
     print(f"{name:16s} {ms:7.3f} ms  {byts[name] / ms / 1e6:7.1f} GB/s  {flop / ms / 1e9:7.1f} TF/s  {dg}", flush=True)
