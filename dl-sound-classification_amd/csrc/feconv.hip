@@ -284,7 +284,9 @@ __global__ __launch_bounds__(FE_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 // the window over.  The two roles meet on every SIMD (one compute + one feeder wave each), so the feeders'
 // VALU and load issue run under the compute waves' MFMAs instead of in a phase of their own.
 constexpr int FS_NT = 512;
-constexpr int FS_DEPTH = 3;  // raw window loads in flight per feeder thread (items k+1 .. k+3)
+#ifndef FS_DEPTH
+#define FS_DEPTH 3  // raw window loads in flight per feeder thread (items k+1 .. k+3)
+#endif
 #ifndef FS_FD
 #define FS_FD 4  // k-steps of B fragments in flight per compute wave
 #endif
@@ -456,28 +458,31 @@ __global__ __launch_bounds__(FS_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     stage(0, raw[0], rok[0]);
     lds_barrier();  // item 0's window in
     // iteration k: item k + FS_DEPTH's loads into the set item k used, item k + 1's window staged into half
-    // (k + 1) & 1 (its loads were issued FS_DEPTH - 1 items ago), barrier.  Unrolled by 6 = lcm(2, FS_DEPTH)
-    // so the register set and the LDS half are compile-time.
+    // (k + 1) & 1 (its loads were issued FS_DEPTH - 1 items ago), barrier.  Unrolled by 12 (a multiple of 2 and
+    // of FS_DEPTH) so the register set and the LDS half are compile-time.
+    static_assert(12 % FS_DEPTH == 0, "feeder unroll");
     auto iter = [&](auto KC, int k) __attribute__((always_inline)) {
-      constexpr int R = decltype(KC)::value;  // k % 6
+      constexpr int R = decltype(KC)::value;  // k % 12
       constexpr int SET = R % FS_DEPTH, NXT = (R + 1) % FS_DEPTH;
       load(k + FS_DEPTH, raw[SET], rok[SET]);
       if (k + 1 < nk) stage((R + 1) & 1, raw[NXT], rok[NXT]);
       lds_barrier();  // the staged window is in LDS
     };
+    // iterations k .. k + 11, stopping after the workgroup's last item
+    auto step = [&](auto KC, int k) __attribute__((always_inline)) {
+      const int kk = k + decltype(KC)::value;
+      if (kk < nk) iter(KC, kk);
+      return kk + 1 < nk;
+    };
 #pragma unroll 1
-    for (int k = 0; k < nk; k += 6) {
-      iter(std::integral_constant<int, 0>{}, k);
-      if (k + 1 >= nk) break;
-      iter(std::integral_constant<int, 1>{}, k + 1);
-      if (k + 2 >= nk) break;
-      iter(std::integral_constant<int, 2>{}, k + 2);
-      if (k + 3 >= nk) break;
-      iter(std::integral_constant<int, 3>{}, k + 3);
-      if (k + 4 >= nk) break;
-      iter(std::integral_constant<int, 4>{}, k + 4);
-      if (k + 5 >= nk) break;
-      iter(std::integral_constant<int, 5>{}, k + 5);
+    for (int k = 0; k < nk; k += 12) {
+      using std::integral_constant;
+      (void)(step(integral_constant<int, 0>{}, k) && step(integral_constant<int, 1>{}, k) &&
+             step(integral_constant<int, 2>{}, k) && step(integral_constant<int, 3>{}, k) &&
+             step(integral_constant<int, 4>{}, k) && step(integral_constant<int, 5>{}, k) &&
+             step(integral_constant<int, 6>{}, k) && step(integral_constant<int, 7>{}, k) &&
+             step(integral_constant<int, 8>{}, k) && step(integral_constant<int, 9>{}, k) &&
+             step(integral_constant<int, 10>{}, k) && step(integral_constant<int, 11>{}, k));
     }
   }
 }
@@ -1112,7 +1117,11 @@ extern "C" int mia_fe_conv2_dgrad(const void* dy2, const void* wpar, void* da1, 
              reinterpret_cast<const bf16*>(wpar), nullptr, reinterpret_cast<bf16*>(da1) + (int64_t)c * w1 * 32, nc,
              w2, wout, 7, (int)cdiv(wout, FE_BM), (int64_t)w1 * 32, (int64_t)w1 * 32};
     // (the warp-specialised form measured no faster here: its stream side alone takes 0.77 ms, DESIGN round 6)
+#ifdef FS_DGRAD  // A/B builds only
+    feconv_ws_kernel<64, 8, 1, false><<<fe_grid1(nc * a.nitem), FS_NT, 0, as_stream(stream)>>>(a);
+#else
     feconv_kernel<64, 8, 1, false><<<fe_grid(nc * a.nitem), FE_NT, 0, as_stream(stream)>>>(a);
+#endif
     MIA_LAUNCH_CHECK("fe_conv2_dgrad");
   }
   return 0;
