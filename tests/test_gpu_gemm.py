@@ -689,7 +689,7 @@ def test_fe_conv2_fwd(cuda, n, w1, pre):
     assert rel(got, ref) < 5e-3
 
 
-@pytest.mark.parametrize("n,w1", [(2, 20001), (300, 600)])
+@pytest.mark.parametrize("n,w1", [(1, 300), (2, 20001), (300, 600)])
 def test_fe_conv2_fwd_forms_bit_identical(cuda, monkeypatch, n, w1):
     """The warp-specialised conv2 forward (default) and the two-workgroup form (MIA_FECONV_WS=0) run the same
     MFMA sequence per output: bit-identical outputs, including a ragged last item and more items than CUs."""
