@@ -82,6 +82,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// LDS-only workgroup barrier: this wave's LDS operations complete, then s_barrier; the "memory" clobber keeps the
+// compiler from moving memory operations across it, and no vmcnt wait is implied (global loads / stores and LDS-DMA
+// stay in flight, unlike __syncthreads)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -291,10 +291,7 @@ constexpr int FS_NT = 512;
 #define FS_FD 4  // k-steps of B fragments in flight per compute wave
 #endif
 
-// LDS-only workgroup barrier: this wave's LDS operations complete, then s_barrier; the "memory" clobber keeps the
-// compiler from moving memory operations across it, and no vmcnt wait is implied (the feeders' window loads and
-// the compute waves' output stores stay in flight)
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// (lds_barrier, common.h: the feeders' window loads and the compute waves' output stores stay in flight across it)
 
 template <int CIN, int KW, int S, bool PRE>
 __global__ __launch_bounds__(FS_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void feconv_ws_kernel(FeArgs g) {
